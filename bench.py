@@ -1,0 +1,250 @@
+#!/usr/bin/env python3
+"""bench.py -- SpMV GFLOP/s + achieved HBM GB/s (fp64) on 1..8 MI355X.
+
+Workload (BASELINE.json configs[1], weak-scaled): every rank owns a block of
+10M rows x 16 nnz/row of a uniform random CSR whose column space is the
+whole matrix (N*10M columns): N=1 is the 10M x 10M config, N=8 is the
+80M x 80M row-partitioned config (configs[4]).  x is generated on rank 0 and
+replicated with an RCCL broadcast over xGMI (setup, untimed -- x is fixed
+across calls as in the reference driver, src/main.cpp:36-102); y slices are
+gathered with RCCL all_gather, timed separately ("collective_ms").
+
+A step = one y = A x over the rank's rows (device-resident x and y).  W
+untimed warm-up steps, then K steps bracketed by barrier +
+torch.cuda.synchronize(); the max over ranks is the step time.  The same K
+steps are timed with HIP events on the plan's stream (spmv_time): that
+per-launch duration feeds `roofline.achieved`.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4]
+                  [--formats auto,csr,ell,ss,hyb] [--no-cpu]
+
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
+
+CONFIGS = {
+    # name: (generator kwargs per rank, description)
+    "c2": (dict(kind="uniform", per_row=16), "uniform 10M x 10M, 16 nnz/row (per GPU)", 10_000_000),
+    "c3": (dict(kind="powerlaw", max_len=10000, alpha=2.0), "power-law 5M rows, 1-10k nnz/row", 5_000_000),
+    "c4": (dict(kind="banded", band_lo=-32, band_hi=31), "banded 20M rows, 64 diagonals", 20_000_000),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--rows", type=int, default=0, help="rows per GPU (default: the config's)")
+    ap.add_argument("--formats", default="auto,csr,ell,ss",
+                    help="first entry is the headline plan; the rest are reported alongside")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
+    ap.add_argument("--cpu-seconds", type=float, default=2.0)
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    import singlespmv_amd as sp
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE",
+              file=sys.stderr)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    distributed = world > 1
+    if distributed:
+        dist.init_process_group("nccl", device_id=dev)
+
+    gen_kw, desc, rows_default = CONFIGS[args.config]
+    rows = args.rows or rows_default
+    m_glob = rows * world
+    n_glob = m_glob
+    row0, row1 = rank * rows, (rank + 1) * rows
+
+    t0 = time.time()
+    kind = gen_kw["kind"]
+    spec = sp.gen_spec(kind, m_glob, n_glob, per_row=gen_kw.get("per_row", 16),
+                       max_len=gen_kw.get("max_len", 10000), alpha=gen_kw.get("alpha", 2.0),
+                       band_lo=gen_kw.get("band_lo", -32), band_hi=gen_kw.get("band_hi", 31),
+                       seed=42)
+    rp, col, val = sp.generate_csr(spec, row0, row1)
+    nnz_local = int(rp[-1])
+    t_gen = time.time() - t0
+
+    # x: generated once on rank 0, replicated by RCCL broadcast over xGMI
+    x = torch.empty(n_glob, dtype=torch.float64, device=dev)
+    if rank == 0:
+        x.copy_(torch.from_numpy(sp.generate_vector(n_glob, seed=43)))
+    t_bcast = 0.0
+    if distributed:
+        torch.cuda.synchronize()
+        dist.barrier()
+        tb = time.perf_counter()
+        dist.broadcast(x, src=0)
+        torch.cuda.synchronize()
+        t_bcast = time.perf_counter() - tb
+    y = torch.empty(rows, dtype=torch.float64, device=dev)
+
+    fmts = [f for f in args.formats.split(",") if f]
+    results = {}
+    headline = None
+    for fi, fmt in enumerate(fmts):
+        tp = time.time()
+        try:
+            plan = sp.Plan.from_csr(rows, n_glob, rp, col, val, fmt=fmt, device=local)
+        except sp.SpmvError as e:
+            results[fmt] = {"error": str(e)}
+            continue
+        t_plan = time.time() - tp
+        info = plan.info()
+        stream = torch.cuda.Stream(device=dev)
+        plan.set_stream(stream)
+        torch.cuda.synchronize()
+        # warm-up
+        if args.warmup:
+            plan.time(x, y, args.warmup)
+        torch.cuda.synchronize()
+        if distributed:
+            dist.barrier()
+        torch.cuda.synchronize()
+        tw = time.perf_counter()
+        ev_ms = plan.time(x, y, args.steps)  # K launches between HIP events
+        torch.cuda.synchronize()
+        if distributed:
+            dist.barrier()
+        wall = time.perf_counter() - tw
+        tmax = torch.tensor([wall, ev_ms], dtype=torch.float64, device=dev)
+        if distributed:
+            dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        wall_max, ev_max = float(tmax[0]), float(tmax[1])
+        launch_s = ev_ms / 1e3 / args.steps
+        flops_total = 2.0 * nnz_local * world * args.steps
+        r = {
+            "format": info["format"], "kernel": info["kernel"],
+            "gflops": flops_total / wall_max / 1e9,
+            "ms_per_step": wall_max / args.steps * 1e3,
+            "event_ms_per_launch": launch_s * 1e3,
+            "achieved_gbs": info["algo_bytes"] / launch_s / 1e9,
+            "algo_bytes": info["algo_bytes"], "stored_slots": info["stored_slots"],
+            "device_bytes": info["device_bytes"], "plan_build_s": round(t_plan, 3),
+            "n_kernels": info["n_kernels"],
+        }
+        for k in ("csr_lanes", "ss_sigma", "ell_width", "n_diags"):
+            if info[k]:
+                r[k] = info[k]
+        results[fmt] = r
+        if fi == 0:
+            headline = (plan, info, r)
+            y_head = y.clone()
+        else:
+            del plan
+        torch.cuda.synchronize()
+
+    if headline is None:
+        if rank == 0:
+            print(json.dumps({"error": "no plan could be built", "details": results}))
+        return 1
+    plan, info, r = headline
+
+    # y gather (RCCL all_gather over xGMI), timed separately from the kernel
+    coll_ms = None
+    if distributed:
+        yall = torch.empty(rows * world, dtype=torch.float64, device=dev)
+        for _ in range(3):
+            dist.all_gather_into_tensor(yall, y_head)
+        torch.cuda.synchronize()
+        dist.barrier()
+        tc = time.perf_counter()
+        reps = 10
+        for _ in range(reps):
+            dist.all_gather_into_tensor(yall, y_head)
+        torch.cuda.synchronize()
+        coll_ms = (time.perf_counter() - tc) / reps * 1e3
+
+    # CPU baseline: the oracle's restatement of opt_crs SpMV (OpenMP, all host
+    # cores of this rank's affinity), reference timing method, rank 0 at N=1
+    cpu = None
+    max_rel = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        import oracle
+        cores = len(os.sched_getaffinity(0))
+        nthreads = min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)))
+        t_cpu, loop, y_cpu = oracle.csr_time(rp, col, val, x.cpu().numpy(), nthreads=nthreads,
+                                             min_seconds=args.cpu_seconds, ntry=3)
+        ygpu = y_head.cpu().numpy()
+        max_rel = float(np.max(np.abs(ygpu - y_cpu) / np.maximum(np.abs(y_cpu), 1e-300)))
+        cpu = {"value": 2.0 * nnz_local / t_cpu / 1e9, "unit": "GFLOP/s", "cores": nthreads,
+               "kind": "port",
+               "sample": f"full {rows}-row matrix, oracle opt_crs restatement (OpenMP static), "
+                         f"{loop} calls x 3 trials after a {args.cpu_seconds:.0f} s doubling warm-up, "
+                         f"min mean per call",
+               "ms_per_call": t_cpu * 1e3}
+
+    achieved = r["achieved_gbs"]
+    out = {
+        "metric": "SpMV GFLOP/s (fp64) + achieved HBM GB/s",
+        "value": r["gflops"],
+        "unit": "GFLOP/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": r["ms_per_step"],
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (seeded generator, seed 42; x seed 43)",
+        "config": {"workload": f"{args.config}: {desc}", "rows_per_gpu": rows,
+                   "m": m_glob, "n": n_glob, "nnz_per_gpu": nnz_local,
+                   "format": r["format"], "kernel": r["kernel"],
+                   "parallelism": f"row-partition x{world}, x replicated (RCCL broadcast)"},
+        "achieved_gbs": achieved,
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "kernel": r["kernel"], "algo_bytes_per_launch": r["algo_bytes"],
+                     "launch_ms": r["event_ms_per_launch"]},
+        "cpu_baseline": cpu,
+        "formats": results,
+        "gen_s": round(t_gen, 2),
+        "x_broadcast_ms": round(t_bcast * 1e3, 3) if distributed else None,
+        "collective_ms": coll_ms,
+        "max_rel_err_vs_cpu": max_rel,
+    }
+    traffic_file = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(traffic_file):
+        try:
+            t = json.load(open(traffic_file))
+            key = f"{args.config}:{rows}:{r['kernel']}"
+            if key in t:
+                out["roofline"]["traffic"] = t[key]
+        except Exception:
+            pass
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if distributed:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,54 @@
+/*
+ * opt_hip.h -- drop-in format plugin for the reference's opt_* dispatch
+ * surface (reference src/opt.h:1-28): the same OptimizeProblem / SpMV pair
+ * every plugin exports (e.g. src/opt_crs.h:15-18, src/opt_cusparse.h:33-37),
+ * backed by libspmv_hip.so on an MI355X.
+ *
+ *   void OptimizeProblem(const SpMat&, const Vec&, SpMatOpt&, VecOpt&);
+ *       mangled _Z15OptimizeProblemRK5SpMatRK3VecR8SpMatOptR6VecOpt
+ *   extern "C" void SpMV(const SpMatOpt&, const VecOpt&, Vec&);
+ *
+ * Format: the first of -DOPT_HIP_{CRS,ELL,SS,DIA,HYB} that is defined
+ * (default AUTO); the environment variable SPMV_HIP_FORMAT
+ * (crs|ell|ss|dia|hyb|auto) overrides it at run time.
+ *
+ * x handling follows the reference: x_opt.val aliases the caller's x
+ * (src/opt_crs.cpp:11-12) and SpMV uploads it on every call the way
+ * opt_cusparse does (src/opt_cusparse.cpp:72).  SPMV_HIP_X_RESIDENT=1 uploads
+ * x only on the first call (the reference driver never changes x,
+ * src/main.cpp:36-102).  y is downloaded on every call (opt_cusparse.cpp:82).
+ *
+ * Errors: the signatures are void, so a failure prints spmv_last_error() and
+ * exits, as CUDA_SAFE_CALL does in the reference (src/util.h:48-55).
+ */
+#ifndef OPT_HIP_H
+#define OPT_HIP_H
+
+#ifndef OPT_HIP_USE_REFERENCE_TYPES
+#include "spmv_util.h"
+#endif
+#include "spmv_hip.h"
+
+struct SpMatOpt {
+    int nRow;
+    int nCol;
+    int nNnz;
+    spmv_plan_t plan;
+    int format;       /* resolved spmv_format_t */
+    double *d_x;      /* device copy of x (owned by the plan's allocator) */
+    int x_uploaded;
+};
+
+struct VecOpt {
+    int size;
+    double *val;
+};
+
+void OptimizeProblem(const SpMat &A, const Vec &x, SpMatOpt &A_opt, VecOpt &x_opt);
+extern "C" {
+void SpMV(const SpMatOpt &A, const VecOpt &x, Vec &y);
+/* (new) release the plan -- the reference never frees its SpMatOpt */
+void SpMVRelease(SpMatOpt &A);
+}
+
+#endif /* OPT_HIP_H */

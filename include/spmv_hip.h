@@ -1,0 +1,210 @@
+/*
+ * spmv_hip.h -- C-ABI of the MI355X-native fp64 SpMV engine (libspmv_hip.so).
+ *
+ * This is the drop-in boundary for the reference's `opt_*` format-dispatch
+ * surface (hir0shim/singleSpMV).  Plain C types only: pointers, sizes, int
+ * status codes.  No exit(), no torch types, no C++ in the signatures.
+ *
+ * Reference interfaces each entry point replaces (paths relative to the
+ * reference repository):
+ *
+ *   spmv_plan_create_coo   OptimizeProblem(const SpMat&, const Vec&, SpMatOpt&,
+ *                          VecOpt&) of every plugin, e.g. src/opt_crs.h:15,
+ *                          src/opt_ell.h:16, src/opt_ss.h:35, src/opt_dia.h:16,
+ *                          src/opt_cusparse.h:33; SpMat is src/util.h:7-19.
+ *   spmv_plan_create_csr*  opt_crs SpMatOpt {ptr, idx, val} (src/opt_crs.h:3-9)
+ *                          and the device CSR of src/opt_cusparse.cpp:36-42.
+ *   spmv_execute           extern "C" SpMV(const SpMatOpt&, const VecOpt&,
+ *                          Vec&) (e.g. src/opt_crs.h:16-18); with host x / host
+ *                          y it reproduces src/opt_cusparse.cpp:72-82 (H2D x,
+ *                          y = 1*A*x + 0*y, D2H y).
+ *   spmv_plan_destroy      (the reference never frees; no counterpart)
+ *   spmv_load_mtx          LoadSparseMatrix (src/util.cpp:30-66)
+ *   spmv_rand_vector       srand + CreateRandomVector (src/main.cpp:18,
+ *                          src/util.cpp:92-102)
+ *   spmv_verify_coo        VerifyResult (src/util.cpp:67-83)
+ *   spmv_gen_*             (new) seeded synthetic matrices for the BASELINE
+ *                          configs, generated in memory instead of .mtx text
+ *   spmv_partition_rows    (new) nnz-balanced row ranges for multi-GPU
+ *
+ * Semantics shared by every format (β = 0): spmv_execute overwrites every
+ * entry of y (src/opt_crs.cpp:68; src/opt_ell.cpp:78; src/opt_dia.cpp:82) and
+ * is idempotent -- repeated calls give identical y (the two-call verification
+ * of src/main.cpp:41-55).  Host input arrays are borrowed read-only during
+ * plan creation and never mutated (unlike the CSR5 handle, which transposes
+ * the caller's arrays in place, CSR5_cuda/anonymouslib_cuda.h:203-204).
+ *
+ * Threading: thread-compatible.  One plan per thread; a plan may be used from
+ * any thread but not concurrently.
+ */
+#ifndef SPMV_HIP_H
+#define SPMV_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SPMV_HIP_API_VERSION 1
+
+/* ---- status codes -------------------------------------------------------- */
+typedef enum spmv_status {
+    SPMV_SUCCESS = 0,
+    SPMV_ERROR_INVALID_VALUE = 1,  /* bad argument / inconsistent arrays    */
+    SPMV_ERROR_NOT_SUPPORTED = 2,  /* format cannot hold this matrix        */
+    SPMV_ERROR_OUT_OF_MEMORY = 3,  /* host or device allocation failed      */
+    SPMV_ERROR_HIP = 4,            /* a HIP runtime call failed             */
+    SPMV_ERROR_IO = 5,             /* file missing / unparsable             */
+    SPMV_ERROR_NO_DEVICE = 6       /* no usable gfx950 device               */
+} spmv_status_t;
+
+/* ---- storage formats (the reference's -DOPT_<FMT> plugins) --------------- */
+typedef enum spmv_format {
+    SPMV_FORMAT_AUTO = 0, /* chosen from the row-length histogram             */
+    SPMV_FORMAT_CSR = 1,  /* opt_crs   (src/opt_crs.cpp)                        */
+    SPMV_FORMAT_ELL = 2,  /* opt_ell   (src/opt_ell.cpp), device: sliced ELL    */
+    SPMV_FORMAT_SS = 3,   /* opt_ss / CSR5: segmented sum over 64 x sigma tiles */
+    SPMV_FORMAT_DIA = 4,  /* opt_dia   (src/opt_dia.cpp), device: row-indexed   */
+    SPMV_FORMAT_HYB = 5   /* ELL(K) + CSR overflow (BASELINE config 3)          */
+} spmv_format_t;
+
+typedef struct spmv_plan_s *spmv_plan_t;
+
+typedef struct spmv_options {
+    int32_t format;     /* spmv_format_t                                      */
+    int32_t device;     /* HIP device ordinal; -1 = the calling thread's current */
+    int32_t csr_lanes;  /* CSR: lanes per row 1..64 (power of two), 0 = auto   */
+    int32_t ell_width;  /* HYB: ELL width K, 0 = auto (row-length histogram)   */
+    int32_t ss_sigma;   /* SS: nnz per lane per tile, 0 = auto                 */
+    int32_t dia_max_diags; /* DIA: refuse beyond this many diagonals (0 = 1024) */
+    double dia_max_fill;   /* DIA: refuse when stored/nnz exceeds this (0 = 3) */
+    int32_t reserved[8];
+} spmv_options_t;
+
+/* Fill `opt` with defaults (AUTO format, current device, auto tuning). */
+void spmv_options_default(spmv_options_t *opt);
+
+/* Plan from a host sorted COO (the reference SpMat, src/util.h:7-19).
+ * Rows must be sorted ascending (LoadSparseMatrix guarantees it); columns
+ * within a row may be in any order, duplicates are summed. */
+int spmv_plan_create_coo(int32_t m, int32_t n, int32_t nnz, const int32_t *row_idx,
+                         const int32_t *col_idx, const double *val,
+                         const spmv_options_t *opt, spmv_plan_t *plan);
+
+/* Plan from a host CSR with 64-bit row pointers (nnz may exceed 2^31). */
+int spmv_plan_create_csr(int64_t m, int64_t n, int64_t nnz, const int64_t *row_ptr,
+                         const int32_t *col_idx, const double *val,
+                         const spmv_options_t *opt, spmv_plan_t *plan);
+
+/* Plan from a host CSR with 32-bit row pointers (opt_crs SpMatOpt layout). */
+int spmv_plan_create_csr32(int32_t m, int32_t n, int32_t nnz, const int32_t *row_ptr,
+                           const int32_t *col_idx, const double *val,
+                           const spmv_options_t *opt, spmv_plan_t *plan);
+
+int spmv_plan_destroy(spmv_plan_t plan);
+
+/* ---- execution ----------------------------------------------------------- */
+#define SPMV_X_DEVICE 0x1u /* x is a device pointer (else host: H2D per call) */
+#define SPMV_Y_DEVICE 0x2u /* y is a device pointer (else host: D2H per call) */
+#define SPMV_ASYNC 0x4u    /* device x and y: return without synchronising    */
+#define SPMV_X_STAGED 0x8u /* re-use the host x uploaded by the previous call
+                              (x may be NULL); error if none was staged       */
+
+/* y = A * x.  x holds n doubles, y holds m doubles. */
+int spmv_execute(spmv_plan_t plan, const double *x, double *y, uint32_t flags);
+
+/* Kernels are launched on this stream (a hipStream_t; NULL = null stream). */
+int spmv_set_stream(spmv_plan_t plan, void *hip_stream);
+
+/* Bench helper: `iters` back-to-back executes (device x, device y) between two
+ * hipEvents recorded on the plan's stream; *ms = elapsed milliseconds total. */
+int spmv_time(spmv_plan_t plan, const double *x_dev, double *y_dev, int32_t iters,
+              double *ms);
+
+typedef struct spmv_plan_info {
+    int32_t format;          /* resolved spmv_format_t                         */
+    int32_t device;
+    int64_t m, n, nnz;
+    int64_t stored_slots;    /* ELL/HYB/DIA slots incl. padding; CSR/SS = nnz   */
+    int64_t device_bytes;    /* device memory held by the plan                 */
+    int64_t algo_bytes;      /* compulsory bytes per execute (roofline model)  */
+    int32_t row_ptr_bytes;   /* 4 or 8                                         */
+    int32_t csr_lanes;       /* CSR / HYB overflow                             */
+    int32_t ell_width;       /* ELL: max slice width; HYB: K                   */
+    int32_t ss_sigma;
+    int32_t n_diags;         /* DIA                                            */
+    int32_t n_kernels;       /* launches per execute                           */
+    int64_t overflow_nnz;    /* HYB: entries outside the ELL part              */
+    int64_t empty_rows;
+    char kernel[64];         /* name of the dominant kernel                    */
+} spmv_plan_info_t;
+
+int spmv_plan_info(spmv_plan_t plan, spmv_plan_info_t *info);
+
+const char *spmv_status_string(int status);
+/* Detail of the last failure on the calling thread ("" if none). */
+const char *spmv_last_error(void);
+
+/* ---- host utilities ------------------------------------------------------ */
+
+/* LoadSparseMatrix semantics (src/util.cpp:30-66): skip leading '%' lines,
+ * header "M N L", exactly L triplets, 1->0 based, stable row-major sort,
+ * duplicates kept.  Arrays are malloc'd; release with spmv_free_host. */
+int spmv_load_mtx(const char *path, int32_t *m, int32_t *n, int32_t *nnz,
+                  int32_t **row_idx, int32_t **col_idx, double **val);
+void spmv_free_host(void *p);
+
+/* glibc srand(seed) then out[i] = rand()/RAND_MAX -- CreateRandomVector
+ * (src/util.cpp:92-102).  Consecutive calls continue the rand() stream. */
+void spmv_srand(uint32_t seed);
+void spmv_rand_vector(int32_t n, double *out);
+
+/* VerifyResult (src/util.cpp:67-83): returns -1 if every row passes, else the
+ * first failing row (abs_err > 1e-6 AND rel_err > 1e-6). */
+int64_t spmv_verify_coo(int32_t m, int32_t nnz, const int32_t *row_idx,
+                        const int32_t *col_idx, const double *val,
+                        const double *x, const double *y);
+
+/* COO (sorted rows) -> CSR, the linear scan of src/opt_crs.cpp:26-33. */
+int spmv_coo_to_csr(int32_t m, int64_t nnz, const int32_t *row_idx, int64_t *row_ptr);
+
+/* ---- synthetic matrices (BASELINE configs 2-5) ---------------------------- */
+typedef enum spmv_gen_kind {
+    SPMV_GEN_UNIFORM = 1,  /* `per_row` nnz per row, columns uniform on [0,n)   */
+    SPMV_GEN_POWERLAW = 2, /* row length ~ P(k) ∝ k^-alpha on [1, max_len]      */
+    SPMV_GEN_BANDED = 3    /* diagonals band_lo..band_hi (col - row), all present */
+} spmv_gen_kind_t;
+
+typedef struct spmv_gen_spec {
+    int32_t kind;        /* spmv_gen_kind_t                                  */
+    int32_t per_row;     /* UNIFORM                                          */
+    int64_t m, n;        /* global shape                                     */
+    int32_t max_len;     /* POWERLAW upper bound (10000 for config 3)        */
+    double alpha;        /* POWERLAW exponent (2.0)                          */
+    int32_t band_lo;     /* BANDED lowest offset  (-32 for config 4)         */
+    int32_t band_hi;     /* BANDED highest offset (+31 for config 4)         */
+    int32_t integer_values; /* 1: values in {0..9} (bitwise-exact sums)      */
+    uint64_t seed;
+} spmv_gen_spec_t;
+
+/* Number of nonzeros of global rows [row_begin, row_end). */
+int spmv_gen_count(const spmv_gen_spec_t *spec, int64_t row_begin, int64_t row_end,
+                   int64_t *nnz);
+/* Fill the CSR of rows [row_begin, row_end): row_ptr has (rows+1) entries and
+ * starts at 0; columns are global, sorted within each row. */
+int spmv_gen_fill(const spmv_gen_spec_t *spec, int64_t row_begin, int64_t row_end,
+                  int64_t *row_ptr, int32_t *col_idx, double *val);
+/* x[i] for global indices [begin, begin+count): U[0,1) (or {0..9}). */
+int spmv_gen_vector(uint64_t seed, int32_t integer_values, int64_t begin,
+                    int64_t count, double *out);
+
+/* nnz-balanced cut rows: cuts[k] = first row r with row_ptr[r] >= k*nnz/parts
+ * (cuts[0] = 0, cuts[parts] = m). */
+int spmv_partition_rows(const int64_t *row_ptr, int64_t m, int32_t parts, int64_t *cuts);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SPMV_HIP_H */

@@ -1,0 +1,407 @@
+/*
+ * oracle.c -- CPU restatement of the reference singleSpMV hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY (see oracle.h).  Built with -ffp-contract=off so
+ * every `acc += a*b` is a rounded multiply then a rounded add, exactly the
+ * arithmetic of the reference source as written.
+ */
+#define _GNU_SOURCE
+#include "oracle.h"
+
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/time.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+void orc_free(void *p) { free(p); }
+
+/* ---------------------------------------------------------------------- */
+/* LoadSparseMatrix -- src/util.cpp:30-66                                  */
+/* ---------------------------------------------------------------------- */
+
+typedef struct {
+    int row, col;
+    double val;
+    int64_t ord; /* input position: makes the sort deterministic for dups */
+} orc_elem;
+
+static int orc_elem_cmp(const void *a, const void *b) {
+    const orc_elem *x = (const orc_elem *)a, *y = (const orc_elem *)b;
+    /* Element::operator< (src/util.h:35-38): row, then col */
+    if (x->row != y->row) return x->row < y->row ? -1 : 1;
+    if (x->col != y->col) return x->col < y->col ? -1 : 1;
+    return x->ord < y->ord ? -1 : (x->ord > y->ord);
+}
+
+int orc_load_mtx(const char *path, int *m, int *n, int *nnz, int **row_idx,
+                 int **col_idx, double **val) {
+    FILE *f = fopen(path, "r");
+    if (!f) return -1; /* util.cpp:32-35 prints "File not Found" and exits */
+    char *line = NULL;
+    size_t cap = 0;
+    ssize_t len;
+    /* util.cpp:37-39: do { getline } while (line[0] == '%') */
+    do {
+        len = getline(&line, &cap, f);
+        if (len < 0) { free(line); fclose(f); return -2; }
+    } while (line[0] == '%');
+    int M, N, L;
+    if (sscanf(line, "%d %d %d", &M, &N, &L) != 3 || L < 0) {
+        free(line); fclose(f); return -2;
+    }
+    free(line);
+    orc_elem *e = (orc_elem *)malloc(sizeof(orc_elem) * (size_t)(L > 0 ? L : 1));
+    /* util.cpp:44-50: exactly L whitespace-separated triplets, 1 -> 0 based */
+    for (int i = 0; i < L; i++) {
+        int r, c;
+        double v;
+        if (fscanf(f, "%d %d %lf", &r, &c, &v) != 3) {
+            free(e); fclose(f); return -2;
+        }
+        e[i].row = r - 1;
+        e[i].col = c - 1;
+        e[i].val = v;
+        e[i].ord = i;
+    }
+    fclose(f);
+    /* util.cpp:51: std::sort by (row, col) */
+    qsort(e, (size_t)L, sizeof(orc_elem), orc_elem_cmp);
+    int *ri = (int *)malloc(sizeof(int) * (size_t)(L > 0 ? L : 1));
+    int *ci = (int *)malloc(sizeof(int) * (size_t)(L > 0 ? L : 1));
+    double *vv = (double *)malloc(sizeof(double) * (size_t)(L > 0 ? L : 1));
+    for (int i = 0; i < L; i++) {
+        ri[i] = e[i].row;
+        ci[i] = e[i].col;
+        vv[i] = e[i].val;
+    }
+    free(e);
+    *m = M; *n = N; *nnz = L;
+    *row_idx = ri; *col_idx = ci; *val = vv;
+    return 0;
+}
+
+/* srand(3) (src/main.cpp:18) + CreateRandomVector (src/util.cpp:92-102) */
+void orc_srand(unsigned seed) { srand(seed); }
+void orc_rand_fill(int n, double *out) {
+    for (int i = 0; i < n; i++) out[i] = (double)rand() / RAND_MAX;
+}
+
+/* ---------------------------------------------------------------------- */
+/* VerifyResult -- src/util.cpp:67-83                                      */
+/* ---------------------------------------------------------------------- */
+
+static int orc_row_fails(double res, double y) {
+    double rel = fabs(fabs(res - y) / res);
+    double abs_err = fabs(res - y);
+    const double EPS = 1e-6;
+    return abs_err > EPS && rel > EPS; /* NaN rel (0/0) never fails */
+}
+
+int64_t orc_verify(int m, int64_t nnz, const int *row_idx, const int *col_idx,
+                   const double *val, const double *x, const double *y,
+                   double *ref_out) {
+    double *res = (double *)calloc((size_t)(m > 0 ? m : 1), sizeof(double));
+    for (int64_t i = 0; i < nnz; i++) res[row_idx[i]] += val[i] * x[col_idx[i]];
+    int64_t bad = -1;
+    for (int i = 0; i < m; i++) {
+        if (orc_row_fails(res[i], y[i])) { bad = i; break; }
+    }
+    if (ref_out) memcpy(ref_out, res, sizeof(double) * (size_t)m);
+    free(res);
+    return bad;
+}
+
+int64_t orc_verify_csr(int64_t m, const int64_t *row_ptr, const int *col_idx,
+                       const double *val, const double *x, const double *y) {
+    int64_t first = INT64_MAX;
+#pragma omp parallel for schedule(static) reduction(min : first)
+    for (int64_t i = 0; i < m; i++) {
+        double res = 0;
+        for (int64_t j = row_ptr[i]; j < row_ptr[i + 1]; j++) res += val[j] * x[col_idx[j]];
+        if (orc_row_fails(res, y[i]) && i < first) first = i;
+    }
+    return first == INT64_MAX ? -1 : first;
+}
+
+/* ---------------------------------------------------------------------- */
+/* opt_crs -- src/opt_crs.cpp                                              */
+/* ---------------------------------------------------------------------- */
+
+void orc_coo_to_csr(int m, int64_t nnz, const int *row_idx, const int *col_idx,
+                    const double *val, int64_t *ptr, int *idx, double *csr_val) {
+    /* src/opt_crs.cpp:26-33 */
+    int64_t p = 0;
+    for (int64_t i = 0; i < nnz; i++) {
+        int r = row_idx[i];
+        idx[i] = col_idx[i];
+        csr_val[i] = val[i];
+        while (p <= r) ptr[p++] = i;
+    }
+    while (p <= m) ptr[p++] = nnz;
+}
+
+void orc_csr_spmv(int64_t m, const int64_t *ptr, const int *idx,
+                  const double *val, const double *x, double *y, int nthreads) {
+#ifdef _OPENMP
+    if (nthreads <= 0) nthreads = omp_get_max_threads();
+#else
+    (void)nthreads;
+#endif
+    /* src/opt_crs.cpp:57-69: omp parallel for (static), sequential row sum */
+#pragma omp parallel for schedule(static) num_threads(nthreads)
+    for (int64_t i = 0; i < m; i++) {
+        double t = 0;
+        for (int64_t j = ptr[i]; j < ptr[i + 1]; j++) {
+            double v = val[j] * x[idx[j]];
+            t += v;
+        }
+        y[i] = t;
+    }
+}
+
+static double orc_now(void) {
+    struct timeval tv;
+    gettimeofday(&tv, NULL);
+    return tv.tv_sec + tv.tv_usec * 1e-6; /* GetTimeBySec, util.cpp:21-25 */
+}
+
+double orc_csr_time(int64_t m, const int64_t *ptr, const int *idx,
+                    const double *val, const double *x, double *y,
+                    int nthreads, double min_seconds, int ntry, int *loop_out) {
+    /* src/main.cpp:58-71: warm-up, doubling loop until >= 1 s */
+    int loop = 1;
+    double t0 = orc_now();
+    do {
+        for (int i = 0; i < loop; i++) orc_csr_spmv(m, ptr, idx, val, x, y, nthreads);
+        loop *= 2;
+    } while (orc_now() - t0 < min_seconds);
+    /* src/main.cpp:79-102: ntry trials, min of mean per call */
+    double best = 1e300;
+    for (int t = 0; t < ntry; t++) {
+        double s = orc_now();
+        for (int i = 0; i < loop; i++) orc_csr_spmv(m, ptr, idx, val, x, y, nthreads);
+        double e = (orc_now() - s) / loop;
+        if (e < best) best = e;
+    }
+    if (loop_out) *loop_out = loop;
+    return best;
+}
+
+int orc_max_threads(void) {
+#ifdef _OPENMP
+    return omp_get_max_threads();
+#else
+    return 1;
+#endif
+}
+
+/* ---------------------------------------------------------------------- */
+/* opt_ell -- src/opt_ell.cpp                                              */
+/* ---------------------------------------------------------------------- */
+
+int orc_ell_width(int m, int64_t nnz, const int *row_idx) {
+    /* src/opt_ell.cpp:28-31: K = max row length */
+    int *cnt = (int *)calloc((size_t)(m > 0 ? m : 1), sizeof(int));
+    for (int64_t i = 0; i < nnz; i++) cnt[row_idx[i]]++;
+    int K = 0;
+    for (int i = 0; i < m; i++) if (cnt[i] > K) K = cnt[i];
+    free(cnt);
+    return K;
+}
+
+void orc_ell_build(int m, int64_t nnz, const int *row_idx, const int *col_idx,
+                   const double *val, int K, int *ell_col, double *ell_val) {
+    int *ptr = (int *)calloc((size_t)(m > 0 ? m : 1), sizeof(int));
+    /* src/opt_ell.cpp:40-45: fill in COO order */
+    for (int64_t i = 0; i < nnz; i++) {
+        int r = row_idx[i];
+        ell_col[(int64_t)r * K + ptr[r]] = col_idx[i];
+        ell_val[(int64_t)r * K + ptr[r]] = val[i];
+        ptr[r]++;
+    }
+    /* src/opt_ell.cpp:46-52: padding slot s -> col = s, val = 0 */
+    for (int i = 0; i < m; i++) {
+        while (ptr[i] < K) {
+            ell_col[(int64_t)i * K + ptr[i]] = ptr[i];
+            ell_val[(int64_t)i * K + ptr[i]] = 0;
+            ptr[i]++;
+        }
+    }
+    free(ptr);
+}
+
+void orc_ell_spmv(int m, int K, const int *ell_col, const double *ell_val,
+                  const double *x, double *y) {
+    /* src/opt_ell.cpp:76-88 */
+#pragma omp parallel for schedule(static)
+    for (int i = 0; i < m; i++) y[i] = 0;
+#pragma omp parallel for schedule(static)
+    for (int r = 0; r < m; r++) {
+        for (int i = 0; i < K; i++) {
+            int col = ell_col[(int64_t)r * K + i];
+            double lv = x[col];
+            double rv = ell_val[(int64_t)r * K + i];
+            y[r] += lv * rv;
+        }
+    }
+}
+
+/* ---------------------------------------------------------------------- */
+/* opt_dia -- src/opt_dia.cpp                                              */
+/* ---------------------------------------------------------------------- */
+
+int orc_dia_count(int m, int n, int64_t nnz, const int *row_idx,
+                  const int *col_idx, int *ioff) {
+    /* src/opt_dia.cpp:22-45 */
+    int64_t N = (int64_t)m + n - 1;
+    int offset = m - 1;
+    unsigned char *occ = (unsigned char *)calloc((size_t)(N > 0 ? N : 1), 1);
+    for (int64_t i = 0; i < nnz; i++) occ[col_idx[i] - row_idx[i] + offset] = 1;
+    int nDiag = 0;
+    for (int64_t d = 0; d < N; d++) {
+        if (occ[d]) {
+            if (ioff) ioff[nDiag] = (int)d;
+            nDiag++;
+        }
+    }
+    free(occ);
+    return nDiag;
+}
+
+void orc_dia_build(int m, int n, int64_t nnz, const int *row_idx,
+                   const int *col_idx, const double *val, int nDiag,
+                   const int *ioff, double *diag) {
+    int64_t N = (int64_t)m + n - 1;
+    int offset = m - 1;
+    int *rev = (int *)malloc(sizeof(int) * (size_t)(N > 0 ? N : 1));
+    for (int64_t d = 0; d < N; d++) rev[d] = -1;
+    for (int p = 0; p < nDiag; p++) rev[ioff[p]] = p;
+    /* src/opt_dia.cpp:47-51: zero filled, n doubles per diagonal */
+    memset(diag, 0, sizeof(double) * (size_t)nDiag * (size_t)n);
+    /* src/opt_dia.cpp:52-56: plain store -> last duplicate wins */
+    for (int64_t i = 0; i < nnz; i++) {
+        int d = col_idx[i] - row_idx[i] + offset;
+        diag[(int64_t)rev[d] * n + col_idx[i]] = val[i];
+    }
+    free(rev);
+}
+
+void orc_dia_spmv(int m, int n, int nDiag, const int *ioff, const double *diag,
+                  const double *x, double *y) {
+    /* src/opt_dia.cpp:81-93 (the per-call tmp[] leak at :80 is not restated) */
+    int offset = m - 1;
+    for (int i = 0; i < m; i++) y[i] = 0;
+    for (int i = 0; i < nDiag; i++) {
+        for (int col = 0; col < n; col++) {
+            int row = col + offset - ioff[i];
+            if (row < 0 || row >= m) continue;
+            double lv = diag[(int64_t)i * n + col];
+            double rv = x[col];
+            y[row] += lv * rv;
+        }
+    }
+}
+
+/* ---------------------------------------------------------------------- */
+/* opt_ss -- src/opt_ss.cpp                                                */
+/* ---------------------------------------------------------------------- */
+
+/* Mul (src/opt_ss.cpp:225-239): buf[p] = val[p] * x[col[p]], padding -> 0 */
+static double *orc_ss_mul(int64_t nnz, int64_t H, int W, const int *col_idx,
+                          const double *val, const double *x) {
+    double *buf = (double *)malloc(sizeof(double) * (size_t)(H * W > 0 ? H * W : 1));
+    for (int64_t p = 0; p < H * W; p++) {
+        if (p < nnz) buf[p] = val[p] * x[col_idx[p]];
+        else buf[p] = 0.0 * x[0]; /* padding: col 0, val 0 (:84-89) */
+    }
+    return buf;
+}
+
+void orc_ss_simple_spmv(int m, int64_t nnz, const int64_t *row_ptr,
+                        const int *col_idx, const double *val, int W,
+                        const double *x, double *y) {
+    int64_t H = nnz / W + (nnz % W != 0);
+    double *buf = orc_ss_mul(nnz, H, W, col_idx, val, x);
+    /* Sum (src/opt_ss.cpp:206-219) */
+    for (int i = 0; i < m; i++) {
+        double t = 0;
+        for (int64_t j = row_ptr[i]; j < row_ptr[i + 1]; j++) t += buf[j];
+        y[i] = t;
+    }
+    free(buf);
+}
+
+void orc_ss_optimized_spmv(int m, int64_t nnz, const int64_t *row_ptr,
+                           const int *col_idx, const double *val, int W,
+                           const double *x, double *y) {
+    int64_t H = nnz / W + (nnz % W != 0);
+    if (H == 0) {
+        for (int i = 0; i < m; i++) y[i] = 0;
+        return;
+    }
+    /* row of every slot; padding slots get row m (src/opt_ss.cpp:71-80) */
+    int *rowof = (int *)malloc(sizeof(int) * (size_t)(H * W));
+    for (int i = 0; i < m; i++)
+        for (int64_t j = row_ptr[i]; j < row_ptr[i + 1]; j++) rowof[j] = i;
+    for (int64_t p = nnz; p < H * W; p++) rowof[p] = m;
+    /* segment_index (src/opt_ss.cpp:91-107) */
+    int *seg = (int *)malloc(sizeof(int) * (size_t)H);
+    seg[0] = 0;
+    for (int64_t i = 1; i < H; i++) {
+        int same = 1;
+        if (rowof[(i - 1) * W] == rowof[i * W]) {
+            for (int j = 1; j < W; j++)
+                if (rowof[i * W + j - 1] != rowof[i * W + j]) same = 0;
+        } else {
+            same = 0;
+        }
+        seg[i] = same ? seg[i - 1] + 1 : 0;
+    }
+    int max_index = 0;
+    for (int64_t i = 0; i < H; i++) if (seg[i] > max_index) max_index = seg[i];
+    /* nStep = ceil(log2(max_index+1)) (src/opt_ss.cpp:121) */
+    int nStep = (int)ceil(log2((double)max_index + 1));
+    double *buf = orc_ss_mul(nnz, H, W, col_idx, val, x);
+    /* Sum1 tree fold (src/opt_ss.cpp:241-260) */
+    int counter = 1 << nStep;
+    for (int s = 0; s < nStep; s++) {
+        counter >>= 1;
+        for (int64_t h = 0; h < H; h++) {
+            if (counter <= seg[h] && seg[h] < counter * 2) {
+                for (int j = 0; j < W; j++) buf[(h - counter) * W + j] += buf[h * W + j];
+            }
+        }
+    }
+    /* Sum2 (src/opt_ss.cpp:262-303, non-PADDING) */
+    for (int i = 0; i < m; i++) {
+        double t = 0;
+        int64_t begin = row_ptr[i], end = row_ptr[i + 1];
+        int64_t begin_seg = begin / W, end_seg = end / W;
+        if (begin_seg == end_seg) {
+            int64_t jb = begin & (W - 1), je = end & (W - 1);
+            for (int64_t j = jb; j < je; j++) t += buf[begin_seg * W + j];
+        } else {
+            if (begin & (W - 1)) { /* upper */
+                int64_t je = (begin & ~(int64_t)(W - 1)) + W;
+                for (int64_t j = begin; j < je; j++) t += buf[j];
+                begin = je;
+            }
+            if (end & (W - 1)) { /* lower, descending */
+                int64_t je = end & ~(int64_t)(W - 1);
+                for (int64_t j = end; j > je; j--) t += buf[j - 1];
+                end = je;
+            }
+            if (begin != end) { /* center: the folded first full segment */
+                for (int j = 0; j < W; j++) t += buf[begin + j];
+            }
+        }
+        y[i] = t;
+    }
+    free(buf);
+    free(seg);
+    free(rowof);
+}

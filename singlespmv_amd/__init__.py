@@ -1,0 +1,357 @@
+"""singlespmv_amd -- MI355X-native fp64 SpMV engine (Python host mirror).
+
+Thin ctypes layer over ``libspmv_hip.so`` (include/spmv_hip.h).  It mirrors
+the reference driver's vocabulary (hir0shim/singleSpMV src/util.h:40-45,
+src/opt_crs.h:15-18):
+
+    A = load_sparse_matrix(path)            # LoadSparseMatrix
+    x = create_random_vector(n)             # srand(3) + CreateRandomVector
+    A_opt = optimize_problem(A, fmt="auto") # OptimizeProblem -> device plan
+    spmv(A_opt, x, y)                       # SpMV (y overwritten, beta = 0)
+    verify_result(A, x, y)                  # VerifyResult
+
+plus the plan object for device-resident x/y (torch tensors or raw device
+pointers), the seeded synthetic generators of the BASELINE configs, and the
+nnz-balanced row partition used by the multi-GPU bench.
+
+PyTorch is plumbing only (device memory, streams, torch.distributed).  There
+is no CPU fallback: if the HIP library is missing every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+
+try:  # load torch's HIP runtime first so the engine shares it (one runtime)
+    import torch  # noqa: F401
+except Exception:  # pragma: no cover - torch is part of the image
+    torch = None
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libspmv_hip.so")
+OPT_LIB_PATH = os.path.join(HERE, "libopt_hip.so")
+
+FORMATS = {"auto": 0, "csr": 1, "crs": 1, "ell": 2, "ss": 3, "dia": 4, "hyb": 5}
+FORMAT_NAMES = {0: "auto", 1: "csr", 2: "ell", 3: "ss", 4: "dia", 5: "hyb"}
+X_DEVICE, Y_DEVICE, ASYNC, X_STAGED = 0x1, 0x2, 0x4, 0x8
+GEN_UNIFORM, GEN_POWERLAW, GEN_BANDED = 1, 2, 3
+
+_I32P = np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")
+_I64P = np.ctypeslib.ndpointer(np.int64, flags="C_CONTIGUOUS")
+_F64P = np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")
+
+
+class SpmvError(RuntimeError):
+    pass
+
+
+class Options(C.Structure):
+    _fields_ = [("format", C.c_int32), ("device", C.c_int32), ("csr_lanes", C.c_int32),
+                ("ell_width", C.c_int32), ("ss_sigma", C.c_int32), ("dia_max_diags", C.c_int32),
+                ("dia_max_fill", C.c_double), ("reserved", C.c_int32 * 8)]
+
+
+class PlanInfo(C.Structure):
+    _fields_ = [("format", C.c_int32), ("device", C.c_int32), ("m", C.c_int64), ("n", C.c_int64),
+                ("nnz", C.c_int64), ("stored_slots", C.c_int64), ("device_bytes", C.c_int64),
+                ("algo_bytes", C.c_int64), ("row_ptr_bytes", C.c_int32), ("csr_lanes", C.c_int32),
+                ("ell_width", C.c_int32), ("ss_sigma", C.c_int32), ("n_diags", C.c_int32),
+                ("n_kernels", C.c_int32), ("overflow_nnz", C.c_int64), ("empty_rows", C.c_int64),
+                ("kernel", C.c_char * 64)]
+
+    def as_dict(self):
+        d = {k: getattr(self, k) for k, _ in self._fields_}
+        d["kernel"] = self.kernel.decode()
+        d["format"] = FORMAT_NAMES.get(self.format, str(self.format))
+        return d
+
+
+class GenSpec(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("per_row", C.c_int32), ("m", C.c_int64), ("n", C.c_int64),
+                ("max_len", C.c_int32), ("alpha", C.c_double), ("band_lo", C.c_int32),
+                ("band_hi", C.c_int32), ("integer_values", C.c_int32), ("seed", C.c_uint64)]
+
+
+# Exported symbols of include/spmv_hip.h (checked by tests/test_abi.py).
+EXPORTS = [
+    "spmv_options_default", "spmv_plan_create_coo", "spmv_plan_create_csr",
+    "spmv_plan_create_csr32", "spmv_plan_destroy", "spmv_execute", "spmv_set_stream",
+    "spmv_time", "spmv_plan_info", "spmv_status_string", "spmv_last_error",
+    "spmv_load_mtx", "spmv_free_host", "spmv_srand", "spmv_rand_vector", "spmv_verify_coo",
+    "spmv_coo_to_csr", "spmv_gen_count", "spmv_gen_fill", "spmv_gen_vector",
+    "spmv_partition_rows",
+]
+
+_lib = None
+
+
+def lib():
+    """The loaded libspmv_hip.so (raises if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise SpmvError(f"{LIB_PATH} missing: run `make` (or __graft_entry__.build()) first; "
+                        "there is no CPU fallback")
+    L = C.CDLL(LIB_PATH)
+    vp, i32, i64, f64 = C.c_void_p, C.c_int32, C.c_int64, C.c_double
+    L.spmv_options_default.argtypes = [C.POINTER(Options)]
+    L.spmv_plan_create_coo.argtypes = [i32, i32, i32, vp, vp, vp, C.POINTER(Options), C.POINTER(vp)]
+    L.spmv_plan_create_csr.argtypes = [i64, i64, i64, vp, vp, vp, C.POINTER(Options), C.POINTER(vp)]
+    L.spmv_plan_create_csr32.argtypes = [i32, i32, i32, vp, vp, vp, C.POINTER(Options), C.POINTER(vp)]
+    L.spmv_plan_destroy.argtypes = [vp]
+    L.spmv_execute.argtypes = [vp, vp, vp, C.c_uint32]
+    L.spmv_set_stream.argtypes = [vp, vp]
+    L.spmv_time.argtypes = [vp, vp, vp, i32, C.POINTER(f64)]
+    L.spmv_plan_info.argtypes = [vp, C.POINTER(PlanInfo)]
+    L.spmv_status_string.argtypes = [C.c_int]
+    L.spmv_status_string.restype = C.c_char_p
+    L.spmv_last_error.restype = C.c_char_p
+    L.spmv_load_mtx.argtypes = [C.c_char_p, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32),
+                                C.POINTER(C.POINTER(i32)), C.POINTER(C.POINTER(i32)),
+                                C.POINTER(C.POINTER(f64))]
+    L.spmv_free_host.argtypes = [vp]
+    L.spmv_srand.argtypes = [C.c_uint32]
+    L.spmv_rand_vector.argtypes = [i32, _F64P]
+    L.spmv_verify_coo.argtypes = [i32, i32, _I32P, _I32P, _F64P, _F64P, _F64P]
+    L.spmv_verify_coo.restype = i64
+    L.spmv_coo_to_csr.argtypes = [i32, i64, _I32P, _I64P]
+    L.spmv_gen_count.argtypes = [C.POINTER(GenSpec), i64, i64, C.POINTER(i64)]
+    L.spmv_gen_fill.argtypes = [C.POINTER(GenSpec), i64, i64, _I64P, vp, vp]
+    L.spmv_gen_vector.argtypes = [C.c_uint64, i32, i64, i64, _F64P]
+    L.spmv_partition_rows.argtypes = [_I64P, i64, i32, _I64P]
+    _lib = L
+    return L
+
+
+def _check(st: int, what: str):
+    if st != 0:
+        L = lib()
+        raise SpmvError(f"{what}: {L.spmv_status_string(st).decode()} "
+                        f"({L.spmv_last_error().decode()})")
+
+
+def _ptr(a) -> int:
+    """Device or host address of a numpy array / torch tensor / int."""
+    if a is None:
+        return 0
+    if isinstance(a, int):
+        return a
+    if isinstance(a, np.ndarray):
+        return a.ctypes.data
+    return int(a.data_ptr())  # torch tensor
+
+
+def _is_device(a) -> bool:
+    return (a is not None and not isinstance(a, (np.ndarray, int))
+            and getattr(a, "is_cuda", False))
+
+
+# ---------------------------------------------------------------- host types
+@dataclass
+class SpMat:
+    """Sorted COO (reference src/util.h:7-19)."""
+    nRow: int
+    nCol: int
+    row_idx: np.ndarray
+    col_idx: np.ndarray
+    val: np.ndarray
+
+    @property
+    def nNnz(self) -> int:
+        return int(self.val.shape[0])
+
+    def to_csr(self):
+        return coo_to_csr(self.nRow, self.row_idx), self.col_idx, self.val
+
+
+def load_sparse_matrix(path: str) -> SpMat:
+    """LoadSparseMatrix (src/util.cpp:30-66)."""
+    L = lib()
+    m, n, nnz = C.c_int32(), C.c_int32(), C.c_int32()
+    r, c, v = C.POINTER(C.c_int32)(), C.POINTER(C.c_int32)(), C.POINTER(C.c_double)()
+    _check(L.spmv_load_mtx(path.encode(), C.byref(m), C.byref(n), C.byref(nnz), C.byref(r),
+                           C.byref(c), C.byref(v)), f"load_sparse_matrix({path})")
+    k = nnz.value
+    out = SpMat(m.value, n.value,
+                np.ctypeslib.as_array(r, shape=(max(k, 1),))[:k].copy(),
+                np.ctypeslib.as_array(c, shape=(max(k, 1),))[:k].copy(),
+                np.ctypeslib.as_array(v, shape=(max(k, 1),))[:k].copy())
+    for p in (r, c, v):
+        L.spmv_free_host(C.cast(p, C.c_void_p))
+    return out
+
+
+def srand(seed: int) -> None:
+    lib().spmv_srand(seed)
+
+
+def create_random_vector(n: int) -> np.ndarray:
+    """CreateRandomVector (src/util.cpp:92-102); seed first with srand()."""
+    x = np.empty(max(n, 1), np.float64)
+    lib().spmv_rand_vector(n, x)
+    return x[:n]
+
+
+def verify_result(A: SpMat, x: np.ndarray, y: np.ndarray) -> bool:
+    """VerifyResult (src/util.cpp:67-83)."""
+    bad = lib().spmv_verify_coo(A.nRow, A.nNnz, A.row_idx, A.col_idx, A.val,
+                                np.ascontiguousarray(x, np.float64),
+                                np.ascontiguousarray(y, np.float64))
+    return bad < 0
+
+
+def coo_to_csr(m: int, row_idx: np.ndarray) -> np.ndarray:
+    rp = np.empty(m + 1, np.int64)
+    _check(lib().spmv_coo_to_csr(m, len(row_idx), np.ascontiguousarray(row_idx, np.int32), rp),
+           "coo_to_csr")
+    return rp
+
+
+# ---------------------------------------------------------------- plans
+def make_options(fmt="auto", device: int = -1, csr_lanes: int = 0, ell_width: int = 0,
+                 ss_sigma: int = 0, dia_max_diags: int = 0, dia_max_fill: float = 0.0) -> Options:
+    o = Options()
+    lib().spmv_options_default(C.byref(o))
+    o.format = FORMATS[fmt] if isinstance(fmt, str) else int(fmt)
+    o.device, o.csr_lanes, o.ell_width, o.ss_sigma = device, csr_lanes, ell_width, ss_sigma
+    o.dia_max_diags, o.dia_max_fill = dia_max_diags, dia_max_fill
+    return o
+
+
+class Plan:
+    """A device-resident matrix in one format (the SpMatOpt of a plugin)."""
+
+    def __init__(self, handle: int, keep=None):
+        self._h = C.c_void_p(handle)
+        self._keep = keep
+
+    # construction -------------------------------------------------------
+    @classmethod
+    def from_csr(cls, m: int, n: int, row_ptr, col, val, fmt="auto", **opts) -> "Plan":
+        rp = np.ascontiguousarray(row_ptr, np.int64)
+        col = np.ascontiguousarray(col, np.int32)
+        val = np.ascontiguousarray(val, np.float64)
+        o = make_options(fmt, **opts)
+        h = C.c_void_p()
+        _check(lib().spmv_plan_create_csr(m, n, len(val), rp.ctypes.data, col.ctypes.data,
+                                          val.ctypes.data, C.byref(o), C.byref(h)),
+               "spmv_plan_create_csr")
+        return cls(h.value)
+
+    @classmethod
+    def from_coo(cls, A: SpMat, fmt="auto", **opts) -> "Plan":
+        o = make_options(fmt, **opts)
+        h = C.c_void_p()
+        r = np.ascontiguousarray(A.row_idx, np.int32)
+        c = np.ascontiguousarray(A.col_idx, np.int32)
+        v = np.ascontiguousarray(A.val, np.float64)
+        _check(lib().spmv_plan_create_coo(A.nRow, A.nCol, A.nNnz, r.ctypes.data, c.ctypes.data,
+                                          v.ctypes.data, C.byref(o), C.byref(h)),
+               "spmv_plan_create_coo")
+        return cls(h.value)
+
+    # execution ------------------------------------------------------------
+    def execute(self, x, y, async_: bool = False) -> None:
+        """y = A x.  numpy arrays are host buffers (H2D x / D2H y per call, as
+        src/opt_cusparse.cpp:72,82); torch CUDA tensors are device buffers."""
+        flags = (X_DEVICE if _is_device(x) else 0) | (Y_DEVICE if _is_device(y) else 0)
+        if async_:
+            flags |= ASYNC
+        if isinstance(y, np.ndarray) and not y.flags.c_contiguous:
+            raise ValueError("y must be C-contiguous")
+        _check(lib().spmv_execute(self._h, _ptr(x), _ptr(y), flags), "spmv_execute")
+
+    def __call__(self, x, y=None):
+        if y is None:
+            info = self.info()
+            if _is_device(x):
+                y = torch.empty(info["m"], dtype=torch.float64, device=x.device)
+            else:
+                y = np.empty(info["m"], np.float64)
+        self.execute(x, y)
+        return y
+
+    def set_stream(self, stream) -> None:
+        s = stream if isinstance(stream, int) else (0 if stream is None else stream.cuda_stream)
+        _check(lib().spmv_set_stream(self._h, C.c_void_p(s)), "spmv_set_stream")
+
+    def time(self, x_dev, y_dev, iters: int) -> float:
+        """Milliseconds for `iters` back-to-back executes (HIP events on the
+        plan's stream)."""
+        ms = C.c_double()
+        _check(lib().spmv_time(self._h, _ptr(x_dev), _ptr(y_dev), iters, C.byref(ms)), "spmv_time")
+        return ms.value
+
+    def info(self) -> dict:
+        i = PlanInfo()
+        _check(lib().spmv_plan_info(self._h, C.byref(i)), "spmv_plan_info")
+        return i.as_dict()
+
+    def destroy(self) -> None:
+        if self._h is not None and self._h.value:
+            lib().spmv_plan_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.destroy()
+        except Exception:
+            pass
+
+
+def optimize_problem(A: SpMat, fmt="auto", **opts) -> Plan:
+    """OptimizeProblem (e.g. src/opt_crs.cpp:10-42): build the device format."""
+    return Plan.from_coo(A, fmt, **opts)
+
+
+def spmv(A_opt: Plan, x, y) -> None:
+    """SpMV (e.g. src/opt_crs.cpp:44-70): y = A x, y overwritten."""
+    A_opt.execute(x, y)
+
+
+# ---------------------------------------------------------------- generators
+def gen_spec(kind: str, m: int, n: Optional[int] = None, per_row: int = 16, max_len: int = 10000,
+             alpha: float = 2.0, band_lo: int = -32, band_hi: int = 31, integer_values=False,
+             seed: int = 42) -> GenSpec:
+    k = {"uniform": GEN_UNIFORM, "powerlaw": GEN_POWERLAW, "banded": GEN_BANDED}[kind]
+    return GenSpec(k, per_row, m, m if n is None else n, max_len, alpha, band_lo, band_hi,
+                   1 if integer_values else 0, seed)
+
+
+def generate_csr(spec: GenSpec, row_begin: int = 0, row_end: Optional[int] = None):
+    """CSR (row_ptr int64, col int32, val f64) of global rows [row_begin, row_end)."""
+    L = lib()
+    re = spec.m if row_end is None else row_end
+    nnz = C.c_int64()
+    _check(L.spmv_gen_count(C.byref(spec), row_begin, re, C.byref(nnz)), "spmv_gen_count")
+    rp = np.empty(re - row_begin + 1, np.int64)
+    col = np.empty(max(nnz.value, 1), np.int32)
+    val = np.empty(max(nnz.value, 1), np.float64)
+    _check(L.spmv_gen_fill(C.byref(spec), row_begin, re, rp, col.ctypes.data, val.ctypes.data),
+           "spmv_gen_fill")
+    return rp, col[:nnz.value], val[:nnz.value]
+
+
+def generate_vector(n: int, seed: int = 43, begin: int = 0, integer_values=False) -> np.ndarray:
+    out = np.empty(max(n, 1), np.float64)
+    _check(lib().spmv_gen_vector(seed, 1 if integer_values else 0, begin, n, out), "spmv_gen_vector")
+    return out[:n]
+
+
+def partition_rows(row_ptr: np.ndarray, parts: int) -> np.ndarray:
+    """nnz-balanced cut rows: cuts[k] = first row with
+    row_ptr[r] >= k*nnz/parts."""
+    cuts = np.empty(parts + 1, np.int64)
+    rp = np.ascontiguousarray(row_ptr, np.int64)
+    _check(lib().spmv_partition_rows(rp, len(rp) - 1, parts, cuts), "spmv_partition_rows")
+    return cuts
+
+
+def algorithmic_bytes_csr(m: int, n: int, nnz: int, rp_bytes: int = 4) -> int:
+    """12*nnz + rp*(m+1) + 8*n + 8*m."""
+    return 12 * nnz + rp_bytes * (m + 1) + 8 * n + 8 * m

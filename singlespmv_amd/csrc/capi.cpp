@@ -1,0 +1,308 @@
+// capi.cpp -- the C-ABI of include/spmv_hip.h: plan life cycle, execute,
+// timing, info.  Every entry point returns an int status; nothing exit()s.
+#include <omp.h>
+
+#include <algorithm>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "internal.hpp"
+
+namespace spmv {
+
+static thread_local std::string g_err;
+void set_error(const std::string &msg) { g_err = msg; }
+const char *last_error() { return g_err.c_str(); }
+
+static int check_device(int device) {
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count == 0) {
+        (void)hipGetLastError();
+        set_error("no HIP device visible (libspmv_hip needs an MI355X / gfx950)");
+        return SPMV_ERROR_NO_DEVICE;
+    }
+    if (device >= count) {
+        set_error("device ordinal out of range");
+        return SPMV_ERROR_INVALID_VALUE;
+    }
+    hipDeviceProp_t prop;
+    SPMV_HIP_TRY(hipGetDeviceProperties(&prop, device));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+        set_error(std::string("device is ") + prop.gcnArchName + "; kernels are built for gfx950 only");
+        return SPMV_ERROR_NO_DEVICE;
+    }
+    return SPMV_SUCCESS;
+}
+
+// Validate a host CSR before anything touches the GPU: an out-of-range
+// column would become an out-of-bounds gather on the device.
+static int validate_csr(const HostCsr &A) {
+    SPMV_CHECK_ARG(A.m >= 0 && A.n >= 0 && A.nnz >= 0, "negative dimension");
+    SPMV_CHECK_ARG(A.m < (int64_t)INT32_MAX && A.n < (int64_t)INT32_MAX,
+                   "m and n must be < 2^31 (int32 column indices)");
+    SPMV_CHECK_ARG(A.row_ptr != nullptr, "row_ptr is NULL");
+    SPMV_CHECK_ARG(A.nnz == 0 || (A.col != nullptr && A.val != nullptr), "col/val is NULL");
+    SPMV_CHECK_ARG(A.row_ptr[0] == 0, "row_ptr[0] != 0");
+    SPMV_CHECK_ARG(A.row_ptr[A.m] == A.nnz, "row_ptr[m] != nnz");
+    int64_t bad_rp = 0, bad_col = 0;
+#pragma omp parallel for schedule(static) reduction(+ : bad_rp)
+    for (int64_t r = 0; r < A.m; ++r) bad_rp += A.row_ptr[r + 1] < A.row_ptr[r];
+    SPMV_CHECK_ARG(bad_rp == 0, "row_ptr is not non-decreasing");
+    const int64_t n = A.n;
+#pragma omp parallel for schedule(static) reduction(+ : bad_col)
+    for (int64_t j = 0; j < A.nnz; ++j) bad_col += (A.col[j] < 0) | (A.col[j] >= n);
+    SPMV_CHECK_ARG(bad_col == 0, "column index outside [0, n)");
+    return SPMV_SUCCESS;
+}
+
+static int create_from_csr(const HostCsr &A, const spmv_options_t *opt_in, spmv_plan_t *out) {
+    SPMV_CHECK_ARG(out != nullptr, "plan out-pointer is NULL");
+    *out = nullptr;
+    spmv_options_t o;
+    if (opt_in) o = *opt_in;
+    else spmv_options_default(&o);
+    SPMV_RETURN_IF(validate_csr(A));
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count == 0) {
+        (void)hipGetLastError();
+        set_error("no HIP device visible (libspmv_hip needs an MI355X / gfx950)");
+        return SPMV_ERROR_NO_DEVICE;
+    }
+    int dev = o.device;
+    if (dev < 0) SPMV_HIP_TRY(hipGetDevice(&dev));
+    SPMV_RETURN_IF(check_device(dev));
+    SPMV_HIP_TRY(hipSetDevice(dev));
+    spmv_plan_s *p = new (std::nothrow) spmv_plan_s;
+    if (!p) {
+        set_error("host allocation of the plan failed");
+        return SPMV_ERROR_OUT_OF_MEMORY;
+    }
+    p->device = dev;
+    p->m = A.m;
+    p->n = A.n;
+    p->nnz = A.nnz;
+    int fmt = o.format == SPMV_FORMAT_AUTO ? choose_format(A, o) : o.format;
+    int st;
+    switch (fmt) {
+        case SPMV_FORMAT_CSR: st = build_csr(p, A, o); break;
+        case SPMV_FORMAT_ELL: st = build_ell(p, A, o, INT32_MAX); break;
+        case SPMV_FORMAT_HYB: st = build_hyb(p, A, o); break;
+        case SPMV_FORMAT_SS: st = build_ss(p, A, o); break;
+        case SPMV_FORMAT_DIA: st = build_dia(p, A, o); break;
+        default:
+            set_error("unknown format");
+            st = SPMV_ERROR_INVALID_VALUE;
+    }
+    if (st != SPMV_SUCCESS) {
+        p->arena.release();
+        delete p;
+        return st;
+    }
+    p->format = fmt;
+    *out = p;
+    return SPMV_SUCCESS;
+}
+
+static int dispatch(const spmv_plan_s *p, const double *x, double *y) {
+    switch (p->format) {
+        case SPMV_FORMAT_CSR: return launch_csr(p, x, y);
+        case SPMV_FORMAT_ELL: return launch_ell(p, x, y);
+        case SPMV_FORMAT_HYB:
+            SPMV_RETURN_IF(launch_ell(p, x, y));
+            return launch_hyb_overflow(p, x, y);
+        case SPMV_FORMAT_SS: return launch_ss(p, x, y);
+        case SPMV_FORMAT_DIA: return launch_dia(p, x, y);
+    }
+    set_error("plan has an unknown format");
+    return SPMV_ERROR_INVALID_VALUE;
+}
+
+static int bind_device(const spmv_plan_s *p) {
+    int cur = -1;
+    SPMV_HIP_TRY(hipGetDevice(&cur));
+    if (cur != p->device) SPMV_HIP_TRY(hipSetDevice(p->device));
+    return SPMV_SUCCESS;
+}
+
+}  // namespace spmv
+
+using namespace spmv;
+
+extern "C" {
+
+void spmv_options_default(spmv_options_t *o) {
+    if (!o) return;
+    std::memset(o, 0, sizeof(*o));
+    o->format = SPMV_FORMAT_AUTO;
+    o->device = -1;
+}
+
+int spmv_plan_create_csr(int64_t m, int64_t n, int64_t nnz, const int64_t *row_ptr,
+                         const int32_t *col_idx, const double *val, const spmv_options_t *opt,
+                         spmv_plan_t *plan) {
+    HostCsr A{m, n, nnz, row_ptr, col_idx, val};
+    return create_from_csr(A, opt, plan);
+}
+
+int spmv_plan_create_csr32(int32_t m, int32_t n, int32_t nnz, const int32_t *row_ptr,
+                           const int32_t *col_idx, const double *val, const spmv_options_t *opt,
+                           spmv_plan_t *plan) {
+    SPMV_CHECK_ARG(m >= 0 && row_ptr != nullptr, "bad m or NULL row_ptr");
+    std::vector<int64_t> rp((size_t)m + 1);
+    for (int32_t i = 0; i <= m; ++i) rp[i] = row_ptr[i];
+    HostCsr A{m, n, nnz, rp.data(), col_idx, val};
+    return create_from_csr(A, opt, plan);
+}
+
+int spmv_coo_to_csr(int32_t m, int64_t nnz, const int32_t *row_idx, int64_t *row_ptr) {
+    SPMV_CHECK_ARG(m >= 0 && nnz >= 0 && row_ptr != nullptr, "bad arguments");
+    SPMV_CHECK_ARG(nnz == 0 || row_idx != nullptr, "row_idx is NULL");
+    // the linear scan of src/opt_crs.cpp:26-33
+    int64_t p = 0;
+    for (int64_t i = 0; i < nnz; ++i) {
+        const int32_t r = row_idx[i];
+        SPMV_CHECK_ARG(r >= 0 && r < m, "row index outside [0, m)");
+        SPMV_CHECK_ARG(r + 1 >= p, "COO rows are not sorted");
+        while (p <= r) row_ptr[p++] = i;
+    }
+    while (p <= m) row_ptr[p++] = nnz;
+    return SPMV_SUCCESS;
+}
+
+int spmv_plan_create_coo(int32_t m, int32_t n, int32_t nnz, const int32_t *row_idx,
+                         const int32_t *col_idx, const double *val, const spmv_options_t *opt,
+                         spmv_plan_t *plan) {
+    SPMV_CHECK_ARG(m >= 0 && nnz >= 0, "negative dimension");
+    std::vector<int64_t> rp((size_t)m + 1);
+    SPMV_RETURN_IF(spmv_coo_to_csr(m, nnz, row_idx, rp.data()));
+    HostCsr A{m, n, nnz, rp.data(), col_idx, val};
+    return create_from_csr(A, opt, plan);
+}
+
+int spmv_plan_destroy(spmv_plan_t p) {
+    if (!p) return SPMV_SUCCESS;
+    (void)bind_device(p);
+    p->arena.release();
+    delete p;
+    return SPMV_SUCCESS;
+}
+
+int spmv_set_stream(spmv_plan_t p, void *stream) {
+    SPMV_CHECK_ARG(p != nullptr, "plan is NULL");
+    p->stream = (hipStream_t)stream;
+    return SPMV_SUCCESS;
+}
+
+int spmv_execute(spmv_plan_t p, const double *x, double *y, uint32_t flags) {
+    SPMV_CHECK_ARG(p != nullptr, "plan is NULL");
+    const bool staged = (flags & SPMV_X_STAGED) != 0;
+    SPMV_CHECK_ARG((x != nullptr || p->n == 0 || staged) && (y != nullptr || p->m == 0), "x or y is NULL");
+    SPMV_CHECK_ARG(!staged || p->x_stage != nullptr, "SPMV_X_STAGED without a previously staged x");
+    SPMV_RETURN_IF(bind_device(p));
+    const double *dx = x;
+    double *dy = y;
+    if (staged) {
+        dx = p->x_stage;
+        flags |= SPMV_X_DEVICE;
+    } else if (!(flags & SPMV_X_DEVICE)) {
+        // opt_cusparse.cpp:72 -- H2D copy of x on every call
+        if (!p->x_stage) {
+            void *q;
+            SPMV_RETURN_IF(p->arena.alloc(&q, sizeof(double) * (size_t)std::max<int64_t>(p->n, 1)));
+            p->x_stage = (double *)q;
+        }
+        if (p->n) SPMV_HIP_TRY(hipMemcpyAsync(p->x_stage, x, sizeof(double) * p->n, hipMemcpyHostToDevice, p->stream));
+        dx = p->x_stage;
+    }
+    if (!(flags & SPMV_Y_DEVICE)) {
+        if (!p->y_stage) {
+            void *q;
+            SPMV_RETURN_IF(p->arena.alloc(&q, sizeof(double) * (size_t)std::max<int64_t>(p->m, 1)));
+            p->y_stage = (double *)q;
+        }
+        dy = p->y_stage;
+    }
+    SPMV_RETURN_IF(dispatch(p, dx, dy));
+    if (!(flags & SPMV_Y_DEVICE)) {
+        // opt_cusparse.cpp:82 -- D2H copy of y on every call
+        if (p->m) SPMV_HIP_TRY(hipMemcpyAsync(y, dy, sizeof(double) * p->m, hipMemcpyDeviceToHost, p->stream));
+        SPMV_HIP_TRY(hipStreamSynchronize(p->stream));
+    } else if (!(flags & SPMV_ASYNC) || !(flags & SPMV_X_DEVICE)) {
+        SPMV_HIP_TRY(hipStreamSynchronize(p->stream));
+    }
+    return SPMV_SUCCESS;
+}
+
+int spmv_time(spmv_plan_t p, const double *x_dev, double *y_dev, int32_t iters, double *ms) {
+    SPMV_CHECK_ARG(p != nullptr && ms != nullptr && iters > 0, "bad arguments");
+    SPMV_RETURN_IF(bind_device(p));
+    hipEvent_t a, b;
+    SPMV_HIP_TRY(hipEventCreate(&a));
+    SPMV_HIP_TRY(hipEventCreate(&b));
+    SPMV_HIP_TRY(hipEventRecord(a, p->stream));
+    int st = SPMV_SUCCESS;
+    for (int i = 0; i < iters && st == SPMV_SUCCESS; ++i) st = dispatch(p, x_dev, y_dev);
+    SPMV_HIP_TRY(hipEventRecord(b, p->stream));
+    SPMV_HIP_TRY(hipEventSynchronize(b));
+    float f = 0;
+    SPMV_HIP_TRY(hipEventElapsedTime(&f, a, b));
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    *ms = f;
+    return st;
+}
+
+int spmv_plan_info(spmv_plan_t p, spmv_plan_info_t *info) {
+    SPMV_CHECK_ARG(p != nullptr && info != nullptr, "NULL argument");
+    std::memset(info, 0, sizeof(*info));
+    info->format = p->format;
+    info->device = p->device;
+    info->m = p->m;
+    info->n = p->n;
+    info->nnz = p->nnz;
+    info->stored_slots = p->stored_slots;
+    info->device_bytes = p->arena.bytes;
+    info->algo_bytes = p->algo_bytes;
+    info->row_ptr_bytes = p->csr.rp64 ? 8 : 4;
+    info->csr_lanes = p->format == SPMV_FORMAT_HYB ? p->hyb.lanes : p->csr.lanes;
+    info->ell_width = p->ell.max_width;
+    info->ss_sigma = p->ss.sigma;
+    info->n_diags = p->dia.n_diags;
+    info->n_kernels = p->n_kernels;
+    info->overflow_nnz = p->hyb.nnz;
+    info->empty_rows = p->empty_rows;
+    std::strncpy(info->kernel, p->kernel_name.c_str(), sizeof(info->kernel) - 1);
+    return SPMV_SUCCESS;
+}
+
+const char *spmv_status_string(int s) {
+    switch (s) {
+        case SPMV_SUCCESS: return "success";
+        case SPMV_ERROR_INVALID_VALUE: return "invalid value";
+        case SPMV_ERROR_NOT_SUPPORTED: return "not supported by this format";
+        case SPMV_ERROR_OUT_OF_MEMORY: return "out of memory";
+        case SPMV_ERROR_HIP: return "HIP runtime error";
+        case SPMV_ERROR_IO: return "I/O error";
+        case SPMV_ERROR_NO_DEVICE: return "no usable gfx950 device";
+    }
+    return "unknown status";
+}
+
+const char *spmv_last_error(void) { return spmv::last_error(); }
+
+int spmv_partition_rows(const int64_t *row_ptr, int64_t m, int32_t parts, int64_t *cuts) {
+    SPMV_CHECK_ARG(row_ptr && cuts && parts > 0 && m >= 0, "bad arguments");
+    const int64_t nnz = row_ptr[m];
+    cuts[0] = 0;
+    for (int k = 1; k < parts; ++k) {
+        const int64_t target = (int64_t)((__int128)nnz * k / parts);
+        cuts[k] = std::lower_bound(row_ptr, row_ptr + m, target) - row_ptr;
+        if (cuts[k] < cuts[k - 1]) cuts[k] = cuts[k - 1];
+    }
+    cuts[parts] = m;
+    return SPMV_SUCCESS;
+}
+
+}  // extern "C"

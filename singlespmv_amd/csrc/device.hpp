@@ -1,0 +1,75 @@
+// device.hpp -- CDNA4 (gfx950) device helpers shared by the SpMV kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace spmv {
+
+typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+
+// Streamed matrix data (col/val) is read exactly once per SpMV: load it with
+// the non-temporal hint so it does not displace x from L2 / Infinity Cache.
+__device__ __forceinline__ i32x4 ld_stream4(const int32_t *p) {
+    return __builtin_nontemporal_load(reinterpret_cast<const i32x4 *>(p));
+}
+__device__ __forceinline__ f64x2 ld_stream2(const double *p) {
+    return __builtin_nontemporal_load(reinterpret_cast<const f64x2 *>(p));
+}
+__device__ __forceinline__ double ld_stream(const double *p) {
+    return __builtin_nontemporal_load(p);
+}
+__device__ __forceinline__ int32_t ld_stream(const int32_t *p) {
+    return __builtin_nontemporal_load(p);
+}
+
+// x gathers: plain cached loads (x is the re-used operand).
+__device__ __forceinline__ double ld_x(const double *x, int32_t c) { return x[c]; }
+
+// y = a*b + c as a rounded multiply followed by a rounded add.  Keeps the
+// per-row arithmetic identical to the reference's `tmp += val*x`
+// (src/opt_crs.cpp:62-66) as compiled without contraction, so sequential-order
+// kernels (ELL, DIA, 1-lane CSR) are bit-exact against oracle/.
+__device__ __forceinline__ double madd(double a, double b, double c) {
+    return __dadd_rn(c, __dmul_rn(a, b));
+}
+
+// Sum over aligned groups of G lanes (G power of two <= 64); every lane of a
+// group ends with the group total.  Butterfly order is fixed -> deterministic.
+template <int G>
+__device__ __forceinline__ double group_sum(double v) {
+#pragma unroll
+    for (int o = G / 2; o > 0; o >>= 1) v = __dadd_rn(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// Inclusive prefix sum of an int across the 64-lane wave (Hillis-Steele).
+__device__ __forceinline__ int wave_inclusive_sum(int v, int lane) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        int t = __shfl_up(v, o, 64);
+        if (lane >= o) v += t;
+    }
+    return v;
+}
+
+// Segmented inclusive scan across the wave: a lane with `start` begins a new
+// segment.  Returns the running sum of the lane's segment up to and including
+// the lane.  Combination order is a fixed tree (deterministic).
+__device__ __forceinline__ double wave_seg_scan(double v, bool start, int lane) {
+    int f = start ? 1 : 0;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        double tv = __shfl_up(v, o, 64);
+        int tf = __shfl_up(f, o, 64);
+        if (lane >= o) {
+            if (!f) v = __dadd_rn(tv, v);
+            f |= tf;
+        }
+    }
+    return v;
+}
+
+}  // namespace spmv

@@ -1,0 +1,363 @@
+// formats.cpp -- host-side OptimizeProblem counterparts: build each device
+// layout from a CSR view and upload it once (the reference does this untimed
+// in OptimizeProblem, src/main.cpp:36).  OpenMP-parallel, 64-bit counts.
+#include <omp.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <limits>
+#include <numeric>
+#include <vector>
+
+#include "internal.hpp"
+
+namespace spmv {
+
+int DevArena::alloc(void **p, size_t n) {
+    if (n == 0) n = 16;
+    void *q = nullptr;
+    hipError_t e = hipMalloc(&q, n);
+    if (e != hipSuccess) {
+        set_error(std::string("hipMalloc(") + std::to_string(n) + "): " + hipGetErrorString(e));
+        (void)hipGetLastError();
+        return e == hipErrorOutOfMemory ? SPMV_ERROR_OUT_OF_MEMORY : SPMV_ERROR_HIP;
+    }
+    ptrs.push_back(q);
+    bytes += (int64_t)n;
+    *p = q;
+    return SPMV_SUCCESS;
+}
+
+void DevArena::release() {
+    for (void *q : ptrs) (void)hipFree(q);
+    ptrs.clear();
+    bytes = 0;
+}
+
+// Allocate count+pad elements, copy count from host, zero the pad.
+template <typename T>
+static int upload(spmv_plan_s *p, T **dst, const T *src, int64_t count, int64_t pad = 0) {
+    void *q = nullptr;
+    SPMV_RETURN_IF(p->arena.alloc(&q, sizeof(T) * (size_t)(count + pad)));
+    if (count > 0) SPMV_HIP_TRY(hipMemcpy(q, src, sizeof(T) * (size_t)count, hipMemcpyHostToDevice));
+    if (pad > 0) SPMV_HIP_TRY(hipMemset((char *)q + sizeof(T) * count, 0, sizeof(T) * (size_t)pad));
+    *dst = (T *)q;
+    return SPMV_SUCCESS;
+}
+
+template <typename T>
+static int dev_alloc(spmv_plan_s *p, T **dst, int64_t count) {
+    void *q = nullptr;
+    SPMV_RETURN_IF(p->arena.alloc(&q, sizeof(T) * (size_t)count));
+    *dst = (T *)q;
+    return SPMV_SUCCESS;
+}
+
+static inline int64_t round_up(int64_t v, int64_t a) { return (v + a - 1) / a * a; }
+
+int auto_csr_lanes(double mean_row) {
+    // one 4-entry chunk per lane per row on average
+    int L = 1;
+    while (L < 64 && 4.0 * L < mean_row) L <<= 1;
+    return L;
+}
+
+int auto_ss_sigma(double mean_row) {
+    // ~one row boundary per lane keeps the in-lane branch count low while
+    // each lane keeps SIGMA*12 bytes of loads in flight
+    if (mean_row <= 6) return 8;
+    if (mean_row <= 24) return 16;
+    return 32;
+}
+
+// ---------------------------------------------------------------- CSR
+int build_csr(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
+    CsrDev &c = p->csr;
+    c.rp64 = A.nnz >= (int64_t)std::numeric_limits<int32_t>::max() - 64;
+    if (c.rp64) {
+        SPMV_RETURN_IF(upload(p, (int64_t **)&c.row_ptr, A.row_ptr, A.m + 1));
+    } else {
+        std::vector<int32_t> rp32((size_t)A.m + 1);
+#pragma omp parallel for schedule(static)
+        for (int64_t i = 0; i <= A.m; ++i) rp32[i] = (int32_t)A.row_ptr[i];
+        SPMV_RETURN_IF(upload(p, (int32_t **)&c.row_ptr, rp32.data(), A.m + 1));
+    }
+    SPMV_RETURN_IF(upload(p, &c.col, A.col, A.nnz, kPad));
+    SPMV_RETURN_IF(upload(p, &c.val, A.val, A.nnz, kPad));
+    const double mean = A.m ? (double)A.nnz / (double)A.m : 0.0;
+    c.lanes = o.csr_lanes > 0 ? o.csr_lanes : auto_csr_lanes(mean);
+    if (c.lanes < 1 || c.lanes > 64 || (c.lanes & (c.lanes - 1))) {
+        set_error("csr_lanes must be a power of two in [1, 64]");
+        return SPMV_ERROR_INVALID_VALUE;
+    }
+    p->stored_slots = A.nnz;
+    p->algo_bytes = 12 * A.nnz + (c.rp64 ? 8 : 4) * (A.m + 1) + 8 * A.n + 8 * A.m;
+    p->n_kernels = 1;
+    p->kernel_name = "csr_vec4_kernel<" + std::to_string(c.lanes) + ">";
+    return SPMV_SUCCESS;
+}
+
+// ---------------------------------------------------------------- ELL
+// cap: maximum slots per row kept in the ELL part (HYB); INT32_MAX for ELL.
+int build_ell(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &, int cap) {
+    EllDev &e = p->ell;
+    e.n_slices = (A.m + 63) / 64;
+    std::vector<int64_t> off((size_t)e.n_slices + 1, 0);
+    int maxw = 0;
+#pragma omp parallel for schedule(static) reduction(max : maxw)
+    for (int64_t s = 0; s < e.n_slices; ++s) {
+        int64_t w = 0;
+        const int64_t r1 = std::min<int64_t>(A.m, (s + 1) * 64);
+        for (int64_t r = s * 64; r < r1; ++r) w = std::max<int64_t>(w, A.row_ptr[r + 1] - A.row_ptr[r]);
+        w = std::min<int64_t>(w, cap);
+        w = round_up(w, 4);
+        off[s + 1] = 64 * w;
+        maxw = std::max<int>(maxw, (int)w);
+    }
+    for (int64_t s = 0; s < e.n_slices; ++s) off[s + 1] += off[s];
+    const int64_t total = off[e.n_slices];
+    std::vector<int32_t> col((size_t)total);
+    std::vector<double> val((size_t)total);
+#pragma omp parallel for schedule(dynamic, 64)
+    for (int64_t s = 0; s < e.n_slices; ++s) {
+        const int64_t base = off[s];
+        const int64_t w = (off[s + 1] - base) / 64;
+        for (int li = 0; li < 64; ++li) {
+            const int64_t r = s * 64 + li;
+            int64_t len = 0, rs = 0;
+            if (r < A.m) {
+                rs = A.row_ptr[r];
+                len = std::min<int64_t>(A.row_ptr[r + 1] - rs, w);
+            }
+            int32_t last = 0;
+            for (int64_t k = 0; k < w; ++k) {
+                const int64_t pos = base + (k >> 2) * 256 + li * 4 + (k & 3);
+                if (k < len) {
+                    last = A.col[rs + k];
+                    col[pos] = last;
+                    val[pos] = A.val[rs + k];
+                } else {
+                    col[pos] = last;  // repeat a real column: no new cache line
+                    val[pos] = 0.0;
+                }
+            }
+        }
+    }
+    SPMV_RETURN_IF(upload(p, &e.slice_off, off.data(), e.n_slices + 1));
+    SPMV_RETURN_IF(upload(p, &e.col, col.data(), total));
+    SPMV_RETURN_IF(upload(p, &e.val, val.data(), total));
+    e.max_width = maxw;
+    p->stored_slots = total;
+    p->algo_bytes = 12 * A.nnz + 8 * A.n + 8 * A.m;
+    p->n_kernels = 1;
+    p->kernel_name = "ell_slice_kernel";
+    return SPMV_SUCCESS;
+}
+
+// ---------------------------------------------------------------- HYB
+static int choose_hyb_width(const HostCsr &A) {
+    // minimise modelled bytes: ELL slots (incl. padding) + overflow entries
+    // + per-overflow-row overhead, over K in {4, 8, ..., 256}
+    const int64_t ns = (A.m + 63) / 64;
+    std::vector<int64_t> smax((size_t)ns);
+#pragma omp parallel for schedule(static)
+    for (int64_t s = 0; s < ns; ++s) {
+        int64_t w = 0;
+        const int64_t r1 = std::min<int64_t>(A.m, (s + 1) * 64);
+        for (int64_t r = s * 64; r < r1; ++r) w = std::max<int64_t>(w, A.row_ptr[r + 1] - A.row_ptr[r]);
+        smax[s] = w;
+    }
+    int bestK = 4;
+    double best = std::numeric_limits<double>::max();
+    for (int K = 4; K <= 256; K += 4) {
+        double slots = 0, ovf = 0, ovr = 0;
+#pragma omp parallel for schedule(static) reduction(+ : slots)
+        for (int64_t s = 0; s < ns; ++s) slots += 64.0 * (double)round_up(std::min<int64_t>(smax[s], K), 4);
+#pragma omp parallel for schedule(static) reduction(+ : ovf, ovr)
+        for (int64_t r = 0; r < A.m; ++r) {
+            const int64_t len = A.row_ptr[r + 1] - A.row_ptr[r];
+            if (len > K) { ovf += (double)(len - K); ovr += 1.0; }
+        }
+        const double cost = 12.0 * slots + 12.0 * ovf + 32.0 * ovr;
+        if (cost < best) { best = cost; bestK = K; }
+    }
+    return bestK;
+}
+
+int build_hyb(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
+    const int K = o.ell_width > 0 ? (int)round_up(o.ell_width, 4) : choose_hyb_width(A);
+    SPMV_RETURN_IF(build_ell(p, A, o, K));
+    const int64_t ell_slots = p->stored_slots;
+    HybDev &h = p->hyb;
+    std::vector<int32_t> rows;
+    std::vector<int64_t> rp(1, 0);
+    for (int64_t r = 0; r < A.m; ++r) {
+        const int64_t len = A.row_ptr[r + 1] - A.row_ptr[r];
+        if (len > K) {
+            rows.push_back((int32_t)r);
+            rp.push_back(rp.back() + (len - K));
+        }
+    }
+    h.n_rows = (int64_t)rows.size();
+    h.nnz = rp.back();
+    std::vector<int32_t> col((size_t)h.nnz);
+    std::vector<double> val((size_t)h.nnz);
+#pragma omp parallel for schedule(dynamic, 16)
+    for (int64_t i = 0; i < h.n_rows; ++i) {
+        const int64_t src = A.row_ptr[rows[i]] + K;
+        std::memcpy(&col[rp[i]], A.col + src, sizeof(int32_t) * (size_t)(rp[i + 1] - rp[i]));
+        std::memcpy(&val[rp[i]], A.val + src, sizeof(double) * (size_t)(rp[i + 1] - rp[i]));
+    }
+    SPMV_RETURN_IF(upload(p, &h.rows, rows.data(), h.n_rows));
+    SPMV_RETURN_IF(upload(p, &h.row_ptr, rp.data(), h.n_rows + 1));
+    SPMV_RETURN_IF(upload(p, &h.col, col.data(), h.nnz, kPad));
+    SPMV_RETURN_IF(upload(p, &h.val, val.data(), h.nnz, kPad));
+    p->ell.max_width = K;
+    p->stored_slots = ell_slots + h.nnz;
+    p->algo_bytes = 12 * A.nnz + 8 * A.n + 8 * A.m + 12 * h.n_rows;
+    p->n_kernels = h.n_rows ? 2 : 1;
+    p->kernel_name = "ell_slice_kernel";
+    return SPMV_SUCCESS;
+}
+
+// ---------------------------------------------------------------- SS
+int build_ss(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
+    SsDev &s = p->ss;
+    const double mean = A.m ? (double)A.nnz / (double)A.m : 0.0;
+    s.sigma = o.ss_sigma > 0 ? o.ss_sigma : auto_ss_sigma(mean);
+    if (s.sigma % 4 || s.sigma < 4 || s.sigma > 32 || s.sigma == 28) {
+        set_error("ss_sigma must be one of 4,8,12,16,20,24,32");
+        return SPMV_ERROR_INVALID_VALUE;
+    }
+    const int64_t T = 64 * (int64_t)s.sigma;
+    s.n_tiles = (A.nnz + T - 1) / T;
+    // ordinals of non-empty rows
+    std::vector<int64_t> nzord((size_t)A.m + 1, 0);
+    for (int64_t r = 0; r < A.m; ++r) nzord[r + 1] = nzord[r] + (A.row_ptr[r + 1] > A.row_ptr[r] ? 1 : 0);
+    s.n_nonempty = nzord[A.m];
+    s.n_empty = A.m - s.n_nonempty;
+    if (s.n_empty > 0) {
+        std::vector<int32_t> nzrow((size_t)std::max<int64_t>(s.n_nonempty, 1));
+        std::vector<int32_t> empty((size_t)s.n_empty);
+        int64_t a = 0, b = 0;
+        for (int64_t r = 0; r < A.m; ++r) {
+            if (A.row_ptr[r + 1] > A.row_ptr[r]) nzrow[a++] = (int32_t)r;
+            else empty[b++] = (int32_t)r;
+        }
+        SPMV_RETURN_IF(upload(p, &s.nzrow, nzrow.data(), s.n_nonempty));
+        SPMV_RETURN_IF(upload(p, &s.empty_rows, empty.data(), s.n_empty));
+    }
+    const int64_t total = s.n_tiles * T;
+    std::vector<uint32_t> flags((size_t)s.n_tiles * 64, 0u);
+    std::vector<int32_t> tord((size_t)s.n_tiles);
+    auto set_flag = [&](int64_t pos) {
+        const int64_t t = pos / T, li = pos % T;
+        uint32_t *w = &flags[(size_t)(t * 64 + li / s.sigma)];
+        __atomic_fetch_or(w, 1u << (li % s.sigma), __ATOMIC_RELAXED);
+    };
+#pragma omp parallel for schedule(static)
+    for (int64_t r = 0; r < A.m; ++r)
+        if (A.row_ptr[r + 1] > A.row_ptr[r]) set_flag(A.row_ptr[r]);
+    if (A.nnz % T) set_flag(A.nnz);  // dummy segment over the padding
+#pragma omp parallel for schedule(static)
+    for (int64_t t = 0; t < s.n_tiles; ++t) {
+        const int64_t r = std::lower_bound(A.row_ptr, A.row_ptr + A.m, t * T) - A.row_ptr;
+        tord[t] = (int32_t)nzord[r];
+    }
+    std::vector<int32_t> col((size_t)total);
+    std::vector<double> val((size_t)total);
+#pragma omp parallel for schedule(static)
+    for (int64_t t = 0; t < s.n_tiles; ++t) {
+        for (int64_t li = 0; li < T; ++li) {
+            const int64_t i = t * T + li;
+            const int64_t lane = li / s.sigma, k = li % s.sigma;
+            const int64_t pos = t * T + (k >> 2) * 256 + lane * 4 + (k & 3);
+            col[pos] = i < A.nnz ? A.col[i] : 0;
+            val[pos] = i < A.nnz ? A.val[i] : 0.0;
+        }
+    }
+    SPMV_RETURN_IF(upload(p, &s.col, col.data(), total));
+    SPMV_RETURN_IF(upload(p, &s.val, val.data(), total));
+    SPMV_RETURN_IF(upload(p, &s.flags, flags.data(), s.n_tiles * 64));
+    SPMV_RETURN_IF(upload(p, &s.tile_ord, tord.data(), s.n_tiles));
+    SPMV_RETURN_IF(dev_alloc(p, &s.head, s.n_tiles));
+    SPMV_RETURN_IF(dev_alloc(p, &s.tail, s.n_tiles));
+    SPMV_RETURN_IF(dev_alloc(p, &s.tail_ord, s.n_tiles));
+    p->stored_slots = total;
+    p->empty_rows = s.n_empty;
+    p->algo_bytes = 12 * A.nnz + 8 * A.n + 8 * A.m;
+    p->n_kernels = 2;
+    p->kernel_name = "ss_tile_kernel<" + std::to_string(s.sigma) + ">";
+    return SPMV_SUCCESS;
+}
+
+// ---------------------------------------------------------------- DIA
+// Occupied diagonals (col - row), ascending.  Returns false when the matrix
+// exceeds the limits (too many diagonals / too much zero fill).
+static bool dia_offsets(const HostCsr &A, int max_diags, double max_fill, std::vector<int32_t> &offs) {
+    const int64_t N = A.m + A.n - 1;
+    if (N <= 0) return true;
+    std::vector<uint8_t> occ((size_t)N, 0);
+#pragma omp parallel for schedule(static)
+    for (int64_t r = 0; r < A.m; ++r)
+        for (int64_t j = A.row_ptr[r]; j < A.row_ptr[r + 1]; ++j) occ[(size_t)(A.col[j] - r + A.m - 1)] = 1;
+    for (int64_t d = 0; d < N; ++d) {
+        if (occ[(size_t)d]) {
+            offs.push_back((int32_t)(d - (A.m - 1)));
+            if ((int)offs.size() > max_diags) return false;
+        }
+    }
+    return (double)offs.size() * (double)A.m <= max_fill * (double)std::max<int64_t>(A.nnz, 1);
+}
+
+int build_dia(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
+    DiaDev &d = p->dia;
+    const int maxd = o.dia_max_diags > 0 ? o.dia_max_diags : 1024;
+    const double fill = o.dia_max_fill > 0 ? o.dia_max_fill : 3.0;
+    std::vector<int32_t> offs;
+    if (!dia_offsets(A, maxd, fill, offs)) {
+        set_error("DIA: matrix has too many diagonals or too much zero fill for the DIA format");
+        return SPMV_ERROR_NOT_SUPPORTED;
+    }
+    d.n_diags = (int)offs.size();
+    d.off_host = offs;
+    const int64_t N = A.m + A.n - 1;
+    std::vector<int32_t> idx((size_t)std::max<int64_t>(N, 1), -1);
+    for (int i = 0; i < d.n_diags; ++i) idx[(size_t)(offs[i] + A.m - 1)] = i;
+    const int64_t slots = (int64_t)d.n_diags * A.m;
+    std::vector<double> val((size_t)std::max<int64_t>(slots, 1), 0.0);
+#pragma omp parallel for schedule(static)
+    for (int64_t r = 0; r < A.m; ++r)
+        for (int64_t j = A.row_ptr[r]; j < A.row_ptr[r + 1]; ++j) {
+            const int di = idx[(size_t)(A.col[j] - r + A.m - 1)];
+            val[(size_t)(di * A.m + r)] += A.val[j];  // duplicates are summed
+        }
+    SPMV_RETURN_IF(upload(p, &d.off, offs.data(), d.n_diags));
+    SPMV_RETURN_IF(upload(p, &d.val, val.data(), slots));
+    p->stored_slots = slots;
+    p->algo_bytes = 8 * A.nnz + 4 * (int64_t)d.n_diags + 8 * A.n + 8 * A.m;
+    p->n_kernels = 1;
+    p->kernel_name = "dia_kernel";
+    return SPMV_SUCCESS;
+}
+
+// ---------------------------------------------------------------- AUTO
+int choose_format(const HostCsr &A, const spmv_options_t &o) {
+    if (A.m == 0 || A.nnz == 0) return SPMV_FORMAT_CSR;
+    const double mean = (double)A.nnz / (double)A.m;
+    int64_t maxlen = 0;
+#pragma omp parallel for schedule(static) reduction(max : maxlen)
+    for (int64_t r = 0; r < A.m; ++r) maxlen = std::max<int64_t>(maxlen, A.row_ptr[r + 1] - A.row_ptr[r]);
+    // banded: few, well-filled diagonals -> DIA moves 8 instead of 12 B/nnz
+    if (maxlen <= 512) {
+        std::vector<int32_t> offs;
+        if (dia_offsets(A, 256, 1.25, offs)) return SPMV_FORMAT_DIA;
+    }
+    (void)o;
+    // near-uniform rows -> sliced ELL; skewed -> segmented sum
+    if ((double)maxlen <= 2.0 * mean + 8.0) return SPMV_FORMAT_ELL;
+    return SPMV_FORMAT_SS;
+}
+
+}  // namespace spmv

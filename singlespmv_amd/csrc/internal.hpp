@@ -1,0 +1,175 @@
+// internal.hpp -- plan layout, error plumbing and launcher declarations shared
+// by the C-ABI (capi.cpp), the host format builders (formats.cpp) and the
+// kernels (k_*.hip).  Not installed; the public surface is include/spmv_hip.h.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "spmv_hip.h"
+
+namespace spmv {
+
+// ---- error plumbing (the C-ABI returns codes; it never exit()s, unlike
+//      src/util.h:48-55 CUDA_SAFE_CALL and src/util.cpp:32-35) -------------
+void set_error(const std::string &msg);
+const char *last_error();
+
+#define SPMV_HIP_TRY(call)                                                      \
+    do {                                                                        \
+        hipError_t e_ = (call);                                                 \
+        if (e_ != hipSuccess) {                                                 \
+            ::spmv::set_error(std::string(#call) + ": " + hipGetErrorString(e_) + \
+                              " (" __FILE__ ":" + std::to_string(__LINE__) + ")"); \
+            return SPMV_ERROR_HIP;                                              \
+        }                                                                       \
+    } while (0)
+
+#define SPMV_CHECK_ARG(cond, msg)                                               \
+    do {                                                                        \
+        if (!(cond)) {                                                          \
+            ::spmv::set_error(msg);                                             \
+            return SPMV_ERROR_INVALID_VALUE;                                    \
+        }                                                                       \
+    } while (0)
+
+#define SPMV_RETURN_IF(status)                                                  \
+    do {                                                                        \
+        int s_ = (status);                                                      \
+        if (s_ != SPMV_SUCCESS) return s_;                                      \
+    } while (0)
+
+// ---- device memory owned by a plan --------------------------------------
+struct DevArena {
+    std::vector<void *> ptrs;
+    int64_t bytes = 0;
+    int alloc(void **p, size_t n);  // hipMalloc, zero-size safe
+    void release();
+};
+
+// ---- per-format device layouts ------------------------------------------
+
+// CSR (opt_crs, src/opt_crs.h:3-9): row_ptr (int32 when nnz < 2^31, else
+// int64), col_idx int32, val f64.  col/val are padded by kPad entries so the
+// 16-byte vector loads of the aligned-start kernel never leave the buffer.
+constexpr int kPad = 8;
+struct CsrDev {
+    void *row_ptr = nullptr;  // int32 or int64 [m+1]
+    bool rp64 = false;
+    int32_t *col = nullptr;   // [nnz + kPad]
+    double *val = nullptr;    // [nnz + kPad]
+    int lanes = 4;            // lanes per row (1..64)
+};
+
+// Sliced ELL (opt_ell, src/opt_ell.cpp): slices of 64 consecutive rows (one
+// wave); slice s has width w_s (multiple of 4) = max row length in the slice
+// (capped at K for HYB).  Slot k of local row i lives at
+//   slice_off[s] + (k/4)*256 + i*4 + (k%4)
+// so one 16-byte load gives a lane 4 consecutive slots of its row and a wave
+// instruction reads 1 KiB contiguous.  Padding: col = last real col of the
+// row (0 for an empty row), val = 0 -> adds +0.0, no new cache line.
+struct EllDev {
+    int64_t n_slices = 0;
+    int64_t *slice_off = nullptr;  // [n_slices + 1] in slots
+    int32_t *col = nullptr;
+    double *val = nullptr;
+    int max_width = 0;
+};
+
+// HYB overflow: rows whose length exceeds K keep entries K.. in a CSR over
+// those rows only; a second kernel adds them (one writer per row).
+struct HybDev {
+    int64_t n_rows = 0;
+    int32_t *rows = nullptr;     // [n_rows] global row ids
+    int64_t *row_ptr = nullptr;  // [n_rows + 1]
+    int32_t *col = nullptr;
+    double *val = nullptr;
+    int64_t nnz = 0;
+    int lanes = 64;
+};
+
+// Segmented sum (opt_ss / CSR5): tiles of 64 lanes x sigma nnz.  Lane l of
+// tile t owns nnz t*64*sigma + l*sigma + k, k in [0, sigma), stored at
+//   t*64*sigma + (k/4)*256 + l*4 + (k%4).
+// flags[t*64 + l] bit k: that nnz is the first entry of a non-empty row.
+// tile_ord[t]: ordinal (among non-empty rows) of the first row that starts
+// inside tile t.  Rows that cross tiles are finished by a fixup kernel from
+// per-tile head/tail partials (deterministic, no atomics, β = 0).
+struct SsDev {
+    int sigma = 16;
+    int64_t n_tiles = 0;
+    int32_t *col = nullptr;
+    double *val = nullptr;
+    uint32_t *flags = nullptr;
+    int32_t *tile_ord = nullptr;
+    double *head = nullptr;      // scratch [n_tiles]
+    double *tail = nullptr;      // scratch [n_tiles]
+    int32_t *tail_ord = nullptr; // scratch [n_tiles], -1 = no row starts in tile
+    int32_t *nzrow = nullptr;    // ordinal -> row (null when no empty rows)
+    int64_t n_nonempty = 0;
+    int32_t *empty_rows = nullptr;
+    int64_t n_empty = 0;
+};
+
+// DIA (opt_dia, src/opt_dia.cpp), row-indexed: val[d*m + r] = A[r, r+off[d]]
+// (0 where absent / outside), offsets ascending.
+struct DiaDev {
+    int n_diags = 0;
+    int32_t *off = nullptr;  // device copy of offsets
+    std::vector<int32_t> off_host;
+    double *val = nullptr;   // [n_diags * m]
+};
+
+}  // namespace spmv
+
+struct spmv_plan_s {
+    int format = SPMV_FORMAT_CSR;
+    int device = 0;
+    int64_t m = 0, n = 0, nnz = 0;
+    hipStream_t stream = nullptr;
+    spmv::DevArena arena;
+    spmv::CsrDev csr;
+    spmv::EllDev ell;
+    spmv::HybDev hyb;
+    spmv::SsDev ss;
+    spmv::DiaDev dia;
+    double *x_stage = nullptr;  // host-x staging (opt_cusparse.cpp:44-45)
+    double *y_stage = nullptr;
+    int64_t stored_slots = 0;
+    int64_t empty_rows = 0;
+    int64_t algo_bytes = 0;
+    int n_kernels = 1;
+    std::string kernel_name;
+};
+
+namespace spmv {
+
+// Host-side matrix view handed to the builders (CSR, 64-bit row pointers).
+struct HostCsr {
+    int64_t m, n, nnz;
+    const int64_t *row_ptr;
+    const int32_t *col;
+    const double *val;
+};
+
+// formats.cpp -- build + upload one format into `p`.
+int build_csr(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o);
+int build_ell(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o, int cap);
+int build_hyb(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o);
+int build_ss(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o);
+int build_dia(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o);
+int choose_format(const HostCsr &A, const spmv_options_t &o);
+int auto_csr_lanes(double mean_row);
+int auto_ss_sigma(double mean_row);
+
+// kernels -- launch y = A x on p->stream (device x, y).
+int launch_csr(const spmv_plan_s *p, const double *x, double *y);
+int launch_ell(const spmv_plan_s *p, const double *x, double *y);
+int launch_hyb_overflow(const spmv_plan_s *p, const double *x, double *y);
+int launch_ss(const spmv_plan_s *p, const double *x, double *y);
+int launch_dia(const spmv_plan_s *p, const double *x, double *y);
+
+}  // namespace spmv

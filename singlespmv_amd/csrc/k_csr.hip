@@ -1,0 +1,123 @@
+// k_csr.hip -- CSR SpMV for gfx950: the opt_crs hot loop
+// (src/opt_crs.cpp:57-69, `y[i] = sum_j val[j] * x[idx[j]]`) re-designed for
+// wave64.
+//
+// csr_vec4<L, RP>: a group of L lanes (L | 64) owns one row.  The group walks
+// the row from its 16-byte-aligned start a = ptr[i] & ~3 in chunks of 4*L
+// entries; each lane issues ONE 16-byte load of 4 column indices and TWO
+// 16-byte loads of 4 values (non-temporal: streamed once), so a wave
+// instruction covers 1 KiB contiguous when rows are contiguous.  Entries
+// outside [ptr[i], ptr[i+1]) are masked (no gather).  Each lane sums its
+// entries in order, then the group reduces with a fixed butterfly; lane 0
+// writes y[i] (β = 0, idempotent).
+//
+// Algorithmic bytes per row: 12*nnz_i + rp bytes + 8 (y) and the
+// x gathers (8*n total, counted once).
+#include "device.hpp"
+#include "internal.hpp"
+
+namespace spmv {
+
+template <int L, typename RP>
+__global__ __launch_bounds__(256) void csr_vec4_kernel(int64_t m, const RP *__restrict__ rp,
+                                                       const int32_t *__restrict__ col,
+                                                       const double *__restrict__ val,
+                                                       const double *__restrict__ x,
+                                                       double *__restrict__ y) {
+    const int64_t gtid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t row = gtid / L;
+    const int lane = threadIdx.x & (L - 1);
+    if (row >= m) return;  // whole groups exit together (L | 256)
+    const int64_t s = rp[row];
+    const int64_t e = rp[row + 1];
+    double acc = 0.0;
+    for (int64_t j = (s & ~(int64_t)3) + 4 * lane; j < e; j += 4 * L) {
+        const i32x4 c = ld_stream4(col + j);
+        const f64x2 v01 = ld_stream2(val + j);
+        const f64x2 v23 = ld_stream2(val + j + 2);
+        // masked gathers: only entries of this row
+        const double x0 = (j + 0 >= s && j + 0 < e) ? ld_x(x, c.x) : 0.0;
+        const double x1 = (j + 1 >= s && j + 1 < e) ? ld_x(x, c.y) : 0.0;
+        const double x2 = (j + 2 >= s && j + 2 < e) ? ld_x(x, c.z) : 0.0;
+        const double x3 = (j + 3 >= s && j + 3 < e) ? ld_x(x, c.w) : 0.0;
+        if (j + 0 >= s && j + 0 < e) acc = madd(v01.x, x0, acc);
+        if (j + 1 >= s && j + 1 < e) acc = madd(v01.y, x1, acc);
+        if (j + 2 >= s && j + 2 < e) acc = madd(v23.x, x2, acc);
+        if (j + 3 >= s && j + 3 < e) acc = madd(v23.y, x3, acc);
+    }
+    acc = group_sum<L>(acc);
+    if (lane == 0) y[row] = acc;
+}
+
+template <int L, typename RP>
+static int launch_csr_t(const spmv_plan_s *p, const double *x, double *y) {
+    const int64_t threads = p->m * L;
+    const int64_t blocks = (threads + 255) / 256;
+    if (blocks == 0) return SPMV_SUCCESS;
+    hipLaunchKernelGGL((csr_vec4_kernel<L, RP>), dim3((unsigned)blocks), dim3(256), 0, p->stream,
+                       p->m, (const RP *)p->csr.row_ptr, p->csr.col, p->csr.val, x, y);
+    SPMV_HIP_TRY(hipGetLastError());
+    return SPMV_SUCCESS;
+}
+
+template <typename RP>
+static int launch_csr_rp(const spmv_plan_s *p, const double *x, double *y) {
+    switch (p->csr.lanes) {
+        case 1: return launch_csr_t<1, RP>(p, x, y);
+        case 2: return launch_csr_t<2, RP>(p, x, y);
+        case 4: return launch_csr_t<4, RP>(p, x, y);
+        case 8: return launch_csr_t<8, RP>(p, x, y);
+        case 16: return launch_csr_t<16, RP>(p, x, y);
+        case 32: return launch_csr_t<32, RP>(p, x, y);
+        case 64: return launch_csr_t<64, RP>(p, x, y);
+        default: set_error("csr lanes must be a power of two in [1,64]"); return SPMV_ERROR_INVALID_VALUE;
+    }
+}
+
+int launch_csr(const spmv_plan_s *p, const double *x, double *y) {
+    return p->csr.rp64 ? launch_csr_rp<int64_t>(p, x, y) : launch_csr_rp<int32_t>(p, x, y);
+}
+
+// ---- HYB overflow: CSR-vector over the overflow rows, y[row] += sum -------
+template <int L>
+__global__ __launch_bounds__(256) void hyb_overflow_kernel(int64_t nrows, const int32_t *__restrict__ rows,
+                                                           const int64_t *__restrict__ rp,
+                                                           const int32_t *__restrict__ col,
+                                                           const double *__restrict__ val,
+                                                           const double *__restrict__ x,
+                                                           double *__restrict__ y) {
+    const int64_t gtid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t r = gtid / L;
+    const int lane = threadIdx.x & (L - 1);
+    if (r >= nrows) return;
+    const int64_t s = rp[r];
+    const int64_t e = rp[r + 1];
+    double acc = 0.0;
+    for (int64_t j = (s & ~(int64_t)3) + 4 * lane; j < e; j += 4 * L) {
+        const i32x4 c = ld_stream4(col + j);
+        const f64x2 v01 = ld_stream2(val + j);
+        const f64x2 v23 = ld_stream2(val + j + 2);
+        if (j + 0 >= s && j + 0 < e) acc = madd(v01.x, ld_x(x, c.x), acc);
+        if (j + 1 >= s && j + 1 < e) acc = madd(v01.y, ld_x(x, c.y), acc);
+        if (j + 2 >= s && j + 2 < e) acc = madd(v23.x, ld_x(x, c.z), acc);
+        if (j + 3 >= s && j + 3 < e) acc = madd(v23.y, ld_x(x, c.w), acc);
+    }
+    acc = group_sum<L>(acc);
+    if (lane == 0) {
+        const int32_t row = rows[r];
+        y[row] = __dadd_rn(y[row], acc);  // single writer per row
+    }
+}
+
+int launch_hyb_overflow(const spmv_plan_s *p, const double *x, double *y) {
+    const HybDev &h = p->hyb;
+    if (h.n_rows == 0) return SPMV_SUCCESS;
+    const int L = 64;
+    const int64_t blocks = (h.n_rows * L + 255) / 256;
+    hipLaunchKernelGGL((hyb_overflow_kernel<64>), dim3((unsigned)blocks), dim3(256), 0, p->stream,
+                       h.n_rows, h.rows, h.row_ptr, h.col, h.val, x, y);
+    SPMV_HIP_TRY(hipGetLastError());
+    return SPMV_SUCCESS;
+}
+
+}  // namespace spmv

@@ -1,0 +1,164 @@
+// k_ss.hip -- segmented-sum SpMV for gfx950: replaces opt_ss
+// (src/opt_ss.cpp:222-350: Mul into val_buf, tree fold "Sum1", row "Sum2")
+// and the vendored CSR5 (CSR5_cuda/detail/cuda/csr5_spmv_cuda.h:275-419:
+// compute -> calibrate -> tail) with a fused, deterministic, idempotent
+// wave64 design.
+//
+// ss_tile_kernel<SIGMA>: one wave = one tile of 64 lanes x SIGMA nnz.  Lane l
+// owns SIGMA consecutive nnz (see SsDev layout: every wave load instruction is
+// 1 KiB contiguous).  Products never touch memory (no val_buf: opt_ss's extra
+// 16 B/nnz is gone).  Per lane: sequential segmented sums split by the row
+// start bit-flags; rows that start and end in the lane are written directly.
+// Across the wave: a segmented scan (fixed tree) carries open rows from lane
+// to lane; the lane where a carried row ends writes it.  A row still open at
+// the tile end leaves (tail partial, its ordinal); the partial of the tile's
+// first row continuing from earlier tiles leaves as head partial.
+//
+// ss_fixup_kernel: one thread per tile whose tail is open adds the heads of
+// the following tiles up to the next tile that starts a row (fixed order --
+// no atomics, unlike the CAS atomicAdd calibrator of CSR5,
+// csr5_spmv_cuda.h:313-382), and zeroes empty rows.  Every y entry is written
+// exactly once per execute (β = 0), fixing the CSR5 non-idempotence noted in
+// SURVEY §3.5.
+#include "device.hpp"
+#include "internal.hpp"
+
+namespace spmv {
+
+__device__ __forceinline__ void ss_store(double *y, const int32_t *nzrow, int64_t n_nonempty,
+                                         int64_t ord, double v) {
+    if (ord < n_nonempty) y[nzrow ? (int64_t)nzrow[ord] : ord] = v;
+}
+
+template <int SIGMA>
+__global__ __launch_bounds__(256) void ss_tile_kernel(
+    int64_t n_tiles, const int32_t *__restrict__ col, const double *__restrict__ val,
+    const uint32_t *__restrict__ flags, const int32_t *__restrict__ tile_ord,
+    const int32_t *__restrict__ nzrow, int64_t n_nonempty, const double *__restrict__ x,
+    double *__restrict__ y, double *__restrict__ head, double *__restrict__ tail,
+    int32_t *__restrict__ tail_ord) {
+    static_assert(SIGMA % 4 == 0 && SIGMA <= 32, "sigma");
+    constexpr int Q = SIGMA / 4;
+    const int64_t tile = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (tile >= n_tiles) return;  // wave-uniform
+    const int64_t base = tile * 64 * SIGMA;
+    const uint32_t f = flags[tile * 64 + lane];
+    const int32_t *cp = col + base + lane * 4;
+    const double *vp = val + base + lane * 4;
+
+    i32x4 c[Q];
+    f64x2 a[Q], b[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+        c[q] = ld_stream4(cp + q * 256);
+        a[q] = ld_stream2(vp + q * 256);
+        b[q] = ld_stream2(vp + q * 256 + 2);
+    }
+    double g[SIGMA];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+        g[4 * q + 0] = ld_x(x, c[q].x);
+        g[4 * q + 1] = ld_x(x, c[q].y);
+        g[4 * q + 2] = ld_x(x, c[q].z);
+        g[4 * q + 3] = ld_x(x, c[q].w);
+    }
+
+    const int pc = __builtin_popcount(f);
+    const int incl = wave_inclusive_sum(pc, lane);
+    const int64_t ord0 = (int64_t)tile_ord[tile] + (incl - pc);  // this lane's first start
+
+    double run = 0.0, head_l = 0.0;
+    int seen = 0;
+#pragma unroll
+    for (int k = 0; k < SIGMA; ++k) {
+        if ((f >> k) & 1u) {
+            if (seen == 0) head_l = run;
+            else ss_store(y, nzrow, n_nonempty, ord0 + seen - 1, run);
+            run = 0.0;
+            ++seen;
+        }
+        const double v = (k & 2) ? ((k & 1) ? b[k >> 2].y : b[k >> 2].x)
+                                 : ((k & 1) ? a[k >> 2].y : a[k >> 2].x);
+        run = madd(v, g[k], run);
+    }
+
+    const bool has = f != 0u;
+    const double S = wave_seg_scan(run, has, lane);  // open-segment sum at lane end
+    double C = __shfl_up(S, 1, 64);
+    if (lane == 0) C = 0.0;
+    const uint64_t ball = __ballot(has);
+    const bool started_before = (ball & ((1ull << lane) - 1ull)) != 0ull;
+    if (has) {
+        const double tot = __dadd_rn(C, head_l);
+        if (started_before) ss_store(y, nzrow, n_nonempty, ord0 - 1, tot);
+        else head[tile] = tot;  // exactly one lane: the first lane with a start
+    }
+    if (lane == 63) {
+        if (ball == 0ull) {
+            head[tile] = S;  // the whole tile continues an earlier row
+            tail_ord[tile] = -1;
+        } else {
+            tail[tile] = S;
+            tail_ord[tile] = tile_ord[tile] + incl - 1;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void ss_fixup_kernel(int64_t n_tiles, const double *__restrict__ head,
+                                                       const double *__restrict__ tail,
+                                                       const int32_t *__restrict__ tail_ord,
+                                                       const int32_t *__restrict__ nzrow,
+                                                       int64_t n_nonempty,
+                                                       const int32_t *__restrict__ empty_rows,
+                                                       int64_t n_empty, double *__restrict__ y) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < n_tiles) {
+        const int32_t ord = tail_ord[t];
+        if (ord >= 0 && ord < n_nonempty) {
+            double s = tail[t];
+            for (int64_t u = t + 1; u < n_tiles; ++u) {
+                s = __dadd_rn(s, head[u]);
+                if (tail_ord[u] >= 0) break;
+            }
+            y[nzrow ? (int64_t)nzrow[ord] : (int64_t)ord] = s;
+        }
+    }
+    if (t < n_empty) y[empty_rows[t]] = 0.0;
+}
+
+template <int SIGMA>
+static void launch_ss_t(const spmv_plan_s *p, const double *x, double *y) {
+    const SsDev &s = p->ss;
+    const int64_t blocks = (s.n_tiles + 3) / 4;
+    hipLaunchKernelGGL((ss_tile_kernel<SIGMA>), dim3((unsigned)blocks), dim3(256), 0, p->stream,
+                       s.n_tiles, s.col, s.val, s.flags, s.tile_ord, s.nzrow, s.n_nonempty, x, y,
+                       s.head, s.tail, s.tail_ord);
+}
+
+int launch_ss(const spmv_plan_s *p, const double *x, double *y) {
+    const SsDev &s = p->ss;
+    if (s.n_tiles > 0) {
+        switch (s.sigma) {
+            case 4: launch_ss_t<4>(p, x, y); break;
+            case 8: launch_ss_t<8>(p, x, y); break;
+            case 12: launch_ss_t<12>(p, x, y); break;
+            case 16: launch_ss_t<16>(p, x, y); break;
+            case 20: launch_ss_t<20>(p, x, y); break;
+            case 24: launch_ss_t<24>(p, x, y); break;
+            case 32: launch_ss_t<32>(p, x, y); break;
+            default: set_error("ss sigma must be one of 4,8,12,16,20,24,32"); return SPMV_ERROR_INVALID_VALUE;
+        }
+        SPMV_HIP_TRY(hipGetLastError());
+    }
+    const int64_t work = s.n_tiles > s.n_empty ? s.n_tiles : s.n_empty;
+    if (work > 0) {
+        hipLaunchKernelGGL(ss_fixup_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0,
+                           p->stream, s.n_tiles, s.head, s.tail, s.tail_ord, s.nzrow, s.n_nonempty,
+                           s.empty_rows, s.n_empty, y);
+        SPMV_HIP_TRY(hipGetLastError());
+    }
+    return SPMV_SUCCESS;
+}
+
+}  // namespace spmv

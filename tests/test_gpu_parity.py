@@ -1,0 +1,242 @@
+"""Parity of the HIP kernels (through the C-ABI) against the oracle and the
+reference golden vectors.  Needs an MI355X: `pytest -m gpu`.
+
+Tolerances (BASELINE north star: within 1e-6 relative fp64):
+* every result must pass the reference VerifyResult criterion
+  (src/util.cpp:67-83: a row fails iff abs > 1e-6 AND rel > 1e-6);
+* non-negative inputs: |y - y_ref| <= 1e-12 * |y_ref| + 1e-300 per row;
+* integer-valued inputs and sequential-order formats (ELL, DIA, 1-lane CSR):
+  bit-exact against the oracle's sequential row sum;
+* every format is idempotent: two calls over a garbage y give identical y
+  (the two-call verification of src/main.cpp:40-56).
+"""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+import singlespmv_amd as sp
+from conftest import golden_names, load_golden
+
+pytestmark = pytest.mark.gpu
+
+FORMATS = ["csr", "ell", "ss", "hyb", "dia", "auto"]
+REL = 1e-12
+
+
+def oracle_y(rp, col, val, x):
+    return oracle.csr_spmv(np.ascontiguousarray(rp, np.int64), np.ascontiguousarray(col, np.int32),
+                           np.ascontiguousarray(val, np.float64), np.ascontiguousarray(x, np.float64))
+
+
+def check_close(y, yref, rel=REL, what=""):
+    err = np.abs(y - yref)
+    tol = rel * np.abs(yref) + 1e-300
+    bad = np.flatnonzero(err > np.maximum(tol, 0))
+    # allow exact-zero rows with tiny absolute error only for signed inputs
+    assert len(bad) == 0, f"{what}: {len(bad)} rows off, first {bad[:5]}: {y[bad[:5]]} vs {yref[bad[:5]]}"
+
+
+def run_plan(plan, x, m, garbage=1.2345e300):
+    y = np.full(m, garbage)
+    plan.execute(x, y)
+    y2 = np.full(m, -garbage)
+    plan.execute(x, y2)
+    assert np.array_equal(y, y2, equal_nan=True), "not idempotent / depends on prior y"
+    return y
+
+
+def make_plan(m, n, rp, col, val, fmt, **kw):
+    try:
+        return sp.Plan.from_csr(m, n, rp, col, val, fmt=fmt, **kw)
+    except sp.SpmvError as e:
+        if fmt == "dia" and "not supported" in str(e):
+            return None
+        raise
+
+
+@pytest.mark.parametrize("name", golden_names())
+@pytest.mark.parametrize("fmt", FORMATS)
+def test_golden(name, fmt):
+    g = load_golden(name)
+    m, n = int(g["m"]), int(g["n"])
+    rp = sp.coo_to_csr(m, g["row"])
+    plan = make_plan(m, n, rp, g["col"], g["val"], fmt)
+    if plan is None:
+        pytest.skip("DIA refuses this matrix (too many diagonals)")
+    y = run_plan(plan, g["x"], m)
+    A = sp.SpMat(m, n, g["row"], g["col"], g["val"])
+    assert sp.verify_result(A, g["x"], y), "VerifyResult (1e-6) failed"
+    yref = g["y_crs"]
+    signed = (g["val"] < 0).any() or (g["x"] < 0).any()
+    if name == "syn_integer":
+        assert np.array_equal(y, yref), "integer-valued inputs must be exact"
+    elif not signed:
+        check_close(y, yref, what=f"{name}/{fmt}")
+    info = plan.info()
+    if info["format"] in ("ell", "dia") or (info["format"] == "csr" and info["csr_lanes"] == 1):
+        assert np.array_equal(y, yref), f"{info['format']} is sequential: must be bit-exact"
+
+
+@pytest.mark.parametrize("lanes", [1, 2, 4, 8, 16, 32, 64])
+def test_csr_lanes(lanes):
+    spec = sp.gen_spec("powerlaw", 20000, max_len=3000, seed=11)
+    rp, col, val = sp.generate_csr(spec)
+    x = sp.generate_vector(20000, seed=5)
+    y = run_plan(sp.Plan.from_csr(20000, 20000, rp, col, val, "csr", csr_lanes=lanes), x, 20000)
+    yo = oracle_y(rp, col, val, x)
+    check_close(y, yo, what=f"lanes={lanes}")
+    if lanes == 1:
+        assert np.array_equal(y, yo)
+
+
+@pytest.mark.parametrize("sigma", [4, 8, 12, 16, 20, 24, 32])
+@pytest.mark.parametrize("kind", ["powerlaw", "uniform", "empty_rows"])
+def test_ss_sigma(sigma, kind):
+    m = 30011
+    if kind == "empty_rows":
+        spec = sp.gen_spec("powerlaw", m, max_len=500, seed=13)
+        rp, col, val = sp.generate_csr(spec)
+        rng = np.random.default_rng(sigma)
+        lens = np.diff(rp)
+        zero = rng.random(m) < 0.1
+        zero[:7] = True
+        zero[-9:] = True
+        keep = np.repeat(~zero, lens)
+        col, val = np.ascontiguousarray(col[keep]), np.ascontiguousarray(val[keep])
+        rp = np.concatenate([[0], np.cumsum(np.where(zero, 0, lens))]).astype(np.int64)
+    else:
+        spec = sp.gen_spec(kind, m, per_row=13, max_len=4000, seed=17)
+        rp, col, val = sp.generate_csr(spec)
+    x = sp.generate_vector(m, seed=19)
+    plan = sp.Plan.from_csr(m, m, rp, col, val, "ss", ss_sigma=sigma)
+    y = run_plan(plan, x, m)
+    check_close(y, oracle_y(rp, col, val, x), what=f"ss sigma={sigma} {kind}")
+
+
+@pytest.mark.parametrize("width", [0, 4, 8, 24, 64])
+def test_hyb_widths(width):
+    m = 25000
+    spec = sp.gen_spec("powerlaw", m, max_len=6000, seed=23)
+    rp, col, val = sp.generate_csr(spec)
+    x = sp.generate_vector(m, seed=29)
+    plan = sp.Plan.from_csr(m, m, rp, col, val, "hyb", ell_width=width)
+    info = plan.info()
+    assert info["n_kernels"] in (1, 2)
+    y = run_plan(plan, x, m)
+    check_close(y, oracle_y(rp, col, val, x), what=f"hyb K={width}")
+
+
+def test_dia_banded_bit_exact_and_refusal():
+    m = 50000
+    spec = sp.gen_spec("banded", m, band_lo=-32, band_hi=31, seed=31)
+    rp, col, val = sp.generate_csr(spec)
+    x = sp.generate_vector(m, seed=37)
+    plan = sp.Plan.from_csr(m, m, rp, col, val, "dia")
+    assert plan.info()["n_diags"] == 64
+    y = run_plan(plan, x, m)
+    assert np.array_equal(y, oracle_y(rp, col, val, x))
+    # AUTO picks DIA for a banded matrix
+    assert sp.Plan.from_csr(m, m, rp, col, val, "auto").info()["format"] == "dia"
+    # a uniform random matrix is refused by DIA
+    rp2, col2, val2 = sp.generate_csr(sp.gen_spec("uniform", 5000, per_row=8))
+    with pytest.raises(sp.SpmvError, match="not supported"):
+        sp.Plan.from_csr(5000, 5000, rp2, col2, val2, "dia")
+
+
+def test_integer_exact_all_formats():
+    m = 40000
+    spec = sp.gen_spec("powerlaw", m, max_len=2000, integer_values=True, seed=41)
+    rp, col, val = sp.generate_csr(spec)
+    x = sp.generate_vector(m, seed=43, integer_values=True)
+    yo = oracle_y(rp, col, val, x)
+    for fmt in ["csr", "ell", "ss", "hyb"]:
+        y = run_plan(sp.Plan.from_csr(m, m, rp, col, val, fmt), x, m)
+        assert np.array_equal(y, yo), fmt
+
+
+def test_rectangular_and_empty():
+    rng = np.random.default_rng(3)
+    for m, n in [(1, 1), (7, 1000), (1000, 7), (0, 5), (5, 1)]:
+        lens = rng.integers(0, 5, size=m)
+        rp = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+        col = rng.integers(0, n, size=rp[-1]).astype(np.int32)
+        val = rng.random(rp[-1])
+        x = rng.random(n)
+        yo = oracle_y(rp, col, val, x) if m else np.zeros(0)
+        for fmt in ["csr", "ell", "ss", "hyb"]:
+            plan = sp.Plan.from_csr(m, n, rp, col, val, fmt)
+            y = np.full(m, 7.0)
+            plan.execute(x, y)
+            check_close(y, yo, what=f"{m}x{n} {fmt}")
+    # all-empty matrix: y = 0
+    plan = sp.Plan.from_csr(4, 4, np.zeros(5, np.int64), np.zeros(0, np.int32), np.zeros(0), "ss")
+    y = np.full(4, 3.0)
+    plan.execute(np.ones(4), y)
+    assert (y == 0).all()
+
+
+def test_device_pointers_and_streams():
+    import torch
+    m = 100000
+    rp, col, val = sp.generate_csr(sp.gen_spec("uniform", m, per_row=16, seed=2))
+    x = sp.generate_vector(m, seed=3)
+    yo = oracle_y(rp, col, val, x)
+    for fmt in ["csr", "ell", "ss"]:
+        plan = sp.Plan.from_csr(m, m, rp, col, val, fmt)
+        xd = torch.from_numpy(x).cuda()
+        yd = torch.full((m,), float("nan"), dtype=torch.float64, device="cuda")
+        s = torch.cuda.Stream()
+        plan.set_stream(s)
+        with torch.cuda.stream(s):
+            plan.execute(xd, yd)
+        torch.cuda.synchronize()
+        check_close(yd.cpu().numpy(), yo, what=fmt)
+        ms = plan.time(xd, yd, 3)
+        assert ms > 0
+
+
+def test_dropin_optimizeproblem_spmv():
+    """The reference-signature drop-in (include/opt_hip.h) via libopt_hip.so."""
+    class SpMatC(C.Structure):
+        _fields_ = [("nRow", C.c_int), ("nCol", C.c_int), ("nNnz", C.c_int),
+                    ("row_idx", C.c_void_p), ("col_idx", C.c_void_p), ("val", C.c_void_p)]
+
+    class VecC(C.Structure):
+        _fields_ = [("size", C.c_int), ("val", C.c_void_p)]
+
+    class SpMatOptC(C.Structure):
+        _fields_ = [("nRow", C.c_int), ("nCol", C.c_int), ("nNnz", C.c_int), ("plan", C.c_void_p),
+                    ("format", C.c_int), ("d_x", C.c_void_p), ("x_uploaded", C.c_int)]
+
+    sp.lib()
+    L = C.CDLL(sp.OPT_LIB_PATH)
+    opt = getattr(L, "_Z15OptimizeProblemRK5SpMatRK3VecR8SpMatOptR6VecOpt")
+    g = load_golden("mtx_random")
+    m, n = int(g["m"]), int(g["n"])
+    row, col, val, x = (np.ascontiguousarray(g[k]) for k in ("row", "col", "val", "x"))
+    A = SpMatC(m, n, len(val), row.ctypes.data, col.ctypes.data, val.ctypes.data)
+    xv = VecC(n, x.ctypes.data)
+    y = np.full(m, 99.0)
+    yv = VecC(m, y.ctypes.data)
+    Ao, xo = SpMatOptC(), VecC()
+    opt(C.byref(A), C.byref(xv), C.byref(Ao), C.byref(xo))
+    assert xo.val == x.ctypes.data  # x_opt aliases x (src/opt_crs.cpp:11-12)
+    for _ in range(2):
+        L.SpMV(C.byref(Ao), C.byref(xo), C.byref(yv))
+        assert sp.verify_result(sp.SpMat(m, n, row, col, val), x, y)
+    check_close(y, g["y_crs"])
+    L.SpMVRelease(C.byref(Ao))
+
+
+def test_driver_binary_reports_block():
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    mtx = os.path.join(root, "tests", "golden", "mtx", "random.mtx")
+    out = subprocess.run([os.path.join(root, "bin", "spmv"), mtx, "--format", "ss"],
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr + out.stdout
+    assert "++++" in out.stdout and "Performance(GFLOPS)" in out.stdout
+    assert "MatrixFormat\tSS" in out.stdout.replace(" ", "")
