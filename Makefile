@@ -14,7 +14,7 @@ JOBS     ?= 8
 ROCM     ?= /opt/rocm
 CXXFLAGS  = -O3 -std=c++17 -fPIC -fopenmp -Wall -Wno-unused-result -Iinclude -I$(ROCM)/include \
             -Isinglespmv_amd/csrc
-HIPFLAGS  = $(CXXFLAGS) --offload-arch=$(ARCH) -munsafe-fp-atomics
+HIPFLAGS  = $(CXXFLAGS) --offload-arch=$(ARCH) -munsafe-fp-atomics -ffp-contract=off
 
 CSRC      = singlespmv_amd/csrc
 LIB       = singlespmv_amd/libspmv_hip.so
@@ -27,15 +27,15 @@ KERN_OBJ  = $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(KERN_SRC))
 HDRS      = include/spmv_hip.h include/opt_hip.h include/spmv_util.h \
             $(CSRC)/internal.hpp $(CSRC)/device.hpp
 
-all: $(LIB) $(OPTLIB) bin/spmv oracle
+all: $(LIB) $(OPTLIB) bin/spmv bin/gather_probe oracle
 
 $(OBJDIR):
 	mkdir -p $(OBJDIR)
 
-$(OBJDIR)/%.o: $(CSRC)/%.cpp $(HDRS) | $(OBJDIR)
+$(OBJDIR)/%.o: $(CSRC)/%.cpp $(HDRS) Makefile | $(OBJDIR)
 	$(HIPCC) $(CXXFLAGS) -x c++ -D__HIP_PLATFORM_AMD__ -c $< -o $@
 
-$(OBJDIR)/%.o: $(CSRC)/%.hip $(HDRS) | $(OBJDIR)
+$(OBJDIR)/%.o: $(CSRC)/%.hip $(HDRS) Makefile | $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(LIB): $(HOST_OBJ) $(KERN_OBJ)
@@ -52,6 +52,11 @@ bin/spmv: tools/spmv_main.cpp $(CSRC)/opt_hip.cpp $(LIB) $(HDRS)
 $(OPTLIB): $(CSRC)/opt_hip.cpp $(LIB) $(HDRS)
 	$(HIPCC) $(CXXFLAGS) -x c++ -D__HIP_PLATFORM_AMD__ -shared -o $@ $(CSRC)/opt_hip.cpp \
 	    -Lsinglespmv_amd -lspmv_hip -Wl,-rpath,'$$ORIGIN'
+
+# x-gather micro-benchmark (tools/gather_probe.hip)
+bin/gather_probe: tools/gather_probe.hip Makefile
+	mkdir -p bin
+	$(HIPCC) $(HIPFLAGS) -o $@ $<
 
 oracle:
 	$(MAKE) -s -C oracle all

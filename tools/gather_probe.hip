@@ -1,0 +1,160 @@
+// gather_probe.hip -- micro-benchmark of the x-gather that bounds SpMV on
+// MI355X (SURVEY §7 hard part 1: "measure first").
+//
+// Every experiment streams N int32 indices (like col_idx) and gathers 8-byte
+// doubles from a table of T bytes (like x), one gather per index, 8 in
+// flight per lane, grid-stride so concurrently resident waves sit at nearby
+// stream positions.  Reports G gathers/s and the streamed GB/s.
+//
+//   e1: uniform random indices over T  (T = 1 MB .. 2 GB)
+//   e2: T = 80 MB, indices confined to a W-byte window that slides across the
+//       table with the stream position (a synchronised column sweep)
+//   e3: HBM streaming read ceiling (dwordx4), for calibration
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+
+#define CK(x)                                                                       \
+    do {                                                                            \
+        hipError_t e = (x);                                                         \
+        if (e != hipSuccess) {                                                      \
+            std::fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e)); \
+            std::exit(1);                                                           \
+        }                                                                           \
+    } while (0)
+
+__device__ __forceinline__ unsigned long long mix(unsigned long long z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+// idx[i] = base(i) + hash(i) % W  where base slides from 0 to T-W over the stream
+__global__ void make_idx(int *idx, long long n, long long tab_elems, long long win_elems) {
+    long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; i < n; i += (long long)gridDim.x * blockDim.x) {
+        long long base = (win_elems >= tab_elems) ? 0 : (long long)((double)i / (double)n * (double)(tab_elems - win_elems));
+        idx[i] = (int)(base + (long long)(mix((unsigned long long)i) % (unsigned long long)win_elems));
+    }
+}
+
+template <int U>
+__global__ __launch_bounds__(256) void gather(const int *__restrict__ idx, const double *__restrict__ tab,
+                                              double *__restrict__ out, long long n) {
+    const long long G = (long long)gridDim.x * blockDim.x;
+    long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    double acc = 0;
+    for (long long i = t; i < n; i += G * U) {
+        int c[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            long long j = i + u * G;
+            c[u] = j < n ? __builtin_nontemporal_load(idx + j) : 0;
+        }
+        double g[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) g[u] = tab[c[u]];
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc += g[u];
+    }
+    out[t] = acc;
+}
+
+__global__ __launch_bounds__(256) void stream_read(const f64x2 *__restrict__ a, double *__restrict__ out, long long n2) {
+    const long long G = (long long)gridDim.x * blockDim.x;
+    long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    double acc = 0;
+    for (long long i = t; i < n2; i += G * 4) {
+        f64x2 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            long long j = i + u * G;
+            v[u] = j < n2 ? __builtin_nontemporal_load(a + j) : f64x2{0, 0};
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc += v[u].x + v[u].y;
+    }
+    out[t] = acc;
+}
+
+static float time_gather(const int *idx, const double *tab, double *out, long long n, int blocks) {
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    hipLaunchKernelGGL(gather<8>, dim3(blocks), dim3(256), 0, 0, idx, tab, out, n);
+    CK(hipDeviceSynchronize());
+    float best = 1e30f;
+    for (int r = 0; r < 5; ++r) {
+        CK(hipEventRecord(a));
+        hipLaunchKernelGGL(gather<8>, dim3(blocks), dim3(256), 0, 0, idx, tab, out, n);
+        CK(hipEventRecord(b));
+        CK(hipEventSynchronize(b));
+        float ms;
+        CK(hipEventElapsedTime(&ms, a, b));
+        if (ms < best) best = ms;
+    }
+    return best;
+}
+
+int main(int argc, char **argv) {
+    const long long N = argc > 1 ? atoll(argv[1]) : 160000000LL;
+    const long long TMAX = 2048LL << 20;
+    int *idx;
+    double *tab, *out;
+    const int blocks = 256 * 8;
+    CK(hipMalloc(&idx, sizeof(int) * N));
+    CK(hipMalloc(&tab, TMAX));
+    CK(hipMalloc(&out, sizeof(double) * blocks * 256));
+    CK(hipMemset(tab, 0, TMAX));
+    std::printf("{\"N\": %lld, \"e1\": [", N);
+    const long long mbs[] = {1, 2, 4, 8, 16, 32, 64, 80, 128, 192, 256, 384, 512, 1024, 2048};
+    bool first = true;
+    for (long long mb : mbs) {
+        const long long te = (mb << 20) / 8;
+        hipLaunchKernelGGL(make_idx, dim3(4096), dim3(256), 0, 0, idx, N, te, te);
+        CK(hipDeviceSynchronize());
+        const float ms = time_gather(idx, tab, out, N, blocks);
+        std::printf("%s{\"table_MB\": %lld, \"ms\": %.4f, \"Ggather_s\": %.2f}", first ? "" : ", ", mb, ms,
+                    N / (ms * 1e-3) / 1e9);
+        first = false;
+        std::fflush(stdout);
+    }
+    std::printf("], \"e2\": [");
+    first = true;
+    const long long te80 = (80LL << 20) / 8;
+    const double wins[] = {0.25, 0.5, 1, 2, 4, 8, 16, 80};
+    for (double w : wins) {
+        const long long we = (long long)(w * (1 << 20)) / 8;
+        hipLaunchKernelGGL(make_idx, dim3(4096), dim3(256), 0, 0, idx, N, te80, we);
+        CK(hipDeviceSynchronize());
+        const float ms = time_gather(idx, tab, out, N, blocks);
+        std::printf("%s{\"window_MB\": %.2f, \"ms\": %.4f, \"Ggather_s\": %.2f}", first ? "" : ", ", w, ms,
+                    N / (ms * 1e-3) / 1e9);
+        first = false;
+        std::fflush(stdout);
+    }
+    // e3: streaming read of 2 GB
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    const long long n2 = TMAX / 16;
+    hipLaunchKernelGGL(stream_read, dim3(blocks), dim3(256), 0, 0, (const f64x2 *)tab, out, n2);
+    CK(hipDeviceSynchronize());
+    float best = 1e30f;
+    for (int r = 0; r < 5; ++r) {
+        CK(hipEventRecord(a));
+        hipLaunchKernelGGL(stream_read, dim3(blocks), dim3(256), 0, 0, (const f64x2 *)tab, out, n2);
+        CK(hipEventRecord(b));
+        CK(hipEventSynchronize(b));
+        float ms;
+        CK(hipEventElapsedTime(&ms, a, b));
+        if (ms < best) best = ms;
+    }
+    std::printf("], \"e3_stream_GBs\": %.1f}\n", TMAX / (best * 1e-3) / 1e9);
+    return 0;
+}
