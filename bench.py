@@ -48,10 +48,13 @@ def parse():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--rows", type=int, default=0, help="rows per GPU (default: the config's)")
-    ap.add_argument("--formats", default="auto,csr,ell,ss",
+    ap.add_argument("--formats", default="auto,csr,ell,ss,css",
                     help="first entry is the headline plan; the rest are reported alongside")
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     ap.add_argument("--cpu-seconds", type=float, default=2.0)
+    ap.add_argument("--sim-world", type=int, default=0,
+                    help="development: run rank 0's share of a K-GPU job on one GPU "
+                         "(n = K * rows); the JSON marks it as emulated")
     return ap.parse_args()
 
 
@@ -61,6 +64,7 @@ def main():
     import torch.distributed as dist
 
     import singlespmv_amd as sp
+    from singlespmv_amd import dist as sdist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -76,17 +80,16 @@ def main():
 
     gen_kw, desc, rows_default = CONFIGS[args.config]
     rows = args.rows or rows_default
-    m_glob = rows * world
+    shape_world = args.sim_world if (args.sim_world and world == 1) else world
+    m_glob = rows * shape_world
     n_glob = m_glob
-    row0, row1 = rank * rows, (rank + 1) * rows
-
     t0 = time.time()
     kind = gen_kw["kind"]
     spec = sp.gen_spec(kind, m_glob, n_glob, per_row=gen_kw.get("per_row", 16),
                        max_len=gen_kw.get("max_len", 10000), alpha=gen_kw.get("alpha", 2.0),
                        band_lo=gen_kw.get("band_lo", -32), band_hi=gen_kw.get("band_hi", 31),
                        seed=42)
-    rp, col, val = sp.generate_csr(spec, row0, row1)
+    (row0, row1), rp, col, val = sdist.shard_generated(spec, rank, shape_world)
     nnz_local = int(rp[-1])
     t_gen = time.time() - t0
 
@@ -99,7 +102,7 @@ def main():
         torch.cuda.synchronize()
         dist.barrier()
         tb = time.perf_counter()
-        dist.broadcast(x, src=0)
+        sdist.replicate_x(x, src=0)
         torch.cuda.synchronize()
         t_bcast = time.perf_counter() - tb
     y = torch.empty(rows, dtype=torch.float64, device=dev)
@@ -168,15 +171,14 @@ def main():
     # y gather (RCCL all_gather over xGMI), timed separately from the kernel
     coll_ms = None
     if distributed:
-        yall = torch.empty(rows * world, dtype=torch.float64, device=dev)
         for _ in range(3):
-            dist.all_gather_into_tensor(yall, y_head)
+            sdist.gather_y(y_head, rows)
         torch.cuda.synchronize()
         dist.barrier()
         tc = time.perf_counter()
         reps = 10
         for _ in range(reps):
-            dist.all_gather_into_tensor(yall, y_head)
+            sdist.gather_y(y_head, rows)
         torch.cuda.synchronize()
         coll_ms = (time.perf_counter() - tc) / reps * 1e3
 
@@ -229,6 +231,9 @@ def main():
         "collective_ms": coll_ms,
         "max_rel_err_vs_cpu": max_rel,
     }
+    if shape_world != world:
+        out["emulated_world"] = shape_world
+        out["config"]["parallelism"] = f"EMULATED rank 0 of {shape_world} (development only)"
     traffic_file = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(traffic_file):
         try:

@@ -67,7 +67,9 @@ typedef enum spmv_format {
     SPMV_FORMAT_ELL = 2,  /* opt_ell   (src/opt_ell.cpp), device: sliced ELL    */
     SPMV_FORMAT_SS = 3,   /* opt_ss / CSR5: segmented sum over 64 x sigma tiles */
     SPMV_FORMAT_DIA = 4,  /* opt_dia   (src/opt_dia.cpp), device: row-indexed   */
-    SPMV_FORMAT_HYB = 5   /* ELL(K) + CSR overflow (BASELINE config 3)          */
+    SPMV_FORMAT_HYB = 5,  /* ELL(K) + CSR overflow (BASELINE config 3)          */
+    SPMV_FORMAT_CSS = 6   /* opt_css lineage: column-slab sweep, y in LDS, x    */
+                          /* slab L2-resident per XCD (large random matrices)  */
 } spmv_format_t;
 
 typedef struct spmv_plan_s *spmv_plan_t;
@@ -80,7 +82,10 @@ typedef struct spmv_options {
     int32_t ss_sigma;   /* SS: nnz per lane per tile, 0 = auto                 */
     int32_t dia_max_diags; /* DIA: refuse beyond this many diagonals (0 = 1024) */
     double dia_max_fill;   /* DIA: refuse when stored/nnz exceeds this (0 = 3) */
-    int32_t reserved[8];
+    int32_t css_slab_shift; /* CSS: slab = 2^shift columns (0 = 18, 2 MiB of x) */
+    int32_t css_lag;        /* CSS: pacing slack in slabs (0 = 4, -1 = no pacing) */
+    int32_t css_pace;       /* CSS: 0/1 pace against every XCD, 2 own XCD only */
+    int32_t reserved[5];
 } spmv_options_t;
 
 /* Fill `opt` with defaults (AUTO format, current device, auto tuning). */
@@ -135,6 +140,8 @@ typedef struct spmv_plan_info {
     int32_t ell_width;       /* ELL: max slice width; HYB: K                   */
     int32_t ss_sigma;
     int32_t n_diags;         /* DIA                                            */
+    int32_t css_passes;      /* CSS: row passes, slabs per pass                */
+    int32_t css_slabs;
     int32_t n_kernels;       /* launches per execute                           */
     int64_t overflow_nnz;    /* HYB: entries outside the ELL part              */
     int64_t empty_rows;

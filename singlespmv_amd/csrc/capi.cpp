@@ -91,6 +91,7 @@ static int create_from_csr(const HostCsr &A, const spmv_options_t *opt_in, spmv_
         case SPMV_FORMAT_HYB: st = build_hyb(p, A, o); break;
         case SPMV_FORMAT_SS: st = build_ss(p, A, o); break;
         case SPMV_FORMAT_DIA: st = build_dia(p, A, o); break;
+        case SPMV_FORMAT_CSS: st = build_css(p, A, o); break;
         default:
             set_error("unknown format");
             st = SPMV_ERROR_INVALID_VALUE;
@@ -114,6 +115,7 @@ static int dispatch(const spmv_plan_s *p, const double *x, double *y) {
             return launch_hyb_overflow(p, x, y);
         case SPMV_FORMAT_SS: return launch_ss(p, x, y);
         case SPMV_FORMAT_DIA: return launch_dia(p, x, y);
+        case SPMV_FORMAT_CSS: return launch_css(p, x, y);
     }
     set_error("plan has an unknown format");
     return SPMV_ERROR_INVALID_VALUE;
@@ -270,6 +272,8 @@ int spmv_plan_info(spmv_plan_t p, spmv_plan_info_t *info) {
     info->ell_width = p->ell.max_width;
     info->ss_sigma = p->ss.sigma;
     info->n_diags = p->dia.n_diags;
+    info->css_passes = p->css.P;
+    info->css_slabs = p->css.S;
     info->n_kernels = p->n_kernels;
     info->overflow_nnz = p->hyb.nnz;
     info->empty_rows = p->empty_rows;

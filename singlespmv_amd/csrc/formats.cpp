@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <numeric>
@@ -342,6 +343,146 @@ int build_dia(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
     return SPMV_SUCCESS;
 }
 
+// ---------------------------------------------------------------- CSS
+// Column-slab sweep (k_css.hip).  Rows are cut into passes x workgroups x
+// waves; every wave's entries are sorted by column and packed into 64-entry
+// chunks with distinct rows (a row whose entry would repeat inside a chunk is
+// deferred, together with its later entries, so per-row column order holds).
+namespace {
+struct CssEntry {
+    int32_t col;
+    uint16_t row;
+    double val;
+};
+}  // namespace
+
+int build_css(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
+    CssDev &c = p->css;
+    int ncu = 0;
+    SPMV_HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, p->device));
+    c.nwg = ncu > 0 ? ncu : 256;
+    constexpr int W = kCssWorkers;
+    const int64_t per_pass = (int64_t)c.nwg * kCssMaxRows;
+    c.P = (int)std::max<int64_t>(1, (A.m + per_pass - 1) / per_pass);
+    c.R = (int)std::max<int64_t>(1, (A.m + (int64_t)c.P * c.nwg - 1) / ((int64_t)c.P * c.nwg));
+    if (o.css_slab_shift > 0) {
+        c.slab_shift = o.css_slab_shift;
+    } else {
+        // narrowest slab that still gives every worker wave ~384 entries per
+        // slab: pacing finer than that is pure overhead (measured sweep,
+        // profiles/r02: 2^18 columns for config 2, wider as n grows)
+        const double per_wave = (double)std::max<int64_t>(A.nnz, 1) / ((double)c.nwg * W * c.P * 384.0);
+        c.slab_shift = 14;
+        while (c.slab_shift < 24 && (double)((A.n + ((int64_t)1 << c.slab_shift) - 1) >> c.slab_shift) > per_wave)
+            ++c.slab_shift;
+    }
+    if (c.slab_shift < 8 || c.slab_shift > 30) {
+        set_error("css_slab_shift must be in [8, 30]");
+        return SPMV_ERROR_INVALID_VALUE;
+    }
+    c.S = (int)std::max<int64_t>(1, (A.n + ((int64_t)1 << c.slab_shift) - 1) >> c.slab_shift);
+    c.lag = o.css_lag == 0 ? 4 : (o.css_lag < 0 ? 0 : o.css_lag);
+    // pace against every XCD when x outgrows half the 256 MiB Infinity Cache:
+    // then the 8 XCDs must sweep the same slab for the MALL to serve 7 of 8
+    c.pace_all = o.css_pace == 2 ? 0 : 1;
+    const int64_t nblocks = (int64_t)c.P * c.nwg;
+    const int64_t nlists = nblocks * W;
+    std::vector<int64_t> woff((size_t)nlists + 1, 0);
+    auto block_rows = [&](int64_t pb, int64_t &r0, int &rows) {
+        r0 = pb * c.R;
+        const int64_t rem = A.m - r0;
+        rows = rem <= 0 ? 0 : (int)std::min<int64_t>(rem, c.R);
+    };
+    // rows of a block go to the worker waves longest-first onto the least
+    // loaded wave (LPT), so one long row does not leave 14 waves idle
+    std::vector<uint8_t> owner((size_t)std::max<int64_t>(A.m, 1), 0);
+#pragma omp parallel
+    {
+        std::vector<std::pair<int64_t, int>> order;
+#pragma omp for schedule(dynamic, 4)
+        for (int64_t pb = 0; pb < nblocks; ++pb) {
+            int64_t r0;
+            int rows;
+            block_rows(pb, r0, rows);
+            order.clear();
+            for (int l = 0; l < rows; ++l) order.push_back({A.row_ptr[r0 + l + 1] - A.row_ptr[r0 + l], l});
+            std::stable_sort(order.begin(), order.end(),
+                             [](const std::pair<int64_t, int> &a, const std::pair<int64_t, int> &b) { return a.first > b.first; });
+            int64_t load[W] = {0};
+            for (const auto &e : order) {
+                int best = 0;
+                for (int w = 1; w < W; ++w)
+                    if (load[w] < load[best]) best = w;
+                load[best] += e.first;
+                owner[(size_t)(r0 + e.second)] = (uint8_t)best;
+            }
+            for (int w = 0; w < W; ++w) woff[(size_t)(pb * W + w + 1)] = load[w];
+        }
+    }
+    for (int64_t L = 0; L < nlists; ++L) woff[L + 1] += woff[L];
+    const int64_t total = woff[nlists];
+    std::vector<int32_t> col((size_t)std::max<int64_t>(total, 1));
+    std::vector<uint16_t> row((size_t)std::max<int64_t>(total, 1));
+    std::vector<double> val((size_t)std::max<int64_t>(total, 1));
+#pragma omp parallel
+    {
+        std::vector<CssEntry> in, defer, next;
+        std::vector<uint32_t> stamp(kCssMaxRows, 0), blocked(kCssMaxRows, 0);
+        uint32_t epoch = 0;
+#pragma omp for schedule(dynamic, 4)
+        for (int64_t L = 0; L < nlists; ++L) {
+            int64_t r0;
+            int rows;
+            block_rows(L / W, r0, rows);
+            const int w = (int)(L % W);
+            in.clear();
+            for (int l = 0; l < rows; ++l) {
+                if (owner[(size_t)(r0 + l)] != w) continue;
+                for (int64_t j = A.row_ptr[r0 + l]; j < A.row_ptr[r0 + l + 1]; ++j)
+                    in.push_back(CssEntry{A.col[j], (uint16_t)l, A.val[j]});
+            }
+            std::stable_sort(in.begin(), in.end(), [](const CssEntry &a, const CssEntry &b) { return a.col < b.col; });
+            int64_t out = woff[L];
+            size_t idx = 0;
+            defer.clear();
+            while (idx < in.size() || !defer.empty()) {
+                ++epoch;
+                int count = 0;
+                next.clear();
+                auto offer = [&](const CssEntry &e) {
+                    if (count < 64 && stamp[e.row] != epoch && blocked[e.row] != epoch) {
+                        stamp[e.row] = epoch;
+                        col[out] = e.col;
+                        row[out] = e.row;
+                        val[out] = e.val;
+                        ++out;
+                        ++count;
+                    } else {
+                        blocked[e.row] = epoch;
+                        next.push_back(e);
+                    }
+                };
+                for (const CssEntry &e : defer) offer(e);
+                while (count < 64 && idx < in.size()) offer(in[idx++]);
+                defer.swap(next);
+            }
+        }
+    }
+    SPMV_RETURN_IF(upload(p, &c.woff, woff.data(), nlists + 1));
+    SPMV_RETURN_IF(upload(p, &c.col, col.data(), total));
+    SPMV_RETURN_IF(upload(p, &c.row, row.data(), total));
+    SPMV_RETURN_IF(upload(p, &c.val, val.data(), total));
+    std::vector<uint64_t> zeros(8 * 16, 0);
+    SPMV_RETURN_IF(upload(p, &c.prog, zeros.data(), (int64_t)zeros.size()));
+    c.launches = 0;
+    if (const char *d = std::getenv("SPMV_CSS_DEBUG")) c.dbg = std::atoi(d);
+    p->stored_slots = total;
+    p->algo_bytes = 12 * A.nnz + 8 * A.n + 8 * A.m;
+    p->n_kernels = 1;
+    p->kernel_name = "css_sweep_kernel";
+    return SPMV_SUCCESS;
+}
+
 // ---------------------------------------------------------------- AUTO
 int choose_format(const HostCsr &A, const spmv_options_t &o) {
     if (A.m == 0 || A.nnz == 0) return SPMV_FORMAT_CSR;
@@ -355,6 +496,9 @@ int choose_format(const HostCsr &A, const spmv_options_t &o) {
         if (dia_offsets(A, 256, 1.25, offs)) return SPMV_FORMAT_DIA;
     }
     (void)o;
+    // x far beyond one XCD's 4 MiB L2 and enough rows to fill every CU:
+    // random gathers dominate -> column-slab sweep (L2-resident x slabs)
+    if (A.n * 8 > ((int64_t)16 << 20) && A.m >= 256 * 2048 && mean >= 2.0) return SPMV_FORMAT_CSS;
     // near-uniform rows -> sliced ELL; skewed -> segmented sum
     if ((double)maxlen <= 2.0 * mean + 8.0) return SPMV_FORMAT_ELL;
     return SPMV_FORMAT_SS;

@@ -123,6 +123,23 @@ struct DiaDev {
     double *val = nullptr;   // [n_diags * m]
 };
 
+// Column-slab sweep (CSS, k_css.hip).  Per (pass p, workgroup b, wave w) a
+// list of entries (global col int32, local row uint16, val f64) sorted by
+// column, every aligned 64-entry chunk row-distinct; woff[(p*nwg+b)*16+w] is
+// the list start (woff index uses kCssWorkers lists per workgroup).  prog: per-XCD-label pacing counters (uint64, 128 B apart).
+constexpr int kCssMaxRows = 19968;
+constexpr int kCssWorkers = 15;  // worker waves per workgroup (+1 pacer wave)
+struct CssDev {
+    int nwg = 0, R = 0, P = 0, S = 0, slab_shift = 17, lag = 2, pace_all = 0;
+    int64_t *woff = nullptr;
+    int32_t *col = nullptr;
+    uint16_t *row = nullptr;
+    double *val = nullptr;
+    uint64_t *prog = nullptr;
+    uint64_t launches = 0;
+    int dbg = 0;  // ablation switches (SPMV_CSS_DEBUG, internal)
+};
+
 }  // namespace spmv
 
 struct spmv_plan_s {
@@ -136,6 +153,7 @@ struct spmv_plan_s {
     spmv::HybDev hyb;
     spmv::SsDev ss;
     spmv::DiaDev dia;
+    spmv::CssDev css;
     double *x_stage = nullptr;  // host-x staging (opt_cusparse.cpp:44-45)
     double *y_stage = nullptr;
     int64_t stored_slots = 0;
@@ -161,6 +179,7 @@ int build_ell(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o, int cap
 int build_hyb(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o);
 int build_ss(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o);
 int build_dia(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o);
+int build_css(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o);
 int choose_format(const HostCsr &A, const spmv_options_t &o);
 int auto_csr_lanes(double mean_row);
 int auto_ss_sigma(double mean_row);
@@ -171,5 +190,6 @@ int launch_ell(const spmv_plan_s *p, const double *x, double *y);
 int launch_hyb_overflow(const spmv_plan_s *p, const double *x, double *y);
 int launch_ss(const spmv_plan_s *p, const double *x, double *y);
 int launch_dia(const spmv_plan_s *p, const double *x, double *y);
+int launch_css(const spmv_plan_s *p, const double *x, double *y);
 
 }  // namespace spmv

@@ -1,0 +1,66 @@
+"""Multi-GPU plumbing of the SpMV path: one process per GPU over
+torch.distributed (backend "nccl" = RCCL over xGMI on MI355X; "gloo" in the
+CPU tests).
+
+The path shards by rows: every rank owns an nnz-balanced row
+range and keeps global column indices; x is replicated once by a broadcast
+(setup, untimed -- x is fixed across calls, src/main.cpp:36-102); a rank's y
+slice is complete after its local SpMV, and the full y is assembled with one
+all_gather when the caller needs it.
+"""
+from __future__ import annotations
+
+from typing import Tuple
+
+import numpy as np
+
+
+def row_range(m: int, rank: int, world: int, row_ptr=None) -> Tuple[int, int]:
+    """[r0, r1) of `rank`: nnz-balanced when the global row_ptr is known
+    (spmv_partition_rows), otherwise equal row blocks (uniform generators)."""
+    if row_ptr is not None:
+        from . import partition_rows
+        cuts = partition_rows(row_ptr, world)
+        return int(cuts[rank]), int(cuts[rank + 1])
+    per = (m + world - 1) // world
+    return min(m, rank * per), min(m, (rank + 1) * per)
+
+
+def shard_generated(spec, rank: int, world: int):
+    """Generate only this rank's rows of a synthetic matrix (equal blocks)."""
+    from . import generate_csr
+    r0, r1 = row_range(spec.m, rank, world)
+    rp, col, val = generate_csr(spec, r0, r1)
+    return (r0, r1), rp, col, val
+
+
+def shard_csr(row_ptr, col, val, rank: int, world: int):
+    """Cut a global host CSR into this rank's nnz-balanced slice."""
+    m = len(row_ptr) - 1
+    r0, r1 = row_range(m, rank, world, row_ptr)
+    b, e = int(row_ptr[r0]), int(row_ptr[r1])
+    return (r0, r1), (row_ptr[r0:r1 + 1] - b).astype(np.int64), col[b:e], val[b:e]
+
+
+def replicate_x(x, src: int = 0):
+    """Broadcast x from `src` to every rank (RCCL/gloo broadcast), in place."""
+    import torch.distributed as dist
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        dist.broadcast(x, src=src)
+    return x
+
+
+def gather_y(y_local, rows_per_rank: int):
+    """All-gather equal, padded y slices into the full y (length
+    world * rows_per_rank; the caller trims the padding)."""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_initialized() and dist.get_world_size() > 1):
+        return y_local
+    world = dist.get_world_size()
+    if y_local.numel() < rows_per_rank:
+        pad = torch.zeros(rows_per_rank - y_local.numel(), dtype=y_local.dtype, device=y_local.device)
+        y_local = torch.cat([y_local, pad])
+    out = torch.empty(world * rows_per_rank, dtype=y_local.dtype, device=y_local.device)
+    dist.all_gather_into_tensor(out, y_local.contiguous())
+    return out

@@ -1,0 +1,88 @@
+"""World-size-2 (and 3) gloo runs of the multi-GPU path on CPU: row sharding,
+x broadcast, y all-gather -- the same singlespmv_amd.dist code bench.py uses.
+The local SpMV is the oracle's opt_crs restatement (no GPU here); the HIP
+kernel itself is covered by the gpu tests."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import oracle
+import singlespmv_amd as sp
+from singlespmv_amd import dist as sdist
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, kind, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        m = 5003
+        spec = sp.gen_spec(kind, m, per_row=9, max_len=700, seed=5)
+        if kind == "uniform":
+            (r0, r1), rp, col, val = sdist.shard_generated(spec, rank, world)
+        else:  # nnz-balanced cut of a skewed global matrix
+            grp, gcol, gval = sp.generate_csr(spec)
+            (r0, r1), rp, col, val = sdist.shard_csr(grp, gcol, gval, rank, world)
+        x = torch.zeros(m, dtype=torch.float64)
+        if rank == 0:
+            x.copy_(torch.from_numpy(sp.generate_vector(m, seed=6)))
+        sdist.replicate_x(x, 0)
+        y_local = torch.from_numpy(oracle.csr_spmv(rp, col, val, x.numpy()))
+        per = (m + world - 1) // world if kind == "uniform" else None
+        if per is None:  # uneven slices: gather with the max slice length
+            t = torch.tensor([r1 - r0])
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            per = int(t)
+            lens = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+            dist.all_gather(lens, torch.tensor([r1 - r0]))
+            lens = [int(v) for v in lens]
+        else:
+            lens = [min(m, (k + 1) * per) - min(m, k * per) for k in range(world)]
+        yall = sdist.gather_y(y_local, per).numpy()
+        y = np.concatenate([yall[k * per:k * per + lens[k]] for k in range(world)])
+        if rank == 0:
+            grp, gcol, gval = sp.generate_csr(spec)
+            yref = oracle.csr_spmv(grp, gcol, gval, sp.generate_vector(m, seed=6))
+            q.put((np.array_equal(y, yref), float(np.abs(x.numpy() - sp.generate_vector(m, seed=6)).max())))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,kind", [(2, "uniform"), (2, "powerlaw"), (3, "powerlaw")])
+def test_row_sharded_spmv_matches_single_process(world, kind):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, kind, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    exact, xerr = q.get(timeout=10)
+    assert xerr == 0.0, "x broadcast corrupted x"
+    assert exact, "sharded y differs from the single-process opt_crs y"
+
+
+def test_partition_is_nnz_balanced():
+    spec = sp.gen_spec("powerlaw", 40000, max_len=5000, seed=9)
+    rp, _, _ = sp.generate_csr(spec)
+    nnz = rp[-1]
+    loads = []
+    for r in range(8):
+        (r0, r1), _, c, _ = sdist.shard_csr(rp, np.zeros(nnz, np.int32), np.zeros(nnz), r, 8)
+        loads.append(len(c))
+    assert sum(loads) == nnz
+    assert max(loads) - min(loads) <= 5000 + 1  # within one row of perfect

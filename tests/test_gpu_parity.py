@@ -22,7 +22,7 @@ from conftest import golden_names, load_golden
 
 pytestmark = pytest.mark.gpu
 
-FORMATS = ["csr", "ell", "ss", "hyb", "dia", "auto"]
+FORMATS = ["csr", "ell", "ss", "hyb", "dia", "css", "auto"]
 REL = 1e-12
 
 
@@ -76,7 +76,7 @@ def test_golden(name, fmt):
     elif not signed:
         check_close(y, yref, what=f"{name}/{fmt}")
     info = plan.info()
-    if info["format"] in ("ell", "dia") or (info["format"] == "csr" and info["csr_lanes"] == 1):
+    if info["format"] in ("ell", "dia", "css") or (info["format"] == "csr" and info["csr_lanes"] == 1):
         assert np.array_equal(y, yref), f"{info['format']} is sequential: must be bit-exact"
 
 
@@ -146,13 +146,40 @@ def test_dia_banded_bit_exact_and_refusal():
         sp.Plan.from_csr(5000, 5000, rp2, col2, val2, "dia")
 
 
+@pytest.mark.parametrize("shift,lag", [(17, 0), (8, 0), (10, 3), (12, -1), (20, 1)])
+def test_css_slabs_and_pacing(shift, lag):
+    """Column-slab sweep: any slab width / pacing slack gives the sequential
+    opt_crs sum bit for bit (rows sorted by column)."""
+    m = 70001
+    spec = sp.gen_spec("powerlaw", m, max_len=3000, seed=47)
+    rp, col, val = sp.generate_csr(spec)
+    x = sp.generate_vector(m, seed=53)
+    plan = sp.Plan.from_csr(m, m, rp, col, val, "css", css_slab_shift=shift, css_lag=lag)
+    info = plan.info()
+    assert info["css_slabs"] == (m + (1 << shift) - 1) >> shift
+    y = run_plan(plan, x, m)
+    assert np.array_equal(y, oracle_y(rp, col, val, x))
+
+
+def test_css_multi_pass():
+    """More rows than #CU x 19968 -> several row passes through LDS."""
+    m = 6_000_000
+    spec = sp.gen_spec("uniform", m, per_row=2, seed=59)
+    rp, col, val = sp.generate_csr(spec)
+    x = sp.generate_vector(m, seed=61)
+    plan = sp.Plan.from_csr(m, m, rp, col, val, "css")
+    assert plan.info()["css_passes"] >= 2
+    y = run_plan(plan, x, m)
+    assert np.array_equal(y, oracle_y(rp, col, val, x))
+
+
 def test_integer_exact_all_formats():
     m = 40000
     spec = sp.gen_spec("powerlaw", m, max_len=2000, integer_values=True, seed=41)
     rp, col, val = sp.generate_csr(spec)
     x = sp.generate_vector(m, seed=43, integer_values=True)
     yo = oracle_y(rp, col, val, x)
-    for fmt in ["csr", "ell", "ss", "hyb"]:
+    for fmt in ["csr", "ell", "ss", "hyb", "css"]:
         y = run_plan(sp.Plan.from_csr(m, m, rp, col, val, fmt), x, m)
         assert np.array_equal(y, yo), fmt
 
@@ -166,7 +193,7 @@ def test_rectangular_and_empty():
         val = rng.random(rp[-1])
         x = rng.random(n)
         yo = oracle_y(rp, col, val, x) if m else np.zeros(0)
-        for fmt in ["csr", "ell", "ss", "hyb"]:
+        for fmt in ["csr", "ell", "ss", "hyb", "css"]:
             plan = sp.Plan.from_csr(m, n, rp, col, val, fmt)
             y = np.full(m, 7.0)
             plan.execute(x, y)
@@ -184,7 +211,7 @@ def test_device_pointers_and_streams():
     rp, col, val = sp.generate_csr(sp.gen_spec("uniform", m, per_row=16, seed=2))
     x = sp.generate_vector(m, seed=3)
     yo = oracle_y(rp, col, val, x)
-    for fmt in ["csr", "ell", "ss"]:
+    for fmt in ["csr", "ell", "ss", "css"]:
         plan = sp.Plan.from_csr(m, m, rp, col, val, fmt)
         xd = torch.from_numpy(x).cuda()
         yd = torch.full((m,), float("nan"), dtype=torch.float64, device="cuda")
