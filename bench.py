@@ -72,11 +72,21 @@ def main():
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE",
               file=sys.stderr)
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    # BENCH_DIST_BACKEND=gloo lets several ranks share one GPU (development
+    # rehearsal of the multi-GPU flow); the driver's runs use nccl = RCCL.
+    backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    local_dev = local % ndev if backend == "gloo" else local
+    torch.cuda.set_device(local_dev)
+    dev = torch.device("cuda", local_dev)
+    local = local_dev
     distributed = world > 1
     if distributed:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
+    sdist.set_cpu_collectives(backend == "gloo")
 
     gen_kw, desc, rows_default = CONFIGS[args.config]
     rows = args.rows or rows_default
@@ -135,10 +145,7 @@ def main():
         if distributed:
             dist.barrier()
         wall = time.perf_counter() - tw
-        tmax = torch.tensor([wall, ev_ms], dtype=torch.float64, device=dev)
-        if distributed:
-            dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        wall_max, ev_max = float(tmax[0]), float(tmax[1])
+        wall_max, ev_max = sdist.max_over_ranks([wall, ev_ms], dev)
         launch_s = ev_ms / 1e3 / args.steps
         flops_total = 2.0 * nnz_local * world * args.steps
         r = {

@@ -42,12 +42,43 @@ def shard_csr(row_ptr, col, val, rank: int, world: int):
     return (r0, r1), (row_ptr[r0:r1 + 1] - b).astype(np.int64), col[b:e], val[b:e]
 
 
+_CPU_COLLECTIVES = False
+
+
+def set_cpu_collectives(flag: bool) -> None:
+    """Route collectives through host copies (gloo rehearsal with several
+    ranks on one GPU); RCCL runs keep device tensors."""
+    global _CPU_COLLECTIVES
+    _CPU_COLLECTIVES = bool(flag)
+
+
+def _dist_on():
+    import torch.distributed as dist
+    return dist.is_initialized() and dist.get_world_size() > 1
+
+
 def replicate_x(x, src: int = 0):
     """Broadcast x from `src` to every rank (RCCL/gloo broadcast), in place."""
     import torch.distributed as dist
-    if dist.is_initialized() and dist.get_world_size() > 1:
-        dist.broadcast(x, src=src)
+    if _dist_on():
+        if _CPU_COLLECTIVES and x.is_cuda:
+            h = x.cpu()
+            dist.broadcast(h, src=src)
+            x.copy_(h)
+        else:
+            dist.broadcast(x, src=src)
     return x
+
+
+def max_over_ranks(values, device):
+    """Element-wise max of a short list of floats over all ranks."""
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor(values, dtype=torch.float64,
+                     device="cpu" if _CPU_COLLECTIVES else device)
+    if _dist_on():
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return [float(v) for v in t.tolist()]
 
 
 def gather_y(y_local, rows_per_rank: int):
@@ -61,6 +92,10 @@ def gather_y(y_local, rows_per_rank: int):
     if y_local.numel() < rows_per_rank:
         pad = torch.zeros(rows_per_rank - y_local.numel(), dtype=y_local.dtype, device=y_local.device)
         y_local = torch.cat([y_local, pad])
+    if _CPU_COLLECTIVES and y_local.is_cuda:
+        parts = [torch.empty(rows_per_rank, dtype=y_local.dtype) for _ in range(world)]
+        dist.all_gather(parts, y_local.cpu())
+        return torch.cat(parts).to(y_local.device)
     out = torch.empty(world * rows_per_rank, dtype=y_local.dtype, device=y_local.device)
     dist.all_gather_into_tensor(out, y_local.contiguous())
     return out
