@@ -158,9 +158,10 @@ def main():
             "device_bytes": info["device_bytes"], "plan_build_s": round(t_plan, 3),
             "n_kernels": info["n_kernels"],
         }
-        for k in ("csr_lanes", "ss_sigma", "ell_width", "n_diags"):
-            if info[k]:
-                r[k] = info[k]
+        relevant = {"csr": ("csr_lanes",), "ss": ("ss_sigma",), "ell": ("ell_width",),
+                    "hyb": ("ell_width",), "dia": ("n_diags",), "css": ("css_passes", "css_slabs")}
+        for k in relevant.get(info["format"], ()):
+            r[k] = info[k]
         results[fmt] = r
         if fi == 0:
             headline = (plan, info, r)

@@ -145,6 +145,7 @@ typedef struct spmv_plan_info {
     int32_t n_kernels;       /* launches per execute                           */
     int64_t overflow_nnz;    /* HYB: entries outside the ELL part              */
     int64_t empty_rows;
+    int64_t css_split_rows;  /* CSS: rows split into pieces (long rows)       */
     char kernel[64];         /* name of the dominant kernel                    */
 } spmv_plan_info_t;
 

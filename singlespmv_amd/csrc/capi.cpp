@@ -277,6 +277,7 @@ int spmv_plan_info(spmv_plan_t p, spmv_plan_info_t *info) {
     info->n_kernels = p->n_kernels;
     info->overflow_nnz = p->hyb.nnz;
     info->empty_rows = p->empty_rows;
+    info->css_split_rows = p->css.split_rows;
     std::strncpy(info->kernel, p->kernel_name.c_str(), sizeof(info->kernel) - 1);
     return SPMV_SUCCESS;
 }

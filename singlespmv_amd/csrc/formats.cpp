@@ -326,13 +326,14 @@ int build_dia(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
     const int64_t N = A.m + A.n - 1;
     std::vector<int32_t> idx((size_t)std::max<int64_t>(N, 1), -1);
     for (int i = 0; i < d.n_diags; ++i) idx[(size_t)(offs[i] + A.m - 1)] = i;
-    const int64_t slots = (int64_t)d.n_diags * A.m;
+    d.mp = round_up(A.m, 2);
+    const int64_t slots = (int64_t)d.n_diags * d.mp;
     std::vector<double> val((size_t)std::max<int64_t>(slots, 1), 0.0);
 #pragma omp parallel for schedule(static)
     for (int64_t r = 0; r < A.m; ++r)
         for (int64_t j = A.row_ptr[r]; j < A.row_ptr[r + 1]; ++j) {
             const int di = idx[(size_t)(A.col[j] - r + A.m - 1)];
-            val[(size_t)(di * A.m + r)] += A.val[j];  // duplicates are summed
+            val[(size_t)(di * d.mp + r)] += A.val[j];  // duplicates are summed
         }
     SPMV_RETURN_IF(upload(p, &d.off, offs.data(), d.n_diags));
     SPMV_RETURN_IF(upload(p, &d.val, val.data(), slots));
@@ -344,18 +345,24 @@ int build_dia(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
 }
 
 // ---------------------------------------------------------------- CSS
-// Column-slab sweep (k_css.hip).  Rows are cut into passes x workgroups x
-// waves; every wave's entries are sorted by column and packed into 64-entry
-// chunks with distinct rows (a row whose entry would repeat inside a chunk is
-// deferred, together with its later entries, so per-row column order holds).
 namespace {
 struct CssEntry {
     int32_t col;
-    uint16_t row;
+    uint16_t slot;
     double val;
+};
+struct CssPiece {
+    int64_t begin, end;  // CSR entry range
+    int slot;            // LDS slot (row l -> slot l; extra pieces after the rows)
 };
 }  // namespace
 
+// Column-slab sweep (k_css.hip).  Rows are cut into nnz-balanced blocks, one
+// per (pass, workgroup), each using <= kCssMaxRows LDS slots; a row longer
+// than half a worker wave's share is split into pieces with their own slots
+// (merged in piece order at pass end), pieces go to the 15 worker waves
+// longest-first onto the least loaded wave (LPT), and each wave's entries are
+// sorted by column.
 int build_css(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
     CssDev &c = p->css;
     int ncu = 0;
@@ -363,8 +370,35 @@ int build_css(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
     c.nwg = ncu > 0 ? ncu : 256;
     constexpr int W = kCssWorkers;
     const int64_t per_pass = (int64_t)c.nwg * kCssMaxRows;
-    c.P = (int)std::max<int64_t>(1, (A.m + per_pass - 1) / per_pass);
-    c.R = (int)std::max<int64_t>(1, (A.m + (int64_t)c.P * c.nwg - 1) / ((int64_t)c.P * c.nwg));
+    const int P_min = (int)std::max<int64_t>(1, (A.m + per_pass - 1) / per_pass);
+    auto row_len = [&](int64_t r) { return A.row_ptr[r + 1] - A.row_ptr[r]; };
+    std::vector<int64_t> bstart;
+    int64_t piece_cap = 0;
+    for (c.P = P_min;; ++c.P) {
+        const int64_t nb = (int64_t)c.P * c.nwg;
+        piece_cap = std::max<int64_t>(64, A.nnz / (nb * W) / 2);
+        auto slots_of = [&](int64_t r) { return std::max<int64_t>(1, (row_len(r) + piece_cap - 1) / piece_cap); };
+        bstart.assign((size_t)nb + 1, 0);
+        bool ok = true;
+        int64_t r = 0;
+        for (int64_t b = 0; b < nb; ++b) {
+            const int64_t target = b == nb - 1 ? A.nnz : (int64_t)((__int128)A.nnz * (b + 1) / nb);
+            int64_t used = 0;
+            while (r < A.m && (b == nb - 1 || A.row_ptr[r] < target || (A.nnz == 0 && r < (b + 1) * ((A.m + nb - 1) / nb)))) {
+                const int64_t k = slots_of(r);
+                if (used + k > kCssMaxRows) break;
+                used += k;
+                ++r;
+            }
+            bstart[(size_t)b + 1] = r;
+        }
+        if (r < A.m) ok = false;  // rows left over: more passes
+        if (ok || c.P > P_min + 1024) break;
+    }
+    if (bstart.back() != A.m) {
+        set_error("CSS: could not fit the rows into LDS row blocks");
+        return SPMV_ERROR_NOT_SUPPORTED;
+    }
     if (o.css_slab_shift > 0) {
         c.slab_shift = o.css_slab_shift;
     } else {
@@ -382,95 +416,87 @@ int build_css(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
     }
     c.S = (int)std::max<int64_t>(1, (A.n + ((int64_t)1 << c.slab_shift) - 1) >> c.slab_shift);
     c.lag = o.css_lag == 0 ? 4 : (o.css_lag < 0 ? 0 : o.css_lag);
-    // pace against every XCD when x outgrows half the 256 MiB Infinity Cache:
-    // then the 8 XCDs must sweep the same slab for the MALL to serve 7 of 8
     c.pace_all = o.css_pace == 2 ? 0 : 1;
     const int64_t nblocks = (int64_t)c.P * c.nwg;
     const int64_t nlists = nblocks * W;
     std::vector<int64_t> woff((size_t)nlists + 1, 0);
-    auto block_rows = [&](int64_t pb, int64_t &r0, int &rows) {
-        r0 = pb * c.R;
-        const int64_t rem = A.m - r0;
-        rows = rem <= 0 ? 0 : (int)std::min<int64_t>(rem, c.R);
-    };
-    // rows of a block go to the worker waves longest-first onto the least
-    // loaded wave (LPT), so one long row does not leave 14 waves idle
-    std::vector<uint8_t> owner((size_t)std::max<int64_t>(A.m, 1), 0);
+    std::vector<int64_t> moff((size_t)nblocks + 1, 0);
+    std::vector<std::vector<int32_t>> merges((size_t)nblocks);
+    std::vector<std::vector<CssPiece>> wave_pieces((size_t)nlists);
 #pragma omp parallel
     {
-        std::vector<std::pair<int64_t, int>> order;
+        std::vector<CssPiece> pieces;
+        std::vector<int> order;
 #pragma omp for schedule(dynamic, 4)
         for (int64_t pb = 0; pb < nblocks; ++pb) {
-            int64_t r0;
-            int rows;
-            block_rows(pb, r0, rows);
-            order.clear();
-            for (int l = 0; l < rows; ++l) order.push_back({A.row_ptr[r0 + l + 1] - A.row_ptr[r0 + l], l});
-            std::stable_sort(order.begin(), order.end(),
-                             [](const std::pair<int64_t, int> &a, const std::pair<int64_t, int> &b) { return a.first > b.first; });
+            const int64_t r0 = bstart[(size_t)pb];
+            const int rows = (int)(bstart[(size_t)pb + 1] - r0);
+            pieces.clear();
+            int extra = rows;
+            for (int l = 0; l < rows; ++l) {
+                const int64_t b0 = A.row_ptr[r0 + l], len = row_len(r0 + l);
+                const int64_t k = std::max<int64_t>(1, (len + piece_cap - 1) / piece_cap);
+                if (k > 1) {
+                    merges[(size_t)pb].insert(merges[(size_t)pb].end(), {l, extra, (int32_t)(k - 1)});
+                }
+                for (int64_t i = 0; i < k; ++i)
+                    pieces.push_back(CssPiece{b0 + len * i / k, b0 + len * (i + 1) / k, i == 0 ? l : extra + (int)i - 1});
+                extra += (int)(k - 1);
+            }
+            order.resize(pieces.size());
+            std::iota(order.begin(), order.end(), 0);
+            std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
+                return pieces[a].end - pieces[a].begin > pieces[b].end - pieces[b].begin;
+            });
             int64_t load[W] = {0};
-            for (const auto &e : order) {
+            for (int i : order) {
                 int best = 0;
                 for (int w = 1; w < W; ++w)
                     if (load[w] < load[best]) best = w;
-                load[best] += e.first;
-                owner[(size_t)(r0 + e.second)] = (uint8_t)best;
+                load[best] += pieces[i].end - pieces[i].begin;
+                wave_pieces[(size_t)(pb * W + best)].push_back(pieces[i]);
             }
             for (int w = 0; w < W; ++w) woff[(size_t)(pb * W + w + 1)] = load[w];
+            moff[(size_t)pb + 1] = (int64_t)merges[(size_t)pb].size() / 3;
         }
     }
     for (int64_t L = 0; L < nlists; ++L) woff[L + 1] += woff[L];
+    for (int64_t b = 0; b < nblocks; ++b) moff[b + 1] += moff[b];
     const int64_t total = woff[nlists];
     std::vector<int32_t> col((size_t)std::max<int64_t>(total, 1));
-    std::vector<uint16_t> row((size_t)std::max<int64_t>(total, 1));
+    std::vector<uint16_t> slot((size_t)std::max<int64_t>(total, 1));
     std::vector<double> val((size_t)std::max<int64_t>(total, 1));
+    std::vector<int32_t> merge((size_t)std::max<int64_t>(3 * moff[nblocks], 1));
 #pragma omp parallel
     {
-        std::vector<CssEntry> in, defer, next;
-        std::vector<uint32_t> stamp(kCssMaxRows, 0), blocked(kCssMaxRows, 0);
-        uint32_t epoch = 0;
+        std::vector<CssEntry> in;
 #pragma omp for schedule(dynamic, 4)
         for (int64_t L = 0; L < nlists; ++L) {
-            int64_t r0;
-            int rows;
-            block_rows(L / W, r0, rows);
-            const int w = (int)(L % W);
             in.clear();
-            for (int l = 0; l < rows; ++l) {
-                if (owner[(size_t)(r0 + l)] != w) continue;
-                for (int64_t j = A.row_ptr[r0 + l]; j < A.row_ptr[r0 + l + 1]; ++j)
-                    in.push_back(CssEntry{A.col[j], (uint16_t)l, A.val[j]});
-            }
+            for (const CssPiece &pc : wave_pieces[(size_t)L])
+                for (int64_t j = pc.begin; j < pc.end; ++j) in.push_back(CssEntry{A.col[j], (uint16_t)pc.slot, A.val[j]});
+            // column order = slab order; stable keeps a row's CSR order
             std::stable_sort(in.begin(), in.end(), [](const CssEntry &a, const CssEntry &b) { return a.col < b.col; });
             int64_t out = woff[L];
-            size_t idx = 0;
-            defer.clear();
-            while (idx < in.size() || !defer.empty()) {
-                ++epoch;
-                int count = 0;
-                next.clear();
-                auto offer = [&](const CssEntry &e) {
-                    if (count < 64 && stamp[e.row] != epoch && blocked[e.row] != epoch) {
-                        stamp[e.row] = epoch;
-                        col[out] = e.col;
-                        row[out] = e.row;
-                        val[out] = e.val;
-                        ++out;
-                        ++count;
-                    } else {
-                        blocked[e.row] = epoch;
-                        next.push_back(e);
-                    }
-                };
-                for (const CssEntry &e : defer) offer(e);
-                while (count < 64 && idx < in.size()) offer(in[idx++]);
-                defer.swap(next);
+            for (const CssEntry &e : in) {
+                col[out] = e.col;
+                slot[out] = e.slot;
+                val[out] = e.val;
+                ++out;
             }
+            std::vector<CssPiece>().swap(wave_pieces[(size_t)L]);
         }
+#pragma omp for schedule(static)
+        for (int64_t b = 0; b < nblocks; ++b)
+            std::copy(merges[(size_t)b].begin(), merges[(size_t)b].end(), merge.begin() + 3 * moff[b]);
     }
+    c.split_rows = moff[nblocks];
     SPMV_RETURN_IF(upload(p, &c.woff, woff.data(), nlists + 1));
+    SPMV_RETURN_IF(upload(p, &c.bstart, bstart.data(), nblocks + 1));
+    SPMV_RETURN_IF(upload(p, &c.moff, moff.data(), nblocks + 1));
+    SPMV_RETURN_IF(upload(p, &c.merge, merge.data(), 3 * moff[nblocks]));
     SPMV_RETURN_IF(upload(p, &c.col, col.data(), total));
-    SPMV_RETURN_IF(upload(p, &c.row, row.data(), total));
+    SPMV_RETURN_IF(upload(p, &c.row, slot.data(), total));
     SPMV_RETURN_IF(upload(p, &c.val, val.data(), total));
     std::vector<uint64_t> zeros(8 * 16, 0);
     SPMV_RETURN_IF(upload(p, &c.prog, zeros.data(), (int64_t)zeros.size()));

@@ -114,24 +114,31 @@ struct SsDev {
     int64_t n_empty = 0;
 };
 
-// DIA (opt_dia, src/opt_dia.cpp), row-indexed: val[d*m + r] = A[r, r+off[d]]
+// DIA (opt_dia, src/opt_dia.cpp), row-indexed: val[d*mp + r] = A[r, r+off[d]]
 // (0 where absent / outside), offsets ascending.
 struct DiaDev {
     int n_diags = 0;
     int32_t *off = nullptr;  // device copy of offsets
     std::vector<int32_t> off_host;
-    double *val = nullptr;   // [n_diags * m]
+    double *val = nullptr;   // [n_diags * mp]
+    int64_t mp = 0;          // diagonal stride: m rounded up to even
 };
 
-// Column-slab sweep (CSS, k_css.hip).  Per (pass p, workgroup b, wave w) a
-// list of entries (global col int32, local row uint16, val f64) sorted by
-// column, every aligned 64-entry chunk row-distinct; woff[(p*nwg+b)*16+w] is
-// the list start (woff index uses kCssWorkers lists per workgroup).  prog: per-XCD-label pacing counters (uint64, 128 B apart).
+// Column-slab sweep (CSS, k_css.hip).  Per (pass p, workgroup b, worker wave
+// w) a list of entries (global col int32, LDS slot uint16, val f64) sorted by
+// column; woff[(p*nwg+b)*kCssWorkers+w] is the list start.  Slots 0..rows-1
+// are the block's rows; rows split into pieces use extra slots, merged at
+// pass end from merge[] triples (slot, first extra slot, count), moff[] per
+// block.  prog: per-XCD-label pacing counters (uint64, 128 B apart).
 constexpr int kCssMaxRows = 19968;
 constexpr int kCssWorkers = 15;  // worker waves per workgroup (+1 pacer wave)
 struct CssDev {
     int nwg = 0, R = 0, P = 0, S = 0, slab_shift = 17, lag = 2, pace_all = 0;
     int64_t *woff = nullptr;
+    int64_t *bstart = nullptr;  // [P*nwg + 1] first row of each (pass, workgroup) block
+    int64_t *moff = nullptr;    // [P*nwg + 1] merge-triple offsets per block
+    int32_t *merge = nullptr;   // (slot, first extra slot, n extra) triples
+    int64_t split_rows = 0;
     int32_t *col = nullptr;
     uint16_t *row = nullptr;
     double *val = nullptr;

@@ -9,11 +9,12 @@
 //
 // Geometry (see CssDev):
 //  * one 1024-thread workgroup per CU: 15 WORKER waves + 1 PACER wave.  The
-//    workgroup owns a block of R <= 19968 rows per pass and accumulates their
+//    workgroup owns an nnz-balanced block of <= 19968 rows per pass and keeps their
 //    y in LDS (160 KB), so y never round-trips through HBM between slabs;
-//  * columns are cut into slabs of 2^slab_shift columns.  Worker wave w owns
-//    the rows l with l % 15 == w and streams its own entry list, sorted by
-//    column, i.e. slab by slab, software-pipelined one 256-entry chunk ahead;
+//  * columns are cut into slabs of 2^slab_shift columns.  Each worker wave
+//    owns a set of rows / row pieces (LPT-balanced by nnz) and streams its own
+//    entry list, sorted by column, i.e. slab by slab, software-pipelined one
+//    256-entry chunk ahead;
 //  * pacing (speed only, never results): workers report finished slabs with
 //    LDS atomics and wait, in LDS, for the slab to be allowed.  The pacer
 //    wave alone talks to global memory: it publishes the workgroup's finished
@@ -23,10 +24,14 @@
 //    the workgroups of an XCD sweep within `lag` slabs of each other and the
 //    XCD's L2 serves the x gathers.  Every wait is bounded.
 //
-// Determinism / exactness: every 64-entry chunk of a wave's list has distinct
-// rows (host builder), a row's entries are added in ascending column order by
-// one wave in program order (ds_add_f64), and the LDS row starts at +0.0 -- so
-// each y[r] is the sequential opt_crs sum (src/opt_crs.cpp:61-66) bit for bit.
+// Determinism / exactness: a row (or row piece) is owned by one wave, which
+// adds its entries in ascending column order (ds_add_f64 in program order;
+// lanes of one instruction that hit the same slot are applied in lane = list
+// order by the LDS unit -- observed, and checked bit for bit by the tests);
+// the slot starts at +0.0.  An unsplit row is therefore the sequential
+// opt_crs sum (src/opt_crs.cpp:61-66) bit for bit; a row longer than half a
+// wave's share is split into pieces whose sums are added in piece order at
+// the end of the pass (deterministic, different rounding order).
 #include "device.hpp"
 #include "internal.hpp"
 
@@ -41,6 +46,7 @@ struct CssChunk {
     double v[4];
 };
 
+template <bool NT>
 __device__ __forceinline__ void css_load(CssChunk &k, int64_t j0, int64_t e1, int lane,
                                          const int32_t *__restrict__ col,
                                          const uint16_t *__restrict__ row,
@@ -49,14 +55,22 @@ __device__ __forceinline__ void css_load(CssChunk &k, int64_t j0, int64_t e1, in
     for (int u = 0; u < 4; ++u) {
         const int64_t j = j0 + u * 64 + lane;
         const bool ok = j < e1;
-        k.c[u] = ok ? ld_stream(col + j) : 0;
-        k.r[u] = ok ? (int32_t)__builtin_nontemporal_load(row + j) : -1;
-        k.v[u] = ok ? ld_stream(val + j) : 0.0;
+        if (NT) {
+            k.c[u] = ok ? ld_stream(col + j) : 0;
+            k.r[u] = ok ? (int32_t)__builtin_nontemporal_load(row + j) : -1;
+            k.v[u] = ok ? ld_stream(val + j) : 0.0;
+        } else {
+            k.c[u] = ok ? col[j] : 0;
+            k.r[u] = ok ? (int32_t)row[j] : -1;
+            k.v[u] = ok ? val[j] : 0.0;
+        }
     }
 }
 
+template <bool NT>
 __global__ __launch_bounds__(kCssThreads) void css_sweep_kernel(
-    int64_t m, int32_t R, int32_t P, int32_t nwg, int32_t S, int32_t slab_shift, int32_t lag,
+    const int64_t *__restrict__ bstart, const int64_t *__restrict__ moff,
+    const int32_t *__restrict__ merge, int32_t P, int32_t nwg, int32_t S, int32_t slab_shift, int32_t lag,
     const int64_t *__restrict__ woff, const int32_t *__restrict__ col,
     const uint16_t *__restrict__ row, const double *__restrict__ val,
     const double *__restrict__ x, double *__restrict__ y, uint64_t *__restrict__ prog,
@@ -72,10 +86,10 @@ __global__ __launch_bounds__(kCssThreads) void css_sweep_kernel(
     const bool pacer = w == kCssWorkers;
 
     for (int p = 0; p < P; ++p) {
-        const int64_t row0 = ((int64_t)p * nwg + b) * R;
-        const int64_t rem = m - row0;
-        const int rows = rem <= 0 ? 0 : (rem < R ? (int)rem : R);
-        for (int i = threadIdx.x; i < rows; i += kCssThreads) ylds[i] = 0.0;
+        // this workgroup's nnz-balanced row block of pass p (<= kCssMaxRows rows)
+        const int64_t row0 = bstart[(int64_t)p * nwg + b];
+        const int rows = (int)(bstart[(int64_t)p * nwg + b + 1] - row0);
+        for (int i = threadIdx.x; i < kCssMaxRows; i += kCssThreads) ylds[i] = 0.0;  // rows + piece slots
         for (int i = threadIdx.x; i < kCssRing; i += kCssThreads) arrive[i] = 0;
         if (threadIdx.x == 0) allowed = pacing ? lag - 1 : S;
         __syncthreads();
@@ -149,7 +163,7 @@ __global__ __launch_bounds__(kCssThreads) void css_sweep_kernel(
                 }
             };
             CssChunk A, B;
-            if (e0 < e1) css_load(A, e0, e1, lane, col, row, val);
+            if (e0 < e1) css_load<NT>(A, e0, e1, lane, col, row, val);
             for (int64_t j0 = e0; j0 < e1; j0 += 256) {
                 // slab of the chunk's first entry (wave-uniform: lane 0, u = 0)
                 const int s0 = __builtin_amdgcn_readfirstlane(A.c[0]) >> slab_shift;
@@ -166,7 +180,7 @@ __global__ __launch_bounds__(kCssThreads) void css_sweep_kernel(
                 // prefetch the next chunk behind the gathers (in-order vmcnt:
                 // waiting for the gathers leaves these 12 loads in flight)
                 const int64_t j1 = j0 + 256;
-                if (j1 < e1) css_load(B, j1, e1, lane, col, row, val);
+                if (j1 < e1) css_load<NT>(B, j1, e1, lane, col, row, val);
                 __builtin_amdgcn_sched_barrier(0);
                 if (dbg & 2) {
 #pragma unroll
@@ -182,6 +196,17 @@ __global__ __launch_bounds__(kCssThreads) void css_sweep_kernel(
             if ((dbg & 2) && dsink == 1.2345) y[0] = dsink;  // keep ablated work alive
         }
         __syncthreads();
+        // rows split into pieces: add the extra pieces in piece order
+        {
+            const int64_t pb = (int64_t)p * nwg + b;
+            for (int64_t i = moff[pb] + threadIdx.x; i < moff[pb + 1]; i += kCssThreads) {
+                const int slot = merge[3 * i], first = merge[3 * i + 1], cnt = merge[3 * i + 2];
+                double acc = ylds[slot];
+                for (int t = 0; t < cnt; ++t) acc = __dadd_rn(acc, ylds[first + t]);
+                ylds[slot] = acc;
+            }
+        }
+        __syncthreads();
         for (int i = threadIdx.x; i < rows; i += kCssThreads) y[row0 + i] = ylds[i];
         __syncthreads();
     }
@@ -192,9 +217,14 @@ int launch_css(const spmv_plan_s *p, const double *x, double *y) {
     if (p->m == 0) return SPMV_SUCCESS;
     spmv_plan_s *mp = const_cast<spmv_plan_s *>(p);
     const uint64_t seq = mp->css.launches++;
-    hipLaunchKernelGGL(css_sweep_kernel, dim3((unsigned)c.nwg), dim3(kCssThreads), 0, p->stream, p->m,
-                       c.R, c.P, c.nwg, c.S, c.slab_shift, c.lag, c.woff, c.col, c.row, c.val, x, y,
-                       c.prog, seq, c.pace_all, c.dbg);
+    if (c.dbg & 8)  // ablation: default cache policy on the matrix stream
+        hipLaunchKernelGGL(css_sweep_kernel<false>, dim3((unsigned)c.nwg), dim3(kCssThreads), 0, p->stream,
+                           c.bstart, c.moff, c.merge, c.P, c.nwg, c.S, c.slab_shift, c.lag, c.woff, c.col, c.row, c.val, x, y,
+                           c.prog, seq, c.pace_all, c.dbg);
+    else
+        hipLaunchKernelGGL(css_sweep_kernel<true>, dim3((unsigned)c.nwg), dim3(kCssThreads), 0, p->stream,
+                           c.bstart, c.moff, c.merge, c.P, c.nwg, c.S, c.slab_shift, c.lag, c.woff, c.col, c.row, c.val, x, y,
+                           c.prog, seq, c.pace_all, c.dbg);
     SPMV_HIP_TRY(hipGetLastError());
     return SPMV_SUCCESS;
 }

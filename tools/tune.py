@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--rows", type=int, default=10_000_000)
     ap.add_argument("--per-row", type=int, default=16)
     ap.add_argument("--ncols", type=int, default=0, help="columns (default: rows)")
+    ap.add_argument("--max-len", type=int, default=10000)
     ap.add_argument("--grid", default="")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
@@ -29,7 +30,7 @@ def main():
     import singlespmv_amd as sp
     m = a.rows
     n = a.ncols or m
-    spec = sp.gen_spec(a.kind, n, n, per_row=a.per_row, seed=42)
+    spec = sp.gen_spec(a.kind, n, n, per_row=a.per_row, max_len=a.max_len, seed=42)
     rp, col, val = sp.generate_csr(spec, 0, m)
     x = torch.from_numpy(sp.generate_vector(n, seed=43)).cuda()
     y = torch.empty(m, dtype=torch.float64, device="cuda")
