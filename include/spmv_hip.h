@@ -19,7 +19,8 @@
  *                          y it reproduces src/opt_cusparse.cpp:72-82 (H2D x,
  *                          y = 1*A*x + 0*y, D2H y).
  *   spmv_plan_destroy      (the reference never frees; no counterpart)
- *   spmv_load_mtx          LoadSparseMatrix (src/util.cpp:30-66)
+ *   spmv_load_mtx          LoadSparseMatrix (src/util.cpp:30-66), parallel
+ *   spmv_{save,load}_csr_bin (new) binary CSR cache
  *   spmv_rand_vector       srand + CreateRandomVector (src/main.cpp:18,
  *                          src/util.cpp:92-102)
  *   spmv_verify_coo        VerifyResult (src/util.cpp:67-83)
@@ -163,6 +164,14 @@ const char *spmv_last_error(void);
 int spmv_load_mtx(const char *path, int32_t *m, int32_t *n, int32_t *nnz,
                   int32_t **row_idx, int32_t **col_idx, double **val);
 void spmv_free_host(void *p);
+
+/* Binary CSR cache ("SPMVCSR1": header, int64 row_ptr, int32 col, f64 val) so
+ * a large Matrix Market file is parsed once.  Arrays from the loader are
+ * malloc'd; release with spmv_free_host. */
+int spmv_save_csr_bin(const char *path, int64_t m, int64_t n, int64_t nnz, const int64_t *row_ptr,
+                      const int32_t *col_idx, const double *val);
+int spmv_load_csr_bin(const char *path, int64_t *m, int64_t *n, int64_t *nnz, int64_t **row_ptr,
+                      int32_t **col_idx, double **val);
 
 /* glibc srand(seed) then out[i] = rand()/RAND_MAX -- CreateRandomVector
  * (src/util.cpp:92-102).  Consecutive calls continue the rand() stream. */

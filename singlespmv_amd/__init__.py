@@ -84,7 +84,7 @@ EXPORTS = [
     "spmv_time", "spmv_plan_info", "spmv_status_string", "spmv_last_error",
     "spmv_load_mtx", "spmv_free_host", "spmv_srand", "spmv_rand_vector", "spmv_verify_coo",
     "spmv_coo_to_csr", "spmv_gen_count", "spmv_gen_fill", "spmv_gen_vector",
-    "spmv_partition_rows",
+    "spmv_partition_rows", "spmv_save_csr_bin", "spmv_load_csr_bin",
 ]
 
 _lib = None
@@ -125,6 +125,10 @@ def lib():
     L.spmv_gen_fill.argtypes = [C.POINTER(GenSpec), i64, i64, _I64P, vp, vp]
     L.spmv_gen_vector.argtypes = [C.c_uint64, i32, i64, i64, _F64P]
     L.spmv_partition_rows.argtypes = [_I64P, i64, i32, _I64P]
+    L.spmv_save_csr_bin.argtypes = [C.c_char_p, i64, i64, i64, _I64P, vp, vp]
+    L.spmv_load_csr_bin.argtypes = [C.c_char_p, C.POINTER(i64), C.POINTER(i64), C.POINTER(i64),
+                                    C.POINTER(C.POINTER(i64)), C.POINTER(C.POINTER(i32)),
+                                    C.POINTER(C.POINTER(f64))]
     _lib = L
     return L
 
@@ -184,6 +188,31 @@ def load_sparse_matrix(path: str) -> SpMat:
                 np.ctypeslib.as_array(v, shape=(max(k, 1),))[:k].copy())
     for p in (r, c, v):
         L.spmv_free_host(C.cast(p, C.c_void_p))
+    return out
+
+
+def save_csr_bin(path: str, m: int, n: int, row_ptr, col, val) -> None:
+    """Write the SPMVCSR1 binary cache (parse a .mtx once, mmap-load later)."""
+    rp = np.ascontiguousarray(row_ptr, np.int64)
+    col = np.ascontiguousarray(col, np.int32)
+    val = np.ascontiguousarray(val, np.float64)
+    _check(lib().spmv_save_csr_bin(path.encode(), m, n, len(val), rp, col.ctypes.data, val.ctypes.data),
+           f"save_csr_bin({path})")
+
+
+def load_csr_bin(path: str):
+    """(m, n, row_ptr, col, val) from a SPMVCSR1 file."""
+    L = lib()
+    m, n, nnz = C.c_int64(), C.c_int64(), C.c_int64()
+    rp, c, v = C.POINTER(C.c_int64)(), C.POINTER(C.c_int32)(), C.POINTER(C.c_double)()
+    _check(L.spmv_load_csr_bin(path.encode(), C.byref(m), C.byref(n), C.byref(nnz), C.byref(rp),
+                               C.byref(c), C.byref(v)), f"load_csr_bin({path})")
+    k = nnz.value
+    out = (m.value, n.value, np.ctypeslib.as_array(rp, shape=(m.value + 1,)).copy(),
+           np.ctypeslib.as_array(c, shape=(max(k, 1),))[:k].copy(),
+           np.ctypeslib.as_array(v, shape=(max(k, 1),))[:k].copy())
+    for q in (rp, c, v):
+        L.spmv_free_host(C.cast(q, C.c_void_p))
     return out
 
 

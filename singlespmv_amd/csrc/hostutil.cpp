@@ -1,6 +1,6 @@
-// hostutil.cpp -- host side of the path around the kernels: the Matrix Market
-// loader (LoadSparseMatrix semantics, src/util.cpp:30-66), CreateRandomVector
-// (src/util.cpp:92-102), VerifyResult (src/util.cpp:67-83), and the seeded
+// hostutil.cpp -- host side of the path around the kernels (the Matrix Market
+// loader lives in mmio.cpp): CreateRandomVector (src/util.cpp:92-102),
+// VerifyResult (src/util.cpp:67-83), and the seeded
 // synthetic generators for the BASELINE configs (built in memory: a 1.28 G-nnz
 // .mtx would be ~38 GB of text, SURVEY §7 hard part 5).
 #include <fcntl.h>
@@ -22,45 +22,6 @@
 using namespace spmv;
 
 namespace {
-
-// ---- Matrix Market text ---------------------------------------------------
-struct Cursor {
-    const char *p, *end;
-    void skip_ws() {
-        while (p < end && (*p == ' ' || *p == '\t' || *p == '\n' || *p == '\r' || *p == '\f' || *p == '\v')) ++p;
-    }
-    bool read_long(long long &v) {
-        skip_ws();
-        if (p >= end) return false;
-        char *q;
-        char buf[64];
-        size_t n = std::min<size_t>(63, (size_t)(end - p));
-        std::memcpy(buf, p, n);
-        buf[n] = 0;
-        v = std::strtoll(buf, &q, 10);
-        if (q == buf) return false;
-        p += (q - buf);
-        return true;
-    }
-    bool read_double(double &v) {
-        skip_ws();
-        if (p >= end) return false;
-        char *q;
-        char buf[128];
-        size_t n = std::min<size_t>(127, (size_t)(end - p));
-        std::memcpy(buf, p, n);
-        buf[n] = 0;
-        v = std::strtod(buf, &q);
-        if (q == buf) return false;
-        p += (q - buf);
-        return true;
-    }
-};
-
-struct Trip {
-    int32_t r, c;
-    double v;
-};
 
 // ---- counter-based generator ----------------------------------------------
 inline uint64_t splitmix64(uint64_t z) {
@@ -118,93 +79,6 @@ inline int64_t banded_len(const spmv_gen_spec_t *s, int64_t r) {
 }  // namespace
 
 extern "C" {
-
-void spmv_free_host(void *p) { std::free(p); }
-
-int spmv_load_mtx(const char *path, int32_t *m, int32_t *n, int32_t *nnz, int32_t **row_idx,
-                  int32_t **col_idx, double **val) {
-    SPMV_CHECK_ARG(path && m && n && nnz && row_idx && col_idx && val, "NULL argument");
-    const int fd = open(path, O_RDONLY);
-    if (fd < 0) {
-        set_error(std::string("File not Found: ") + path);  // util.cpp:32-35
-        return SPMV_ERROR_IO;
-    }
-    struct stat st;
-    if (fstat(fd, &st) != 0) {
-        close(fd);
-        set_error("fstat failed");
-        return SPMV_ERROR_IO;
-    }
-    const size_t size = (size_t)st.st_size;
-    const char *base = size ? (const char *)mmap(nullptr, size, PROT_READ, MAP_PRIVATE, fd, 0) : "";
-    close(fd);
-    if (base == MAP_FAILED) {
-        set_error("mmap failed");
-        return SPMV_ERROR_IO;
-    }
-    Cursor cur{base, base + size};
-    // util.cpp:37-39: skip lines whose first character is '%'
-    while (cur.p < cur.end && *cur.p == '%') {
-        const char *nl = (const char *)std::memchr(cur.p, '\n', (size_t)(cur.end - cur.p));
-        cur.p = nl ? nl + 1 : cur.end;
-    }
-    long long M, N, L;
-    int status = SPMV_SUCCESS;
-    std::vector<Trip> t;
-    if (!cur.read_long(M) || !cur.read_long(N) || !cur.read_long(L) || M < 0 || N < 0 || L < 0 ||
-        M >= INT32_MAX || N >= INT32_MAX || L >= INT32_MAX) {
-        set_error("bad Matrix Market header");
-        status = SPMV_ERROR_IO;
-    } else {
-        t.resize((size_t)L);
-        // util.cpp:44-50: exactly L triplets, 1 -> 0 based
-        for (long long i = 0; i < L; ++i) {
-            long long r, c;
-            double v;
-            if (!cur.read_long(r) || !cur.read_long(c) || !cur.read_double(v)) {
-                set_error("truncated triplet list (fewer than L entries)");
-                status = SPMV_ERROR_IO;
-                break;
-            }
-            if (r < 1 || r > M || c < 1 || c > N) {
-                set_error("entry outside the declared shape");
-                status = SPMV_ERROR_IO;
-                break;
-            }
-            t[(size_t)i] = Trip{(int32_t)(r - 1), (int32_t)(c - 1), v};
-        }
-    }
-    if (size) munmap((void *)base, size);
-    if (status != SPMV_SUCCESS) return status;
-    // util.cpp:51: sort row-major by (row, col); stable keeps duplicates in
-    // file order (std::sort leaves them unspecified)
-    std::stable_sort(t.begin(), t.end(), [](const Trip &a, const Trip &b) {
-        return a.r != b.r ? a.r < b.r : a.c < b.c;
-    });
-    const size_t k = t.size() ? t.size() : 1;
-    int32_t *ri = (int32_t *)std::malloc(sizeof(int32_t) * k);
-    int32_t *ci = (int32_t *)std::malloc(sizeof(int32_t) * k);
-    double *vv = (double *)std::malloc(sizeof(double) * k);
-    if (!ri || !ci || !vv) {
-        std::free(ri);
-        std::free(ci);
-        std::free(vv);
-        set_error("host allocation failed");
-        return SPMV_ERROR_OUT_OF_MEMORY;
-    }
-    for (size_t i = 0; i < t.size(); ++i) {
-        ri[i] = t[i].r;
-        ci[i] = t[i].c;
-        vv[i] = t[i].v;
-    }
-    *m = (int32_t)M;
-    *n = (int32_t)N;
-    *nnz = (int32_t)L;
-    *row_idx = ri;
-    *col_idx = ci;
-    *val = vv;
-    return SPMV_SUCCESS;
-}
 
 void spmv_srand(uint32_t seed) { srand(seed); }
 void spmv_rand_vector(int32_t n, double *out) {

@@ -172,6 +172,9 @@ __global__ __launch_bounds__(kCssThreads) void css_sweep_kernel(
                 if (dbg & 1) {
 #pragma unroll
                     for (int u = 0; u < 4; ++u) g[u] = (double)A.c[u];
+                } else if (dbg & 16) {  // ablation: every gather inside one 1 MiB window (all L2 hits)
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) g[u] = ld_x(x, A.c[u] & 0x1FFFF);
                 } else {
 #pragma unroll
                     for (int u = 0; u < 4; ++u) g[u] = ld_x(x, A.c[u]);

@@ -117,3 +117,50 @@ def test_partition_rows_balanced():
         for k in range(1, parts):
             assert rp[cuts[k]] >= k * nnz // parts
             assert cuts[k] == 0 or rp[cuts[k] - 1] < k * nnz / parts
+
+
+def _write_mtx(path, m, n, row, col, val, header="%%MatrixMarket matrix coordinate real general\n% c\n",
+               sep="\n"):
+    with open(path, "w") as f:
+        f.write(header)
+        f.write(f"{m} {n} {len(val)}\n")
+        f.write(sep.join(f"{r + 1} {c + 1} {float(v)!r}" for r, c, v in zip(row, col, val)))
+        f.write("\n")
+
+
+@pytest.mark.parametrize("sep", ["\n", "\t\n", "  \n\n", " "])
+def test_parallel_loader_matches_oracle_loader(tmp_path, sep):
+    """Large shuffled file (multi-chunk parallel parse): identical COO to the
+    oracle's restatement of LoadSparseMatrix, whatever the line structure."""
+    rng = np.random.default_rng(1)
+    m, n, k = 40000, 30000, 600000
+    row = rng.integers(0, m, k)
+    col = rng.integers(0, n, k)
+    val = rng.standard_normal(k) * 10.0 ** rng.integers(-5, 5, k)
+    p = str(tmp_path / "big.mtx")
+    _write_mtx(p, m, n, row, col, val, sep=sep)
+    A = sp.load_sparse_matrix(p)
+    mo, no, ro, co, vo = oracle.load_mtx(p)
+    assert (A.nRow, A.nCol) == (mo, no)
+    assert np.array_equal(A.row_idx, ro) and np.array_equal(A.col_idx, co)
+    assert np.array_equal(A.val, vo)
+
+
+def test_loader_ignores_entries_beyond_L(tmp_path):
+    p = tmp_path / "x.mtx"
+    p.write_text("3 3 2\n1 1 1.5\n2 2\n2.5 3 3 9.0\n")  # triplet split over lines; 3rd ignored
+    A = sp.load_sparse_matrix(str(p))
+    assert A.row_idx.tolist() == [0, 1] and A.val.tolist() == [1.5, 2.5]
+
+
+def test_csr_bin_roundtrip(tmp_path):
+    rp, col, val = sp.generate_csr(sp.gen_spec("powerlaw", 7777, max_len=400, seed=3))
+    p = str(tmp_path / "a.csrbin")
+    sp.save_csr_bin(p, 7777, 7777, rp, col, val)
+    m, n, rp2, col2, val2 = sp.load_csr_bin(p)
+    assert (m, n) == (7777, 7777)
+    assert np.array_equal(rp, rp2) and np.array_equal(col, col2) and np.array_equal(val, val2)
+    with open(p, "r+b") as f:
+        f.write(b"NOTMAGIC")
+    with pytest.raises(sp.SpmvError):
+        sp.load_csr_bin(p)
