@@ -69,8 +69,11 @@ typedef enum spmv_format {
     SPMV_FORMAT_SS = 3,   /* opt_ss / CSR5: segmented sum over 64 x sigma tiles */
     SPMV_FORMAT_DIA = 4,  /* opt_dia   (src/opt_dia.cpp), device: row-indexed   */
     SPMV_FORMAT_HYB = 5,  /* ELL(K) + CSR overflow (BASELINE config 3)          */
-    SPMV_FORMAT_CSS = 6   /* opt_css lineage: column-slab sweep, y in LDS, x    */
+    SPMV_FORMAT_CSS = 6,  /* opt_css lineage: column-slab sweep, y in LDS, x    */
                           /* slab L2-resident per XCD (large random matrices)  */
+    SPMV_FORMAT_COO = 7,  /* opt_coo   (src/opt_coo.cpp): f64 atomics per row segment */
+    SPMV_FORMAT_JDS = 8   /* opt_jds   (src/opt_jds.cpp): rows sorted by length,  */
+                          /* jagged 64-row slices, y permuted back             */
 } spmv_format_t;
 
 typedef struct spmv_plan_s *spmv_plan_t;

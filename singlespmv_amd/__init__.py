@@ -35,8 +35,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libspmv_hip.so")
 OPT_LIB_PATH = os.path.join(HERE, "libopt_hip.so")
 
-FORMATS = {"auto": 0, "csr": 1, "crs": 1, "ell": 2, "ss": 3, "dia": 4, "hyb": 5, "css": 6}
-FORMAT_NAMES = {0: "auto", 1: "csr", 2: "ell", 3: "ss", 4: "dia", 5: "hyb", 6: "css"}
+FORMATS = {"auto": 0, "csr": 1, "crs": 1, "ell": 2, "ss": 3, "dia": 4, "hyb": 5, "css": 6, "coo": 7, "jds": 8}
+FORMAT_NAMES = {0: "auto", 1: "csr", 2: "ell", 3: "ss", 4: "dia", 5: "hyb", 6: "css", 7: "coo", 8: "jds"}
 X_DEVICE, Y_DEVICE, ASYNC, X_STAGED = 0x1, 0x2, 0x4, 0x8
 GEN_UNIFORM, GEN_POWERLAW, GEN_BANDED = 1, 2, 3
 

@@ -92,6 +92,8 @@ static int create_from_csr(const HostCsr &A, const spmv_options_t *opt_in, spmv_
         case SPMV_FORMAT_SS: st = build_ss(p, A, o); break;
         case SPMV_FORMAT_DIA: st = build_dia(p, A, o); break;
         case SPMV_FORMAT_CSS: st = build_css(p, A, o); break;
+        case SPMV_FORMAT_COO: st = build_coo(p, A, o); break;
+        case SPMV_FORMAT_JDS: st = build_jds(p, A, o); break;
         default:
             set_error("unknown format");
             st = SPMV_ERROR_INVALID_VALUE;
@@ -116,6 +118,8 @@ static int dispatch(const spmv_plan_s *p, const double *x, double *y) {
         case SPMV_FORMAT_SS: return launch_ss(p, x, y);
         case SPMV_FORMAT_DIA: return launch_dia(p, x, y);
         case SPMV_FORMAT_CSS: return launch_css(p, x, y);
+        case SPMV_FORMAT_COO: return launch_coo(p, x, y);
+        case SPMV_FORMAT_JDS: return launch_ell(p, x, y);
     }
     set_error("plan has an unknown format");
     return SPMV_ERROR_INVALID_VALUE;

@@ -101,8 +101,10 @@ int build_csr(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
 
 // ---------------------------------------------------------------- ELL
 // cap: maximum slots per row kept in the ELL part (HYB); INT32_MAX for ELL.
-int build_ell(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &, int cap) {
+// order (JDS): slice row i is matrix row order[i]; nullptr = identity.
+int build_ell(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &, int cap, const int32_t *order) {
     EllDev &e = p->ell;
+    auto src = [&](int64_t r) -> int64_t { return order ? (int64_t)order[r] : r; };
     e.n_slices = (A.m + 63) / 64;
     std::vector<int64_t> off((size_t)e.n_slices + 1, 0);
     int maxw = 0;
@@ -110,7 +112,7 @@ int build_ell(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &, int cap)
     for (int64_t s = 0; s < e.n_slices; ++s) {
         int64_t w = 0;
         const int64_t r1 = std::min<int64_t>(A.m, (s + 1) * 64);
-        for (int64_t r = s * 64; r < r1; ++r) w = std::max<int64_t>(w, A.row_ptr[r + 1] - A.row_ptr[r]);
+        for (int64_t r = s * 64; r < r1; ++r) w = std::max<int64_t>(w, A.row_ptr[src(r) + 1] - A.row_ptr[src(r)]);
         w = std::min<int64_t>(w, cap);
         w = round_up(w, 4);
         off[s + 1] = 64 * w;
@@ -128,8 +130,8 @@ int build_ell(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &, int cap)
             const int64_t r = s * 64 + li;
             int64_t len = 0, rs = 0;
             if (r < A.m) {
-                rs = A.row_ptr[r];
-                len = std::min<int64_t>(A.row_ptr[r + 1] - rs, w);
+                rs = A.row_ptr[src(r)];
+                len = std::min<int64_t>(A.row_ptr[src(r) + 1] - rs, w);
             }
             int32_t last = 0;
             for (int64_t k = 0; k < w; ++k) {
@@ -153,6 +155,43 @@ int build_ell(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &, int cap)
     p->algo_bytes = 12 * A.nnz + 8 * A.n + 8 * A.m;
     p->n_kernels = 1;
     p->kernel_name = "ell_slice_kernel";
+    return SPMV_SUCCESS;
+}
+
+// ---------------------------------------------------------------- JDS
+// opt_jds (src/opt_jds.cpp:29-71): rows sorted by decreasing length (stable),
+// stored as 64-row jagged slices of the sliced-ELL layout; y is written back
+// through the permutation.  Each row is still summed in its own order.
+int build_jds(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
+    std::vector<int32_t> order((size_t)std::max<int64_t>(A.m, 1));
+    std::iota(order.begin(), order.begin() + A.m, 0);
+    std::stable_sort(order.begin(), order.begin() + A.m, [&](int32_t a, int32_t b) {
+        return A.row_ptr[a + 1] - A.row_ptr[a] > A.row_ptr[b + 1] - A.row_ptr[b];
+    });
+    SPMV_RETURN_IF(build_ell(p, A, o, INT32_MAX, order.data()));
+    SPMV_RETURN_IF(upload(p, &p->ell.perm, order.data(), A.m));
+    p->algo_bytes += 4 * A.m;
+    p->kernel_name = "ell_slice_kernel<perm>";
+    return SPMV_SUCCESS;
+}
+
+// ---------------------------------------------------------------- COO
+// opt_coo (src/opt_coo.cpp:21-47): zero y, then y[row] += val*x[col] with
+// atomics; here one f64 atomic per equal-row run of a wave instead of one
+// per entry.
+int build_coo(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &) {
+    CooDev &c = p->coo;
+    std::vector<int32_t> row((size_t)std::max<int64_t>(A.nnz, 1));
+#pragma omp parallel for schedule(dynamic, 1024)
+    for (int64_t r = 0; r < A.m; ++r)
+        for (int64_t j = A.row_ptr[r]; j < A.row_ptr[r + 1]; ++j) row[(size_t)j] = (int32_t)r;
+    SPMV_RETURN_IF(upload(p, &c.row, row.data(), A.nnz));
+    SPMV_RETURN_IF(upload(p, &c.col, A.col, A.nnz));
+    SPMV_RETURN_IF(upload(p, &c.val, A.val, A.nnz));
+    p->stored_slots = A.nnz;
+    p->algo_bytes = 16 * A.nnz + 8 * A.n + 8 * A.m;
+    p->n_kernels = 2;
+    p->kernel_name = "coo_segment_kernel";
     return SPMV_SUCCESS;
 }
 

@@ -72,6 +72,7 @@ struct CsrDev {
 // instruction reads 1 KiB contiguous.  Padding: col = last real col of the
 // row (0 for an empty row), val = 0 -> adds +0.0, no new cache line.
 struct EllDev {
+    int32_t *perm = nullptr;       // JDS: slice row i -> matrix row perm[i]
     int64_t n_slices = 0;
     int64_t *slice_off = nullptr;  // [n_slices + 1] in slots
     int32_t *col = nullptr;
@@ -112,6 +113,15 @@ struct SsDev {
     int64_t n_nonempty = 0;
     int32_t *empty_rows = nullptr;
     int64_t n_empty = 0;
+};
+
+// COO (opt_coo, src/opt_coo.cpp): sorted (row, col, val); one wave handles
+// 64 consecutive entries per step, reduces equal-row runs in registers and
+// issues one f64 atomic add per run (y zeroed first).
+struct CooDev {
+    int32_t *row = nullptr;
+    int32_t *col = nullptr;
+    double *val = nullptr;
 };
 
 // DIA (opt_dia, src/opt_dia.cpp), row-indexed: val[d*mp + r] = A[r, r+off[d]]
@@ -161,6 +171,7 @@ struct spmv_plan_s {
     spmv::SsDev ss;
     spmv::DiaDev dia;
     spmv::CssDev css;
+    spmv::CooDev coo;
     double *x_stage = nullptr;  // host-x staging (opt_cusparse.cpp:44-45)
     double *y_stage = nullptr;
     int64_t stored_slots = 0;
@@ -182,11 +193,14 @@ struct HostCsr {
 
 // formats.cpp -- build + upload one format into `p`.
 int build_csr(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o);
-int build_ell(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o, int cap);
+int build_ell(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o, int cap,
+              const int32_t *order = nullptr);
 int build_hyb(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o);
 int build_ss(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o);
 int build_dia(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o);
 int build_css(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o);
+int build_coo(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o);
+int build_jds(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o);
 int choose_format(const HostCsr &A, const spmv_options_t &o);
 int auto_csr_lanes(double mean_row);
 int auto_ss_sigma(double mean_row);
@@ -198,5 +212,6 @@ int launch_hyb_overflow(const spmv_plan_s *p, const double *x, double *y);
 int launch_ss(const spmv_plan_s *p, const double *x, double *y);
 int launch_dia(const spmv_plan_s *p, const double *x, double *y);
 int launch_css(const spmv_plan_s *p, const double *x, double *y);
+int launch_coo(const spmv_plan_s *p, const double *x, double *y);
 
 }  // namespace spmv

@@ -9,14 +9,17 @@
 // wave-uniform, so the loop has no divergence.  Each row is summed
 // sequentially in slot order with a rounded multiply + rounded add, i.e. the
 // same arithmetic as opt_crs/opt_ell (bit-exact against oracle/).  Padding
-// slots carry val = 0 and repeat a real column of the row.
+// slots carry val = 0 and repeat a real column of the row.  With PERM the
+// slices hold rows sorted by length (JDS, src/opt_jds.cpp:29-71, 91-103) and
+// y is written through the permutation.
 #include "device.hpp"
 #include "internal.hpp"
 
 namespace spmv {
 
-template <int UNROLL, bool ADD>
+template <int UNROLL, bool ADD, bool PERM>
 __global__ __launch_bounds__(256) void ell_slice_kernel(int64_t m, int64_t n_slices,
+                                                        const int32_t *__restrict__ perm,
                                                         const int64_t *__restrict__ slice_off,
                                                         const int32_t *__restrict__ col,
                                                         const double *__restrict__ val,
@@ -66,8 +69,9 @@ __global__ __launch_bounds__(256) void ell_slice_kernel(int64_t m, int64_t n_sli
         acc = madd(b.x, g2, acc);
         acc = madd(b.y, g3, acc);
     }
-    const int64_t row = slice * 64 + lane;
-    if (row < m) {
+    const int64_t srow = slice * 64 + lane;
+    if (srow < m) {
+        const int64_t row = PERM ? (int64_t)perm[srow] : srow;  // JDS: back to matrix order
         if (ADD) y[row] = __dadd_rn(y[row], acc);
         else y[row] = acc;
     }
@@ -77,8 +81,12 @@ int launch_ell(const spmv_plan_s *p, const double *x, double *y) {
     const EllDev &e = p->ell;
     if (e.n_slices == 0) return SPMV_SUCCESS;
     const int64_t blocks = (e.n_slices + 3) / 4;
-    hipLaunchKernelGGL((ell_slice_kernel<4, false>), dim3((unsigned)blocks), dim3(256), 0, p->stream,
-                       p->m, e.n_slices, e.slice_off, e.col, e.val, x, y);
+    if (e.perm)
+        hipLaunchKernelGGL((ell_slice_kernel<4, false, true>), dim3((unsigned)blocks), dim3(256), 0, p->stream,
+                           p->m, e.n_slices, e.perm, e.slice_off, e.col, e.val, x, y);
+    else
+        hipLaunchKernelGGL((ell_slice_kernel<4, false, false>), dim3((unsigned)blocks), dim3(256), 0,
+                           p->stream, p->m, e.n_slices, e.perm, e.slice_off, e.col, e.val, x, y);
     SPMV_HIP_TRY(hipGetLastError());
     return SPMV_SUCCESS;
 }

@@ -22,7 +22,7 @@ from conftest import golden_names, load_golden
 
 pytestmark = pytest.mark.gpu
 
-FORMATS = ["csr", "ell", "ss", "hyb", "dia", "css", "auto"]
+FORMATS = ["csr", "ell", "ss", "hyb", "dia", "css", "coo", "jds", "auto"]
 REL = 1e-12
 
 
@@ -76,7 +76,7 @@ def test_golden(name, fmt):
     elif not signed:
         check_close(y, yref, what=f"{name}/{fmt}")
     info = plan.info()
-    sequential = info["format"] in ("ell", "dia") or (info["format"] == "csr" and info["csr_lanes"] == 1) \
+    sequential = info["format"] in ("ell", "dia", "jds") or (info["format"] == "csr" and info["csr_lanes"] == 1) \
         or (info["format"] == "css" and info["css_split_rows"] == 0)
     if sequential:
         assert np.array_equal(y, yref), f"{info['format']} is sequential: must be bit-exact"
@@ -199,13 +199,33 @@ def test_css_multi_pass():
     assert np.array_equal(y, oracle_y(rp, col, val, x))
 
 
+def test_jds_permutation_and_coo_atomics():
+    """JDS (rows sorted by length, y permuted back) is the sequential row sum;
+    COO (one f64 atomic per row run per wave) is within 1e-12 and exact for
+    every row that sits inside one 64-entry step."""
+    m = 50000
+    spec = sp.gen_spec("powerlaw", m, max_len=1500, seed=73)
+    rp, col, val = sp.generate_csr(spec)
+    x = sp.generate_vector(m, seed=79)
+    yo = oracle_y(rp, col, val, x)
+    pj = sp.Plan.from_csr(m, m, rp, col, val, "jds")
+    assert np.array_equal(run_plan(pj, x, m), yo)
+    pc = sp.Plan.from_csr(m, m, rp, col, val, "coo")
+    y = np.full(m, np.nan)
+    pc.execute(x, y)
+    check_close(y, yo, what="coo")
+    lens = np.diff(rp)
+    inside = (rp[:-1] // 64 == (rp[1:] - 1) // 64) & (lens > 0)
+    assert np.array_equal(y[inside], yo[inside])
+
+
 def test_integer_exact_all_formats():
     m = 40000
     spec = sp.gen_spec("powerlaw", m, max_len=2000, integer_values=True, seed=41)
     rp, col, val = sp.generate_csr(spec)
     x = sp.generate_vector(m, seed=43, integer_values=True)
     yo = oracle_y(rp, col, val, x)
-    for fmt in ["csr", "ell", "ss", "hyb", "css"]:
+    for fmt in ["csr", "ell", "ss", "hyb", "css", "coo", "jds"]:
         y = run_plan(sp.Plan.from_csr(m, m, rp, col, val, fmt), x, m)
         assert np.array_equal(y, yo), fmt
 
@@ -219,7 +239,7 @@ def test_rectangular_and_empty():
         val = rng.random(rp[-1])
         x = rng.random(n)
         yo = oracle_y(rp, col, val, x) if m else np.zeros(0)
-        for fmt in ["csr", "ell", "ss", "hyb", "css"]:
+        for fmt in ["csr", "ell", "ss", "hyb", "css", "coo", "jds"]:
             plan = sp.Plan.from_csr(m, n, rp, col, val, fmt)
             y = np.full(m, 7.0)
             plan.execute(x, y)
