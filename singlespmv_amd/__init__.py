@@ -80,7 +80,7 @@ class GenSpec(C.Structure):
 # Exported symbols of include/spmv_hip.h (checked by tests/test_abi.py).
 EXPORTS = [
     "spmv_options_default", "spmv_plan_create_coo", "spmv_plan_create_csr",
-    "spmv_plan_create_csr32", "spmv_plan_destroy", "spmv_execute", "spmv_set_stream",
+    "spmv_plan_create_csr32", "spmv_plan_create_csr_device", "spmv_plan_destroy", "spmv_execute", "spmv_set_stream",
     "spmv_time", "spmv_plan_info", "spmv_status_string", "spmv_last_error",
     "spmv_load_mtx", "spmv_free_host", "spmv_srand", "spmv_rand_vector", "spmv_verify_coo",
     "spmv_coo_to_csr", "spmv_gen_count", "spmv_gen_fill", "spmv_gen_vector",
@@ -104,6 +104,8 @@ def lib():
     L.spmv_plan_create_coo.argtypes = [i32, i32, i32, vp, vp, vp, C.POINTER(Options), C.POINTER(vp)]
     L.spmv_plan_create_csr.argtypes = [i64, i64, i64, vp, vp, vp, C.POINTER(Options), C.POINTER(vp)]
     L.spmv_plan_create_csr32.argtypes = [i32, i32, i32, vp, vp, vp, C.POINTER(Options), C.POINTER(vp)]
+    L.spmv_plan_create_csr_device.argtypes = [i64, i64, i64, vp, vp, vp, C.POINTER(Options),
+                                              C.POINTER(vp)]
     L.spmv_plan_destroy.argtypes = [vp]
     L.spmv_execute.argtypes = [vp, vp, vp, C.c_uint32]
     L.spmv_set_stream.argtypes = [vp, vp]
@@ -273,6 +275,24 @@ class Plan:
         _check(lib().spmv_plan_create_csr(m, n, len(val), rp.ctypes.data, col.ctypes.data,
                                           val.ctypes.data, C.byref(o), C.byref(h)),
                "spmv_plan_create_csr")
+        return cls(h.value)
+
+    @classmethod
+    def from_device_csr(cls, m: int, n: int, row_ptr, col, val, fmt="auto", **opts) -> "Plan":
+        """Plan from torch CUDA tensors (int64 row_ptr, int32 col, float64
+        val): CSR and SS are converted on the device, other formats stage
+        through the host (spmv_plan_create_csr_device)."""
+        for name, t, dt in (("row_ptr", row_ptr, torch.int64), ("col", col, torch.int32),
+                            ("val", val, torch.float64)):
+            if not _is_device(t) or t.dtype != dt or not t.is_contiguous():
+                raise ValueError(f"{name} must be a contiguous {dt} CUDA tensor")
+        if "device" not in opts:
+            opts["device"] = row_ptr.device.index or 0
+        o = make_options(fmt, **opts)
+        h = C.c_void_p()
+        _check(lib().spmv_plan_create_csr_device(m, n, val.numel(), _ptr(row_ptr), _ptr(col), _ptr(val),
+                                                 C.byref(o), C.byref(h)),
+               "spmv_plan_create_csr_device")
         return cls(h.value)
 
     @classmethod

@@ -162,6 +162,74 @@ int spmv_plan_create_csr32(int32_t m, int32_t n, int32_t nnz, const int32_t *row
     return create_from_csr(A, opt, plan);
 }
 
+int spmv_plan_create_csr_device(int64_t m, int64_t n, int64_t nnz, const int64_t *d_row_ptr,
+                                const int32_t *d_col_idx, const double *d_val, const spmv_options_t *opt_in,
+                                spmv_plan_t *out) {
+    SPMV_CHECK_ARG(out != nullptr, "plan out-pointer is NULL");
+    *out = nullptr;
+    spmv_options_t o;
+    if (opt_in) o = *opt_in;
+    else spmv_options_default(&o);
+    SPMV_CHECK_ARG(m >= 0 && n >= 0 && nnz >= 0, "negative dimension");
+    SPMV_CHECK_ARG(m < (int64_t)INT32_MAX && n < (int64_t)INT32_MAX, "m and n must be < 2^31 (int32 column indices)");
+    SPMV_CHECK_ARG(d_row_ptr != nullptr, "row_ptr is NULL");
+    SPMV_CHECK_ARG(nnz == 0 || (d_col_idx != nullptr && d_val != nullptr), "col/val is NULL");
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count == 0) {
+        (void)hipGetLastError();
+        set_error("no HIP device visible (libspmv_hip needs an MI355X / gfx950)");
+        return SPMV_ERROR_NO_DEVICE;
+    }
+    int dev = o.device;
+    if (dev < 0) SPMV_HIP_TRY(hipGetDevice(&dev));
+    SPMV_RETURN_IF(check_device(dev));
+    SPMV_HIP_TRY(hipSetDevice(dev));
+    const void *ptrs[3] = {d_row_ptr, d_col_idx, d_val};
+    for (int k = 0; k < (nnz ? 3 : 1); ++k) {
+        hipPointerAttribute_t a;
+        if (hipPointerGetAttributes(&a, ptrs[k]) != hipSuccess || a.type != hipMemoryTypeDevice || a.device != dev) {
+            (void)hipGetLastError();
+            set_error("spmv_plan_create_csr_device: arrays must be device memory on the plan's device");
+            return SPMV_ERROR_INVALID_VALUE;
+        }
+    }
+    SPMV_RETURN_IF(validate_csr_device(d_row_ptr, m, d_col_idx, nnz, n));
+    if (o.format != SPMV_FORMAT_CSR && o.format != SPMV_FORMAT_SS) {
+        // host builders: stage the CSR through host memory
+        std::vector<int64_t> rp((size_t)m + 1);
+        std::vector<int32_t> col((size_t)nnz);
+        std::vector<double> val((size_t)nnz);
+        SPMV_HIP_TRY(hipMemcpy(rp.data(), d_row_ptr, 8 * (size_t)(m + 1), hipMemcpyDeviceToHost));
+        if (nnz) {
+            SPMV_HIP_TRY(hipMemcpy(col.data(), d_col_idx, 4 * (size_t)nnz, hipMemcpyDeviceToHost));
+            SPMV_HIP_TRY(hipMemcpy(val.data(), d_val, 8 * (size_t)nnz, hipMemcpyDeviceToHost));
+        }
+        o.device = dev;
+        HostCsr A{m, n, nnz, rp.data(), col.data(), val.data()};
+        return create_from_csr(A, &o, out);
+    }
+    spmv_plan_s *p = new (std::nothrow) spmv_plan_s;
+    if (!p) {
+        set_error("host allocation of the plan failed");
+        return SPMV_ERROR_OUT_OF_MEMORY;
+    }
+    p->device = dev;
+    p->m = m;
+    p->n = n;
+    p->nnz = nnz;
+    const double mean = m ? (double)nnz / (double)m : 0.0;
+    const int st = o.format == SPMV_FORMAT_CSR ? build_csr_device(p, d_row_ptr, d_col_idx, d_val, o, mean)
+                                               : build_ss_device(p, d_row_ptr, d_col_idx, d_val, o, mean);
+    if (st != SPMV_SUCCESS) {
+        p->arena.release();
+        delete p;
+        return st;
+    }
+    p->format = o.format;
+    *out = p;
+    return SPMV_SUCCESS;
+}
+
 int spmv_coo_to_csr(int32_t m, int64_t nnz, const int32_t *row_idx, int64_t *row_ptr) {
     SPMV_CHECK_ARG(m >= 0 && nnz >= 0 && row_ptr != nullptr, "bad arguments");
     SPMV_CHECK_ARG(nnz == 0 || row_idx != nullptr, "row_idx is NULL");
