@@ -60,6 +60,15 @@ def parse():
 
 def main():
     args = parse()
+    # host cores of this process, read before any OpenMP runtime pins the
+    # main thread to one place
+    host_cores = len(os.sched_getaffinity(0))
+    if int(os.environ.get("WORLD_SIZE", "1")) == 1:
+        # CPU baseline on all cores of the affinity, pinned (SURVEY §8(d):
+        # binding moved the reference CRS from 4.5 to 7.0 GFLOP/s); set before
+        # any OpenMP runtime is loaded.  Not for N>1: ranks share the host.
+        os.environ.setdefault("OMP_PROC_BIND", "close")
+        os.environ.setdefault("OMP_PLACES", "cores")
     import torch
     import torch.distributed as dist
 
@@ -164,6 +173,7 @@ def main():
             r[k] = info[k]
         results[fmt] = r
         if fi == 0:
+            r["phases_ms"] = plan.profile(x, y, 10)
             headline = (plan, info, r)
             y_head = y.clone()
         else:
@@ -196,20 +206,26 @@ def main():
     max_rel = None
     if rank == 0 and world == 1 and not args.no_cpu:
         import oracle
-        cores = len(os.sched_getaffinity(0))
-        nthreads = min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)))
+        nthreads = min(host_cores, int(os.environ.get("OMP_NUM_THREADS", host_cores)))
         t_cpu, loop, y_cpu = oracle.csr_time(rp, col, val, x.cpu().numpy(), nthreads=nthreads,
                                              min_seconds=args.cpu_seconds, ntry=3)
         ygpu = y_head.cpu().numpy()
         max_rel = float(np.max(np.abs(ygpu - y_cpu) / np.maximum(np.abs(y_cpu), 1e-300)))
         cpu = {"value": 2.0 * nnz_local / t_cpu / 1e9, "unit": "GFLOP/s", "cores": nthreads,
-               "kind": "port",
+               "kind": "port", "nproc": os.cpu_count(),
+               "omp_proc_bind": os.environ.get("OMP_PROC_BIND"),
+               "omp_places": os.environ.get("OMP_PLACES"),
                "sample": f"full {rows}-row matrix, oracle opt_crs restatement (OpenMP static), "
                          f"{loop} calls x 3 trials after a {args.cpu_seconds:.0f} s doubling warm-up, "
                          f"min mean per call",
                "ms_per_call": t_cpu * 1e3}
 
     achieved = r["achieved_gbs"]
+    # measured STREAM-read ceiling of this GPU (reported beside the spec peak)
+    stream_gbs = sp.stream_probe(local, 2 << 30, 10)
+    # the reference's CSR5 byte model (CSR5_cuda/detail/utils.h:10-14), which
+    # charges x per nnz -- for comparability with published CSR5 numbers only
+    csr5_bytes = (rows + 1 + nnz_local) * 4 + (2 * nnz_local + rows) * 8
     out = {
         "metric": "SpMV GFLOP/s (fp64) + achieved HBM GB/s",
         "value": r["gflops"],
@@ -231,7 +247,9 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                      "kernel": r["kernel"], "algo_bytes_per_launch": r["algo_bytes"],
-                     "launch_ms": r["event_ms_per_launch"]},
+                     "launch_ms": r["event_ms_per_launch"],
+                     "stream_ceiling_gbs": stream_gbs, "frac_of_stream": achieved / stream_gbs,
+                     "csr5_model_gbs": csr5_bytes / (r["event_ms_per_launch"] * 1e-3) / 1e9},
         "cpu_baseline": cpu,
         "formats": results,
         "gen_s": round(t_gen, 2),

@@ -20,6 +20,9 @@
  *                          y = 1*A*x + 0*y, D2H y).
  *   spmv_plan_destroy      (the reference never frees; no counterpart)
  *   spmv_load_mtx          LoadSparseMatrix (src/util.cpp:30-66), parallel
+ *   spmv_load_mtx_csr      the CSR5 benchmark's banner-aware loader
+ *                          (CSR5_cuda/main.cu:157-306): pattern/integer,
+ *                          symmetric expansion, straight to CSR
  *   spmv_{save,load}_csr_bin (new) binary CSR cache
  *   spmv_rand_vector       srand + CreateRandomVector (src/main.cpp:18,
  *                          src/util.cpp:92-102)
@@ -124,6 +127,20 @@ int spmv_plan_create_csr_device(int64_t m, int64_t n, int64_t nnz, const int64_t
 
 int spmv_plan_destroy(spmv_plan_t plan);
 
+/* ---- per-phase profile (replaces the g_profile / PROF_BEGIN instrumentation
+ * of src/util.cpp:16-18, src/util.h:59-65 and the Mul/Sum split printed by
+ * src/main.cpp:172-175).  Runs `iters` synchronised calls on device x/y and
+ * returns the mean ms of each phase of the plan's launch sequence:
+ *   CSR "csr" | ELL, JDS "ell" | HYB "ell","overflow" | SS "tile","fixup" |
+ *   DIA "dia" | CSS "sweep" | COO "zero_y","segment". */
+int spmv_profile(spmv_plan_t plan, const double *x_dev, double *y_dev, int32_t iters,
+                 double *phase_ms, int32_t max_phases, int32_t *n_phases);
+const char *spmv_phase_name(spmv_plan_t plan, int32_t k);
+
+/* Measured STREAM-read ceiling of `device` (GB/s): nontemporal 16-byte reads
+ * of a `bytes` buffer (use >> 256 MB), `iters` launches timed with events. */
+int spmv_stream_probe(int32_t device, int64_t bytes, int32_t iters, double *read_gbs);
+
 /* ---- execution ----------------------------------------------------------- */
 #define SPMV_X_DEVICE 0x1u /* x is a device pointer (else host: H2D per call) */
 #define SPMV_Y_DEVICE 0x2u /* y is a device pointer (else host: D2H per call) */
@@ -177,6 +194,19 @@ const char *spmv_last_error(void);
 int spmv_load_mtx(const char *path, int32_t *m, int32_t *n, int32_t *nnz,
                   int32_t **row_idx, int32_t **col_idx, double **val);
 void spmv_free_host(void *p);
+
+/* Banner-aware Matrix Market -> CSR with the CSR5 benchmark's semantics
+ * (opt/Benchmark_SpMV_using_CSR5/CSR5_cuda/main.cu:157-306): needs a
+ * "%%MatrixMarket matrix coordinate <field> <symmetry>" banner; field real |
+ * integer | pattern (values 1.0); complex -> SPMV_ERROR_NOT_SUPPORTED;
+ * symmetric/hermitian off-diagonal entries are mirrored (skew-symmetric is
+ * not, as in the reference).  Rows keep file order (a mirrored entry right
+ * after its original) unless SPMV_MTX_SORT_COLUMNS.  *info (optional) =
+ * field (0 real, 1 integer, 2 pattern) | 4 if mirrored | 8 if skew. */
+#define SPMV_MTX_SORT_COLUMNS 0x1u
+#define SPMV_MTX_NO_EXPAND 0x2u
+int spmv_load_mtx_csr(const char *path, uint32_t flags, int64_t *m, int64_t *n, int64_t *nnz,
+                      int64_t **row_ptr, int32_t **col_idx, double **val, uint32_t *info);
 
 /* Binary CSR cache ("SPMVCSR1": header, int64 row_ptr, int32 col, f64 val) so
  * a large Matrix Market file is parsed once.  Arrays from the loader are

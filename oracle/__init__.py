@@ -256,3 +256,62 @@ def ref_spmv(fmt: str, m, n, row, col, val, x, y_init=None, calls: int = 2
                    np.ascontiguousarray(val, np.float64),
                    np.ascontiguousarray(x, np.float64), y, calls)
     return y[:m], bool(ok)
+
+
+def load_mtx_csr5(path: str):
+    """Pure-Python restatement of the CSR5 benchmark's loader
+    (opt/Benchmark_SpMV_using_CSR5/CSR5_cuda/main.cu:157-306) for small files:
+    banner field/symmetry (:169-193), fscanf triplets (:208-239), counters +
+    mirrored counts (:241-247), exclusive scan (:249-258), file-order scatter
+    with the mirrored copy right after its original (:266-300).
+    Returns (m, n, row_ptr, col, val) or raises ValueError."""
+    with open(path) as f:
+        banner = f.readline().split()
+        if len(banner) < 5 or banner[0].lower() != "%%matrixmarket":
+            raise ValueError("banner")
+        field, sym = banner[3].lower(), banner[4].lower()
+        if field == "complex":
+            raise ValueError("complex")
+        lines = f.read().split("\n")
+    i = 0
+    while lines[i].startswith("%") or not lines[i].strip():
+        i += 1
+    m, n, nnz_rep = (int(t) for t in lines[i].split()[:3])
+    toks = " ".join(lines[i + 1:]).split()
+    per = 2 if field == "pattern" else 3
+    rows, cols, vals = [], [], []
+    for e in range(nnz_rep):
+        r, c = int(toks[per * e]) - 1, int(toks[per * e + 1]) - 1
+        if field == "pattern":
+            v = 1.0
+        elif field == "integer":
+            v = float(int(toks[per * e + 2]))
+        else:
+            v = float(toks[per * e + 2])
+        rows.append(r)
+        cols.append(c)
+        vals.append(v)
+    symmetric = sym in ("symmetric", "hermitian")
+    counter = [0] * (m + 1)
+    for r in rows:
+        counter[r] += 1
+    if symmetric:
+        for r, c in zip(rows, cols):
+            if r != c:
+                counter[c] += 1
+    ptr = [0] * (m + 1)
+    for r in range(1, m + 1):
+        ptr[r] = ptr[r - 1] + counter[r - 1]
+    nnz = ptr[m]
+    col = [0] * nnz
+    val = [0.0] * nnz
+    fill = [0] * m
+    for r, c, v in zip(rows, cols, vals):
+        off = ptr[r] + fill[r]
+        col[off], val[off] = c, v
+        fill[r] += 1
+        if symmetric and r != c:
+            off = ptr[c] + fill[c]
+            col[off], val[off] = r, v
+            fill[c] += 1
+    return m, n, np.array(ptr, np.int64), np.array(col, np.int32), np.array(val, np.float64)

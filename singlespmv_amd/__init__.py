@@ -81,8 +81,8 @@ class GenSpec(C.Structure):
 EXPORTS = [
     "spmv_options_default", "spmv_plan_create_coo", "spmv_plan_create_csr",
     "spmv_plan_create_csr32", "spmv_plan_create_csr_device", "spmv_plan_destroy", "spmv_execute", "spmv_set_stream",
-    "spmv_time", "spmv_plan_info", "spmv_status_string", "spmv_last_error",
-    "spmv_load_mtx", "spmv_free_host", "spmv_srand", "spmv_rand_vector", "spmv_verify_coo",
+    "spmv_time", "spmv_profile", "spmv_phase_name", "spmv_stream_probe", "spmv_plan_info", "spmv_status_string", "spmv_last_error",
+    "spmv_load_mtx", "spmv_load_mtx_csr", "spmv_free_host", "spmv_srand", "spmv_rand_vector", "spmv_verify_coo",
     "spmv_coo_to_csr", "spmv_gen_count", "spmv_gen_fill", "spmv_gen_vector",
     "spmv_partition_rows", "spmv_save_csr_bin", "spmv_load_csr_bin",
 ]
@@ -110,6 +110,10 @@ def lib():
     L.spmv_execute.argtypes = [vp, vp, vp, C.c_uint32]
     L.spmv_set_stream.argtypes = [vp, vp]
     L.spmv_time.argtypes = [vp, vp, vp, i32, C.POINTER(f64)]
+    L.spmv_profile.argtypes = [vp, vp, vp, i32, C.POINTER(f64), i32, C.POINTER(i32)]
+    L.spmv_stream_probe.argtypes = [i32, i64, i32, C.POINTER(f64)]
+    L.spmv_phase_name.argtypes = [vp, i32]
+    L.spmv_phase_name.restype = C.c_char_p
     L.spmv_plan_info.argtypes = [vp, C.POINTER(PlanInfo)]
     L.spmv_status_string.argtypes = [C.c_int]
     L.spmv_status_string.restype = C.c_char_p
@@ -117,6 +121,10 @@ def lib():
     L.spmv_load_mtx.argtypes = [C.c_char_p, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32),
                                 C.POINTER(C.POINTER(i32)), C.POINTER(C.POINTER(i32)),
                                 C.POINTER(C.POINTER(f64))]
+    L.spmv_load_mtx_csr.argtypes = [C.c_char_p, C.c_uint32, C.POINTER(i64), C.POINTER(i64),
+                                    C.POINTER(i64), C.POINTER(C.POINTER(i64)),
+                                    C.POINTER(C.POINTER(C.c_int32)), C.POINTER(C.POINTER(f64)),
+                                    C.POINTER(C.c_uint32)]
     L.spmv_free_host.argtypes = [vp]
     L.spmv_srand.argtypes = [C.c_uint32]
     L.spmv_rand_vector.argtypes = [i32, _F64P]
@@ -193,6 +201,26 @@ def load_sparse_matrix(path: str) -> SpMat:
     return out
 
 
+def load_mtx_csr(path: str, sort_columns: bool = False, expand: bool = True):
+    """(m, n, row_ptr, col, val, info) with the CSR5 benchmark's loader
+    semantics (CSR5_cuda/main.cu:157-306); info = {"field", "mirrored", "skew"}."""
+    L = lib()
+    m, n, nnz, inf = C.c_int64(), C.c_int64(), C.c_int64(), C.c_uint32()
+    rp, c, v = C.POINTER(C.c_int64)(), C.POINTER(C.c_int32)(), C.POINTER(C.c_double)()
+    flags = (1 if sort_columns else 0) | (0 if expand else 2)
+    _check(L.spmv_load_mtx_csr(path.encode(), flags, C.byref(m), C.byref(n), C.byref(nnz), C.byref(rp),
+                               C.byref(c), C.byref(v), C.byref(inf)), f"load_mtx_csr({path})")
+    k = nnz.value
+    out = (m.value, n.value, np.ctypeslib.as_array(rp, shape=(m.value + 1,)).copy(),
+           np.ctypeslib.as_array(c, shape=(max(k, 1),))[:k].copy(),
+           np.ctypeslib.as_array(v, shape=(max(k, 1),))[:k].copy(),
+           {"field": ["real", "integer", "pattern"][inf.value & 3], "mirrored": bool(inf.value & 4),
+            "skew": bool(inf.value & 8)})
+    for q in (rp, c, v):
+        L.spmv_free_host(C.cast(q, C.c_void_p))
+    return out
+
+
 def save_csr_bin(path: str, m: int, n: int, row_ptr, col, val) -> None:
     """Write the SPMVCSR1 binary cache (parse a .mtx once, mmap-load later)."""
     rp = np.ascontiguousarray(row_ptr, np.int64)
@@ -235,6 +263,13 @@ def verify_result(A: SpMat, x: np.ndarray, y: np.ndarray) -> bool:
                                 np.ascontiguousarray(x, np.float64),
                                 np.ascontiguousarray(y, np.float64))
     return bad < 0
+
+
+def stream_probe(device: int = 0, bytes_: int = 2 << 30, iters: int = 10) -> float:
+    """Measured STREAM-read GB/s of the device (the practical HBM ceiling)."""
+    g = C.c_double()
+    _check(lib().spmv_stream_probe(device, bytes_, iters, C.byref(g)), "spmv_stream_probe")
+    return g.value
 
 
 def coo_to_csr(m: int, row_idx: np.ndarray) -> np.ndarray:
@@ -338,6 +373,16 @@ class Plan:
         ms = C.c_double()
         _check(lib().spmv_time(self._h, _ptr(x_dev), _ptr(y_dev), iters, C.byref(ms)), "spmv_time")
         return ms.value
+
+    def profile(self, x_dev, y_dev, iters: int = 10) -> dict:
+        """Mean ms per phase of one execute ({"tile": .., "fixup": ..} for SS),
+        the counterpart of the reference's g_profile Mul/Sum split."""
+        ms = (C.c_double * 8)()
+        n = C.c_int32()
+        _check(lib().spmv_profile(self._h, _ptr(x_dev), _ptr(y_dev), iters, ms, 8, C.byref(n)),
+               "spmv_profile")
+        L = lib()
+        return {L.spmv_phase_name(self._h, k).decode() or f"phase{k}": ms[k] for k in range(n.value)}
 
     def info(self) -> dict:
         i = PlanInfo()

@@ -114,6 +114,7 @@ static int dispatch(const spmv_plan_s *p, const double *x, double *y) {
         case SPMV_FORMAT_ELL: return launch_ell(p, x, y);
         case SPMV_FORMAT_HYB:
             SPMV_RETURN_IF(launch_ell(p, x, y));
+            phase_mark(p);  // ell | overflow
             return launch_hyb_overflow(p, x, y);
         case SPMV_FORMAT_SS: return launch_ss(p, x, y);
         case SPMV_FORMAT_DIA: return launch_dia(p, x, y);
@@ -325,6 +326,50 @@ int spmv_time(spmv_plan_t p, const double *x_dev, double *y_dev, int32_t iters, 
     (void)hipEventDestroy(a);
     (void)hipEventDestroy(b);
     *ms = f;
+    return st;
+}
+
+static const char *const kPhases[][3] = {
+    {"", "", ""},           {"csr", "", ""},   {"ell", "", ""},     {"tile", "fixup", ""},
+    {"dia", "", ""},        {"ell", "overflow", ""}, {"sweep", "", ""}, {"zero_y", "segment", ""},
+    {"ell", "", ""}};
+
+const char *spmv_phase_name(spmv_plan_t p, int32_t k) {
+    if (!p || k < 0 || k > 2 || p->format < 0 || p->format > SPMV_FORMAT_JDS) return "";
+    return kPhases[p->format][k];
+}
+
+int spmv_profile(spmv_plan_t p, const double *x_dev, double *y_dev, int32_t iters, double *phase_ms,
+                 int32_t max_phases, int32_t *n_phases) {
+    SPMV_CHECK_ARG(p != nullptr && iters > 0 && phase_ms != nullptr && n_phases != nullptr && max_phases > 0,
+                   "bad arguments");
+    SPMV_RETURN_IF(bind_device(p));
+    for (auto &e : p->prof_ev) SPMV_HIP_TRY(hipEventCreate(&e));
+    std::vector<double> acc(8, 0.0);
+    int nph = 1, st = SPMV_SUCCESS;
+    for (int i = 0; i < iters && st == SPMV_SUCCESS; ++i) {
+        p->prof_k = 0;
+        (void)hipEventRecord(p->prof_ev[0], p->stream);
+        st = dispatch(p, x_dev, y_dev);
+        const int k = p->prof_k;
+        p->prof_k = -1;
+        (void)hipEventRecord(p->prof_ev[k + 1], p->stream);
+        if (hipEventSynchronize(p->prof_ev[k + 1]) != hipSuccess) {
+            st = SPMV_ERROR_HIP;
+            set_error("spmv_profile: event synchronisation failed");
+            break;
+        }
+        nph = k + 1;
+        for (int j = 0; j <= k; ++j) {
+            float f = 0;
+            (void)hipEventElapsedTime(&f, p->prof_ev[j], p->prof_ev[j + 1]);
+            acc[j] += f;
+        }
+    }
+    p->prof_k = -1;
+    for (auto &e : p->prof_ev) (void)hipEventDestroy(e);
+    *n_phases = nph;
+    for (int j = 0; j < std::min(nph, max_phases); ++j) phase_ms[j] = acc[j] / iters;
     return st;
 }
 

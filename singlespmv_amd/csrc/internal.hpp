@@ -179,6 +179,10 @@ struct spmv_plan_s {
     int64_t algo_bytes = 0;
     int n_kernels = 1;
     std::string kernel_name;
+    // spmv_profile: per-phase events (the g_profile/PROF_BEGIN counterpart,
+    // src/util.h:59-65); prof_k < 0 = not profiling
+    mutable hipEvent_t prof_ev[9] = {};
+    mutable int prof_k = -1;
 };
 
 namespace spmv {
@@ -210,6 +214,11 @@ int build_ss_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, c
 int choose_format(const HostCsr &A, const spmv_options_t &o);
 int auto_csr_lanes(double mean_row);
 int auto_ss_sigma(double mean_row);
+
+// end of one phase of a multi-kernel launch (no-op unless profiling)
+inline void phase_mark(const spmv_plan_s *p) {
+    if (p->prof_k >= 0 && p->prof_k < 7) (void)hipEventRecord(p->prof_ev[++p->prof_k], p->stream);
+}
 
 // kernels -- launch y = A x on p->stream (device x, y).
 int launch_csr(const spmv_plan_s *p, const double *x, double *y);

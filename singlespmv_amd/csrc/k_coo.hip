@@ -38,6 +38,7 @@ __global__ __launch_bounds__(256) void coo_segment_kernel(int64_t nnz, const int
 
 int launch_coo(const spmv_plan_s *p, const double *x, double *y) {
     if (p->m) SPMV_HIP_TRY(hipMemsetAsync(y, 0, sizeof(double) * (size_t)p->m, p->stream));
+    phase_mark(p);  // zero_y | segment
     if (p->nnz == 0) return SPMV_SUCCESS;
     const int64_t waves = (p->nnz + 63) / 64;
     const int64_t blocks = std::min<int64_t>((waves + 3) / 4, 256 * 64);

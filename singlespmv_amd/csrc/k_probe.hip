@@ -1,0 +1,73 @@
+// k_probe.hip -- the measured STREAM-read ceiling SURVEY §8(d) asks bench.py
+// to report beside the 8 TB/s spec: a nontemporal 16-byte-per-lane read of
+// a buffer far larger than the 256 MB MALL, timed with HIP events.
+#include "device.hpp"
+#include "internal.hpp"
+
+namespace spmv {
+namespace {
+
+__global__ __launch_bounds__(256) void stream_read_kernel(const f64x2 *__restrict__ a, int64_t n2,
+                                                          double *__restrict__ sink) {
+    const int64_t G = (int64_t)gridDim.x * blockDim.x;
+    double acc = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n2; i += G * 4) {
+        f64x2 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int64_t j = i + u * G;
+            v[u] = j < n2 ? __builtin_nontemporal_load(a + j) : f64x2{0.0, 0.0};
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc += v[u].x + v[u].y;
+    }
+    if (acc == 12345.678) *sink = acc;  // keeps the loads live; never true for a zeroed buffer
+}
+
+}  // namespace
+}  // namespace spmv
+
+using namespace spmv;
+
+extern "C" int spmv_stream_probe(int32_t device, int64_t bytes, int32_t iters, double *read_gbs) {
+    SPMV_CHECK_ARG(read_gbs != nullptr && bytes >= (1 << 20) && iters > 0, "bad arguments");
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count == 0) {
+        (void)hipGetLastError();
+        set_error("no HIP device visible");
+        return SPMV_ERROR_NO_DEVICE;
+    }
+    SPMV_CHECK_ARG(device >= 0 && device < count, "device ordinal out of range");
+    SPMV_HIP_TRY(hipSetDevice(device));
+    const int64_t n2 = bytes / 16;
+    f64x2 *a = nullptr;
+    double *sink = nullptr;
+    SPMV_HIP_TRY(hipMalloc(&a, (size_t)n2 * 16));
+    if (hipMalloc(&sink, 8) != hipSuccess) {
+        (void)hipFree(a);
+        set_error("hipMalloc failed");
+        return SPMV_ERROR_OUT_OF_MEMORY;
+    }
+    (void)hipMemset(a, 0, (size_t)n2 * 16);
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    const unsigned blocks = 256 * 16;
+    hipLaunchKernelGGL(stream_read_kernel, dim3(blocks), dim3(256), 0, 0, a, n2, sink);  // warm-up
+    (void)hipEventRecord(e0, 0);
+    for (int i = 0; i < iters; ++i) hipLaunchKernelGGL(stream_read_kernel, dim3(blocks), dim3(256), 0, 0, a, n2, sink);
+    (void)hipEventRecord(e1, 0);
+    hipError_t e = hipEventSynchronize(e1);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    (void)hipFree(a);
+    (void)hipFree(sink);
+    if (e != hipSuccess) {
+        set_error(std::string("stream probe: ") + hipGetErrorString(e));
+        return SPMV_ERROR_HIP;
+    }
+    *read_gbs = (double)n2 * 16 * iters / (ms * 1e-3) / 1e9;
+    return SPMV_SUCCESS;
+}

@@ -151,6 +151,7 @@ int launch_ss(const spmv_plan_s *p, const double *x, double *y) {
         }
         SPMV_HIP_TRY(hipGetLastError());
     }
+    phase_mark(p);  // tile | fixup
     const int64_t work = s.n_tiles > s.n_empty ? s.n_tiles : s.n_empty;
     if (work > 0) {
         hipLaunchKernelGGL(ss_fixup_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0,

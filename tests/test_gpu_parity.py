@@ -379,3 +379,21 @@ def test_device_conversion_matches_host_build():
         sp.Plan.from_device_csr(2, 6, torch.tensor([0, 2, 2], device="cuda"), bad_col, v, "ss")
     with pytest.raises(ValueError):
         sp.Plan.from_device_csr(2, 6, rp, bad_col, v, "csr")  # host row_ptr
+
+
+def test_profile_phases():
+    """spmv_profile: the per-phase split (reference g_profile Mul/Sum)."""
+    import torch
+    m = 200000
+    rp, col, val = sp.generate_csr(sp.gen_spec("powerlaw", m, max_len=2000, seed=4))
+    x = torch.from_numpy(sp.generate_vector(m, seed=5)).cuda()
+    y = torch.empty(m, dtype=torch.float64, device="cuda")
+    want = {"csr": ["csr"], "ell": ["ell"], "jds": ["ell"], "hyb": ["ell", "overflow"],
+            "ss": ["tile", "fixup"], "css": ["sweep"], "coo": ["zero_y", "segment"]}
+    for fmt, names in want.items():
+        plan = sp.Plan.from_csr(m, m, rp, col, val, fmt, ell_width=8 if fmt == "hyb" else 0)
+        prof = plan.profile(x, y, 5)
+        assert list(prof) == names, (fmt, prof)
+        assert all(v >= 0 for v in prof.values()) and sum(prof.values()) > 0
+        yo = oracle_y(rp, col, val, x.cpu().numpy())
+        check_close(y.cpu().numpy(), yo, what=f"profile {fmt}")
