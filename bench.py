@@ -171,7 +171,7 @@ def main():
                     "hyb": ("ell_width",), "dia": ("n_diags",), "css": ("css_passes", "css_slabs")}
         for k in relevant.get(info["format"], ()):
             r[k] = info[k]
-        results[fmt] = r
+        results[fmt if fmt not in results else f"{fmt}_{fi}"] = r
         if fi == 0:
             r["phases_ms"] = plan.profile(x, y, 10)
             headline = (plan, info, r)
@@ -207,15 +207,26 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:
         import oracle
         nthreads = min(host_cores, int(os.environ.get("OMP_NUM_THREADS", host_cores)))
-        t_cpu, loop, y_cpu = oracle.csr_time(rp, col, val, x.cpu().numpy(), nthreads=nthreads,
-                                             min_seconds=args.cpu_seconds, ntry=3)
+        x_host = x.cpu().numpy()
+        if oracle.ref_available("crs"):
+            # the reference's own opt_crs (src/opt_crs.cpp, compiled from its
+            # sources into oracle/_ref) under its driver's timing method
+            row_idx = np.repeat(np.arange(rows, dtype=np.int32), np.diff(rp))
+            t_cpu, loop, y_cpu = oracle.ref_time("crs", rows, n_glob, row_idx, col, val, x_host,
+                                                 min_seconds=args.cpu_seconds, ntry=3)
+            del row_idx
+            kind_cpu, what = "reference", "reference opt_crs (src/opt_crs.cpp:44-70) built from its sources"
+        else:
+            t_cpu, loop, y_cpu = oracle.csr_time(rp, col, val, x_host, nthreads=nthreads,
+                                                 min_seconds=args.cpu_seconds, ntry=3)
+            kind_cpu, what = "port", "oracle opt_crs restatement (OpenMP static)"
         ygpu = y_head.cpu().numpy()
         max_rel = float(np.max(np.abs(ygpu - y_cpu) / np.maximum(np.abs(y_cpu), 1e-300)))
         cpu = {"value": 2.0 * nnz_local / t_cpu / 1e9, "unit": "GFLOP/s", "cores": nthreads,
-               "kind": "port", "nproc": os.cpu_count(),
+               "kind": kind_cpu, "nproc": os.cpu_count(),
                "omp_proc_bind": os.environ.get("OMP_PROC_BIND"),
                "omp_places": os.environ.get("OMP_PLACES"),
-               "sample": f"full {rows}-row matrix, oracle opt_crs restatement (OpenMP static), "
+               "sample": f"full {rows}-row matrix, {what}, "
                          f"{loop} calls x 3 trials after a {args.cpu_seconds:.0f} s doubling warm-up, "
                          f"min mean per call",
                "ms_per_call": t_cpu * 1e3}

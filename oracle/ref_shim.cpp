@@ -83,4 +83,45 @@ int ref_run(int m, int n, int nnz, const int *row_idx, const int *col_idx,
     return VerifyResult(A, xv, yv) ? 1 : 0;
 }
 
+// The reference driver's timing of a plugin (src/main.cpp:36, 58-102):
+// OptimizeProblem once; warm-up doubling `loop` until the cumulative time
+// reaches min_seconds (1.0 in the reference); then ntry batches of `loop`
+// calls (10 in the reference), min mean seconds per call.  y gets the last
+// result.
+double ref_time(int m, int n, int nnz, const int *row_idx, const int *col_idx, const double *val,
+                const double *x, double *y, double min_seconds, int ntry, int *loop_out) {
+    SpMat A;
+    A.nRow = m;
+    A.nCol = n;
+    A.nNnz = nnz;
+    A.row_idx = const_cast<int *>(row_idx);
+    A.col_idx = const_cast<int *>(col_idx);
+    A.val = const_cast<double *>(val);
+    Vec xv;
+    xv.size = n;
+    xv.val = const_cast<double *>(x);
+    Vec yv;
+    yv.size = m;
+    yv.val = y;
+    SpMatOpt A_opt;
+    VecOpt x_opt;
+    g_profile = std::vector<double>(10);
+    OptimizeProblem(A, xv, A_opt, x_opt);
+    int loop = 1;
+    const double t0 = GetTimeBySec();
+    do {
+        for (int i = 0; i < loop; i++) SpMV(A_opt, x_opt, yv);
+        loop *= 2;
+    } while (GetTimeBySec() - t0 < min_seconds);
+    double best = 0;
+    for (int t = 0; t < ntry; t++) {
+        const double a = GetTimeBySec();
+        for (int i = 0; i < loop; i++) SpMV(A_opt, x_opt, yv);
+        const double e = (GetTimeBySec() - a) / loop;
+        best = t == 0 ? e : (e < best ? e : best);
+    }
+    *loop_out = loop;
+    return best;
+}
+
 }  // extern "C"

@@ -373,6 +373,25 @@ int spmv_profile(spmv_plan_t p, const double *x_dev, double *y_dev, int32_t iter
     return st;
 }
 
+// internal (not in the public header): the CSS per-wave timestamps of the
+// last launch when the plan was built with SPMV_CSS_DEBUG & 32
+int64_t spmv_css_timestamps(spmv_plan_t p, uint64_t *out, int64_t cap) {
+    if (!p || p->format != SPMV_FORMAT_CSS || !p->css.tstamp) return -1;
+    const int64_t n = (int64_t)p->css.P * p->css.nwg * (kCssWorkers + 2);
+    if (out && cap >= n && hipMemcpy(out, p->css.tstamp, 8 * (size_t)n, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    return n;
+}
+
+// internal: the CSS block/list layout (bstart [P*nwg+1], woff [P*nwg*15+1])
+int spmv_css_layout(spmv_plan_t p, int64_t *bstart, int64_t *woff) {
+    if (!p || p->format != SPMV_FORMAT_CSS) return -1;
+    const int64_t nb = (int64_t)p->css.P * p->css.nwg;
+    if (hipMemcpy(bstart, p->css.bstart, 8 * (size_t)(nb + 1), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    if (hipMemcpy(woff, p->css.woff, 8 * (size_t)(nb * kCssWorkers + 1), hipMemcpyDeviceToHost) != hipSuccess)
+        return -1;
+    return 0;
+}
+
 int spmv_plan_info(spmv_plan_t p, spmv_plan_info_t *info) {
     SPMV_CHECK_ARG(p != nullptr && info != nullptr, "NULL argument");
     std::memset(info, 0, sizeof(*info));

@@ -9,6 +9,7 @@
 #include <cstring>
 #include <limits>
 #include <numeric>
+#include <queue>
 #include <vector>
 
 #include "internal.hpp"
@@ -411,30 +412,97 @@ int build_css(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
     const int64_t per_pass = (int64_t)c.nwg * kCssMaxRows;
     const int P_min = (int)std::max<int64_t>(1, (A.m + per_pass - 1) / per_pass);
     auto row_len = [&](int64_t r) { return A.row_ptr[r + 1] - A.row_ptr[r]; };
-    std::vector<int64_t> bstart;
+    // Row blocks.  Short rows keep matrix order in contiguous runs cut by
+    // nnz; rows much longer than the mean ("long") are then dealt
+    // longest-first to the block with the least nnz that still has LDS slots
+    // (LPT), so one block does not inherit a cluster of heavy rows (with
+    // ~19.5 K rows per block at config 3 the slot cap alone left blocks at
+    // 0.8-1.3x the mean nnz).  rmap lists each block's rows, slot order.
+    const double mean_len = A.m ? (double)A.nnz / (double)A.m : 0.0;
+    const int64_t tau = std::max<int64_t>(64, (int64_t)(8.0 * mean_len));
+    std::vector<int64_t> longs, shorts;
+    for (int64_t r = 0; r < A.m; ++r) (row_len(r) > tau ? longs : shorts).push_back(r);
+    std::stable_sort(longs.begin(), longs.end(), [&](int64_t a, int64_t b) { return row_len(a) > row_len(b); });
+    int64_t short_nnz = 0;
+    for (int64_t r : shorts) short_nnz += row_len(r);
+    std::vector<int64_t> roff;          // [nb + 1] into rmap
+    std::vector<int32_t> rmap;          // block rows in slot order
     int64_t piece_cap = 0;
-    for (c.P = P_min;; ++c.P) {
+    int piece_div = 2;
+    if (const char *d = std::getenv("SPMV_CSS_PIECE_DIV")) piece_div = std::max(1, std::atoi(d));
+    bool fitted = false;
+    for (c.P = P_min; c.P <= P_min + 1024 && !fitted; ++c.P) {
         const int64_t nb = (int64_t)c.P * c.nwg;
-        piece_cap = std::max<int64_t>(64, A.nnz / (nb * W) / 2);
+        piece_cap = std::max<int64_t>(64, A.nnz / (nb * W) / piece_div);
         auto slots_of = [&](int64_t r) { return std::max<int64_t>(1, (row_len(r) + piece_cap - 1) / piece_cap); };
-        bstart.assign((size_t)nb + 1, 0);
-        bool ok = true;
-        int64_t r = 0;
+        int64_t long_slots = 0;
+        for (int64_t r : longs) long_slots += slots_of(r);
+        const int64_t ns = (int64_t)shorts.size();
+        // every block keeps room for its share of the long-row slots
+        const int64_t reserve = longs.empty() ? 0 : (long_slots + nb - 1) / nb + 8;
+        const int64_t cap_short = kCssMaxRows - reserve;
+        if (cap_short <= 0 || ns > cap_short * nb) continue;
+        // contiguous short runs, cumulative nnz targets, slot-capped
+        std::vector<int64_t> s_off((size_t)nb + 1, 0), b_nnz((size_t)nb, 0), b_slots((size_t)nb, 0);
+        size_t i = 0;
+        int64_t cum = 0;  // nnz of shorts[0, i)
         for (int64_t b = 0; b < nb; ++b) {
-            const int64_t target = b == nb - 1 ? A.nnz : (int64_t)((__int128)A.nnz * (b + 1) / nb);
-            int64_t used = 0;
-            while (r < A.m && (b == nb - 1 || A.row_ptr[r] < target || (A.nnz == 0 && r < (b + 1) * ((A.m + nb - 1) / nb)))) {
-                const int64_t k = slots_of(r);
-                if (used + k > kCssMaxRows) break;
-                used += k;
-                ++r;
+            const bool last = b == nb - 1;
+            const int64_t tgt_nnz = (int64_t)((__int128)short_nnz * (b + 1) / nb);
+            const int64_t tgt_cnt = (int64_t)((__int128)ns * (b + 1) / nb);
+            // rows this block must take so the later blocks can hold the rest
+            const int64_t must = std::max<int64_t>(0, (ns - (int64_t)i) - (nb - b - 1) * cap_short);
+            while ((int64_t)i < ns && b_slots[(size_t)b] < cap_short) {
+                const bool forced = b_slots[(size_t)b] < must;
+                if (!last && !forced && (short_nnz > 0 ? cum >= tgt_nnz : (int64_t)i >= tgt_cnt)) break;
+                const int64_t len = row_len(shorts[i]);
+                b_slots[(size_t)b] += 1;
+                b_nnz[(size_t)b] += len;
+                cum += len;
+                ++i;
             }
-            bstart[(size_t)b + 1] = r;
+            s_off[(size_t)b + 1] = (int64_t)i;
         }
-        if (r < A.m) ok = false;  // rows left over: more passes
-        if (ok || c.P > P_min + 1024) break;
+        if (i < shorts.size()) continue;  // short rows left over: more passes
+        // LPT of the long rows over blocks with free slots
+        std::vector<std::vector<int64_t>> blong((size_t)nb);
+        typedef std::pair<int64_t, int64_t> NB;  // (nnz, block)
+        std::priority_queue<NB, std::vector<NB>, std::greater<NB>> heap;
+        for (int64_t b = 0; b < nb; ++b) heap.push({b_nnz[(size_t)b], b});
+        bool ok = true;
+        std::vector<NB> full;
+        for (int64_t r : longs) {
+            const int64_t k = slots_of(r);
+            while (!heap.empty() && b_slots[(size_t)heap.top().second] + k > kCssMaxRows) {
+                full.push_back(heap.top());
+                heap.pop();
+            }
+            if (heap.empty()) {
+                ok = false;
+                break;
+            }
+            NB t = heap.top();
+            heap.pop();
+            blong[(size_t)t.second].push_back(r);
+            b_slots[(size_t)t.second] += k;
+            t.first += row_len(r);
+            heap.push(t);
+            for (const NB &f : full) heap.push(f);  // a shorter row may still fit there
+            full.clear();
+        }
+        if (!ok) continue;
+        roff.assign((size_t)nb + 1, 0);
+        rmap.clear();
+        rmap.reserve((size_t)A.m);
+        for (int64_t b = 0; b < nb; ++b) {
+            for (int64_t q = s_off[(size_t)b]; q < s_off[(size_t)b + 1]; ++q) rmap.push_back((int32_t)shorts[(size_t)q]);
+            for (int64_t r : blong[(size_t)b]) rmap.push_back((int32_t)r);
+            roff[(size_t)b + 1] = (int64_t)rmap.size();
+        }
+        fitted = true;
+        break;
     }
-    if (bstart.back() != A.m) {
+    if (!fitted) {
         set_error("CSS: could not fit the rows into LDS row blocks");
         return SPMV_ERROR_NOT_SUPPORTED;
     }
@@ -468,12 +536,13 @@ int build_css(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
         std::vector<int> order;
 #pragma omp for schedule(dynamic, 4)
         for (int64_t pb = 0; pb < nblocks; ++pb) {
-            const int64_t r0 = bstart[(size_t)pb];
-            const int rows = (int)(bstart[(size_t)pb + 1] - r0);
+            const int64_t r0 = roff[(size_t)pb];
+            const int rows = (int)(roff[(size_t)pb + 1] - r0);
             pieces.clear();
             int extra = rows;
             for (int l = 0; l < rows; ++l) {
-                const int64_t b0 = A.row_ptr[r0 + l], len = row_len(r0 + l);
+                const int64_t row = rmap[(size_t)(r0 + l)];
+                const int64_t b0 = A.row_ptr[row], len = row_len(row);
                 const int64_t k = std::max<int64_t>(1, (len + piece_cap - 1) / piece_cap);
                 if (k > 1) {
                     merges[(size_t)pb].insert(merges[(size_t)pb].end(), {l, extra, (int32_t)(k - 1)});
@@ -531,16 +600,20 @@ int build_css(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
     }
     c.split_rows = moff[nblocks];
     SPMV_RETURN_IF(upload(p, &c.woff, woff.data(), nlists + 1));
-    SPMV_RETURN_IF(upload(p, &c.bstart, bstart.data(), nblocks + 1));
+    SPMV_RETURN_IF(upload(p, &c.bstart, roff.data(), nblocks + 1));
+    c.rmap = nullptr;  // identity (rows in matrix order) unless long rows were dealt out
+    if (!longs.empty()) SPMV_RETURN_IF(upload(p, &c.rmap, rmap.data(), (int64_t)rmap.size()));
     SPMV_RETURN_IF(upload(p, &c.moff, moff.data(), nblocks + 1));
     SPMV_RETURN_IF(upload(p, &c.merge, merge.data(), 3 * moff[nblocks]));
-    SPMV_RETURN_IF(upload(p, &c.col, col.data(), total));
-    SPMV_RETURN_IF(upload(p, &c.row, slot.data(), total));
-    SPMV_RETURN_IF(upload(p, &c.val, val.data(), total));
+    // +1 zeroed entry: masked lanes of the sweep load index 0 unconditionally
+    SPMV_RETURN_IF(upload(p, &c.col, col.data(), total, 1));
+    SPMV_RETURN_IF(upload(p, &c.row, slot.data(), total, 1));
+    SPMV_RETURN_IF(upload(p, &c.val, val.data(), total, 1));
     std::vector<uint64_t> zeros(8 * 16, 0);
     SPMV_RETURN_IF(upload(p, &c.prog, zeros.data(), (int64_t)zeros.size()));
     c.launches = 0;
     if (const char *d = std::getenv("SPMV_CSS_DEBUG")) c.dbg = std::atoi(d);
+    if (c.dbg & 32) SPMV_RETURN_IF(dev_alloc(p, &c.tstamp, (int64_t)c.P * c.nwg * (kCssWorkers + 2)));
     p->stored_slots = total;
     p->algo_bytes = 12 * A.nnz + 8 * A.n + 8 * A.m;
     p->n_kernels = 1;

@@ -145,7 +145,8 @@ constexpr int kCssWorkers = 15;  // worker waves per workgroup (+1 pacer wave)
 struct CssDev {
     int nwg = 0, R = 0, P = 0, S = 0, slab_shift = 17, lag = 2, pace_all = 0;
     int64_t *woff = nullptr;
-    int64_t *bstart = nullptr;  // [P*nwg + 1] first row of each (pass, workgroup) block
+    int64_t *bstart = nullptr;  // [P*nwg + 1] offsets of each (pass, workgroup) block's rows in rmap
+    int32_t *rmap = nullptr;    // block rows in slot order; null = identity (contiguous blocks)
     int64_t *moff = nullptr;    // [P*nwg + 1] merge-triple offsets per block
     int32_t *merge = nullptr;   // (slot, first extra slot, n extra) triples
     int64_t split_rows = 0;
@@ -155,6 +156,7 @@ struct CssDev {
     uint64_t *prog = nullptr;
     uint64_t launches = 0;
     int dbg = 0;  // ablation switches (SPMV_CSS_DEBUG, internal)
+    uint64_t *tstamp = nullptr;  // dbg & 32: [P*nwg][kCssWorkers + 2] s_memrealtime stamps
 };
 
 }  // namespace spmv

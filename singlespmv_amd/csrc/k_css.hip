@@ -46,6 +46,9 @@ struct CssChunk {
     double v[4];
 };
 
+// One 256-entry chunk, branch-free (so the compiler's in-order vmcnt
+// tracking stays exact across the pipeline): lanes past e1 load entry 0 and
+// are redirected to the dummy slot kCssMaxRows with value 0 by css_mask.
 template <bool NT>
 __device__ __forceinline__ void css_load(CssChunk &k, int64_t j0, int64_t e1, int lane,
                                          const int32_t *__restrict__ col,
@@ -54,28 +57,47 @@ __device__ __forceinline__ void css_load(CssChunk &k, int64_t j0, int64_t e1, in
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
         const int64_t j = j0 + u * 64 + lane;
-        const bool ok = j < e1;
+        const int64_t jj = j < e1 ? j : 0;
         if (NT) {
-            k.c[u] = ok ? ld_stream(col + j) : 0;
-            k.r[u] = ok ? (int32_t)__builtin_nontemporal_load(row + j) : -1;
-            k.v[u] = ok ? ld_stream(val + j) : 0.0;
+            k.c[u] = ld_stream(col + jj);
+            k.r[u] = (int32_t)__builtin_nontemporal_load(row + jj);
+            k.v[u] = ld_stream(val + jj);
         } else {
-            k.c[u] = ok ? col[j] : 0;
-            k.r[u] = ok ? (int32_t)row[j] : -1;
-            k.v[u] = ok ? val[j] : 0.0;
+            k.c[u] = col[jj];
+            k.r[u] = (int32_t)row[jj];
+            k.v[u] = val[jj];
         }
     }
 }
 
-template <bool NT>
+__device__ __forceinline__ void css_mask(CssChunk &k, int64_t j0, int64_t e1, int lane) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const bool ok = j0 + u * 64 + lane < e1;
+        k.r[u] = ok ? k.r[u] : kCssMaxRows;
+        k.v[u] = ok ? k.v[u] : 0.0;
+    }
+}
+
+template <int DBG>
+__device__ __forceinline__ void css_gather(double (&g)[4], const CssChunk &k, const double *__restrict__ x) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        if (DBG & 1) g[u] = (double)k.c[u];                   // ablation: no gathers
+        else if (DBG & 16) g[u] = ld_x(x, k.c[u] & 0x1FFFF);  // ablation: all gathers in 1 MiB
+        else g[u] = ld_x(x, k.c[u]);
+    }
+}
+
+template <bool NT, int DBG>
 __global__ __launch_bounds__(kCssThreads) void css_sweep_kernel(
-    const int64_t *__restrict__ bstart, const int64_t *__restrict__ moff,
+    const int64_t *__restrict__ bstart, const int32_t *__restrict__ rmap, const int64_t *__restrict__ moff,
     const int32_t *__restrict__ merge, int32_t P, int32_t nwg, int32_t S, int32_t slab_shift, int32_t lag,
     const int64_t *__restrict__ woff, const int32_t *__restrict__ col,
     const uint16_t *__restrict__ row, const double *__restrict__ val,
     const double *__restrict__ x, double *__restrict__ y, uint64_t *__restrict__ prog,
-    uint64_t seq, int32_t pace_all, int32_t dbg) {
-    __shared__ double ylds[kCssMaxRows];
+    uint64_t seq, int32_t pace_all, uint64_t *__restrict__ tstamp) {
+    __shared__ double ylds[kCssMaxRows + 1];  // + dummy slot for masked lanes
     __shared__ int32_t arrive[kCssRing];
     __shared__ int32_t allowed;
     const int w = threadIdx.x >> 6;
@@ -93,6 +115,8 @@ __global__ __launch_bounds__(kCssThreads) void css_sweep_kernel(
         for (int i = threadIdx.x; i < kCssRing; i += kCssThreads) arrive[i] = 0;
         if (threadIdx.x == 0) allowed = pacing ? lag - 1 : S;
         __syncthreads();
+        uint64_t *ts = tstamp ? tstamp + ((int64_t)p * nwg + b) * (kCssWorkers + 2) : nullptr;
+        if (ts && threadIdx.x == 0) ts[0] = __builtin_amdgcn_s_memrealtime();
 
         if (pacer) {
             // ---------------- pacer wave: the only wave touching prog[] ----
@@ -162,41 +186,48 @@ __global__ __launch_bounds__(kCssThreads) void css_sweep_kernel(
                     }
                 }
             };
-            CssChunk A, B;
-            if (e0 < e1) css_load<NT>(A, e0, e1, lane, col, row, val);
-            for (int64_t j0 = e0; j0 < e1; j0 += 256) {
-                // slab of the chunk's first entry (wave-uniform: lane 0, u = 0)
-                const int s0 = __builtin_amdgcn_readfirstlane(A.c[0]) >> slab_shift;
+            // Software pipeline, issue order per iteration k (in-order vmcnt):
+            //   gathers(k+1) | loads(k+3) | wait gathers(k) | LDS atomics(k)
+            // so two chunks of gathers and two of stream loads stay in flight
+            // while the atomics of chunk k run.  Lanes past e1 are masked in
+            // the loads (slot -1) and gather x[0].
+            CssChunk L0, L1, L2, L3;
+            double g0[4], g1[4];
+            css_load<NT>(L0, e0, e1, lane, col, row, val);
+            css_load<NT>(L1, e0 + 256, e1, lane, col, row, val);
+            if (e0 < e1) {
+                const int s0 = __builtin_amdgcn_readfirstlane(L0.c[0]) >> slab_shift;
                 if (s0 > cur) enter(s0);
-                double g[4];
-                if (dbg & 1) {
+            }
+            css_gather<DBG>(g0, L0, x);
+            css_load<NT>(L2, e0 + 512, e1, lane, col, row, val);
+            for (int64_t j0 = e0; j0 < e1; j0 += 256) {
+                __builtin_amdgcn_sched_barrier(0);
+                if (j0 + 256 < e1) {
+                    const int s1 = __builtin_amdgcn_readfirstlane(L1.c[0]) >> slab_shift;
+                    if (s1 > cur) enter(s1);
+                }
+                css_gather<DBG>(g1, L1, x);
+                __builtin_amdgcn_sched_barrier(0);
+                css_load<NT>(L3, j0 + 768, e1, lane, col, row, val);
+                __builtin_amdgcn_sched_barrier(0);
+                css_mask(L0, j0, e1, lane);
+                if (DBG & 2) {
 #pragma unroll
-                    for (int u = 0; u < 4; ++u) g[u] = (double)A.c[u];
-                } else if (dbg & 16) {  // ablation: every gather inside one 1 MiB window (all L2 hits)
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) g[u] = ld_x(x, A.c[u] & 0x1FFFF);
+                    for (int u = 0; u < 4; ++u) dsink += __dmul_rn(L0.v[u], g0[u]) * (double)L0.r[u];
                 } else {
 #pragma unroll
-                    for (int u = 0; u < 4; ++u) g[u] = ld_x(x, A.c[u]);
+                    for (int u = 0; u < 4; ++u) atomicAdd(&ylds[L0.r[u]], __dmul_rn(L0.v[u], g0[u]));
                 }
-                __builtin_amdgcn_sched_barrier(0);
-                // prefetch the next chunk behind the gathers (in-order vmcnt:
-                // waiting for the gathers leaves these 12 loads in flight)
-                const int64_t j1 = j0 + 256;
-                if (j1 < e1) css_load<NT>(B, j1, e1, lane, col, row, val);
-                __builtin_amdgcn_sched_barrier(0);
-                if (dbg & 2) {
+                L0 = L1;
+                L1 = L2;
+                L2 = L3;
 #pragma unroll
-                    for (int u = 0; u < 4; ++u) dsink += __dmul_rn(A.v[u], g[u]) * (double)A.r[u];
-                } else {
-#pragma unroll
-                    for (int u = 0; u < 4; ++u)
-                        if (A.r[u] >= 0) atomicAdd(&ylds[A.r[u]], __dmul_rn(A.v[u], g[u]));
-                }
-                A = B;
+                for (int u = 0; u < 4; ++u) g0[u] = g1[u];
             }
             enter(S);  // report every remaining slab
-            if ((dbg & 2) && dsink == 1.2345) y[0] = dsink;  // keep ablated work alive
+            if (ts && lane == 0) ts[1 + w] = __builtin_amdgcn_s_memrealtime();
+            if ((DBG & 2) && dsink == 1.2345) y[0] = dsink;  // keep ablated work alive
         }
         __syncthreads();
         // rows split into pieces: add the extra pieces in piece order
@@ -210,24 +241,42 @@ __global__ __launch_bounds__(kCssThreads) void css_sweep_kernel(
             }
         }
         __syncthreads();
-        for (int i = threadIdx.x; i < rows; i += kCssThreads) y[row0 + i] = ylds[i];
+        if (rmap)
+            for (int i = threadIdx.x; i < rows; i += kCssThreads) y[rmap[row0 + i]] = ylds[i];
+        else
+            for (int i = threadIdx.x; i < rows; i += kCssThreads) y[row0 + i] = ylds[i];
         __syncthreads();
+        if (ts && threadIdx.x == 0) ts[kCssWorkers + 1] = __builtin_amdgcn_s_memrealtime();
     }
+}
+
+template <bool NT, int DBG>
+static void launch_css_t(const spmv_plan_s *p, const double *x, double *y, uint64_t seq) {
+    const CssDev &c = p->css;
+    hipLaunchKernelGGL((css_sweep_kernel<NT, DBG>), dim3((unsigned)c.nwg), dim3(kCssThreads), 0, p->stream,
+                       c.bstart, c.rmap, c.moff, c.merge, c.P, c.nwg, c.S, c.slab_shift, c.lag, c.woff, c.col, c.row, c.val,
+                       x, y, c.prog, seq, c.pace_all, c.tstamp);
 }
 
 int launch_css(const spmv_plan_s *p, const double *x, double *y) {
     const CssDev &c = p->css;
     if (p->m == 0) return SPMV_SUCCESS;
+    if (p->nnz == 0) {  // no entries: y = 0 (and x may be empty)
+        SPMV_HIP_TRY(hipMemsetAsync(y, 0, sizeof(double) * (size_t)p->m, p->stream));
+        return SPMV_SUCCESS;
+    }
     spmv_plan_s *mp = const_cast<spmv_plan_s *>(p);
     const uint64_t seq = mp->css.launches++;
-    if (c.dbg & 8)  // ablation: default cache policy on the matrix stream
-        hipLaunchKernelGGL(css_sweep_kernel<false>, dim3((unsigned)c.nwg), dim3(kCssThreads), 0, p->stream,
-                           c.bstart, c.moff, c.merge, c.P, c.nwg, c.S, c.slab_shift, c.lag, c.woff, c.col, c.row, c.val, x, y,
-                           c.prog, seq, c.pace_all, c.dbg);
-    else
-        hipLaunchKernelGGL(css_sweep_kernel<true>, dim3((unsigned)c.nwg), dim3(kCssThreads), 0, p->stream,
-                           c.bstart, c.moff, c.merge, c.P, c.nwg, c.S, c.slab_shift, c.lag, c.woff, c.col, c.row, c.val, x, y,
-                           c.prog, seq, c.pace_all, c.dbg);
+    // ablations (SPMV_CSS_DEBUG, internal): 1 no gathers, 2 no LDS atomics,
+    // 8 default cache policy on the matrix stream, 16 all gathers in 1 MiB
+    switch (c.dbg & 19) {
+        case 1: launch_css_t<true, 1>(p, x, y, seq); break;
+        case 2: launch_css_t<true, 2>(p, x, y, seq); break;
+        case 16: launch_css_t<true, 16>(p, x, y, seq); break;
+        default:
+            if (c.dbg & 8) launch_css_t<false, 0>(p, x, y, seq);
+            else launch_css_t<true, 0>(p, x, y, seq);
+    }
     SPMV_HIP_TRY(hipGetLastError());
     return SPMV_SUCCESS;
 }

@@ -10,6 +10,14 @@
 //   e2: T = 80 MB, indices confined to a W-byte window that slides across the
 //       table with the stream position (a synchronised column sweep)
 //   e3: HBM streaming read ceiling (dwordx4), for calibration
+//   e4: small tables (4 KB .. 1 MB): is an L1 (TCP) hit cheaper than an L2 hit?
+//   e5: 1 MB table, fewer workgroups: per-CU or chip-wide (L2) bound?
+//   e6: 64 MB table, groups of k consecutive lanes read the same 128 B line:
+//       does the vector memory path merge same-line lanes of one instruction?
+//   e8: 1 MB table, gathers + the CSS entry stream (4 B col + 2 B slot + 8 B
+//       value per gather) vs the 4 B index stream alone
+//   e7: 1 MB table, one 1024-thread workgroup per CU (LDS-pinned), 256 .. 16
+//       CUs: does the per-CU rate rise when fewer CUs share the L2?
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -41,6 +49,71 @@ __global__ void make_idx(int *idx, long long n, long long tab_elems, long long w
         long long base = (win_elems >= tab_elems) ? 0 : (long long)((double)i / (double)n * (double)(tab_elems - win_elems));
         idx[i] = (int)(base + (long long)(mix((unsigned long long)i) % (unsigned long long)win_elems));
     }
+}
+
+// gather<8> in 1024-thread workgroups pinned one per CU by 96 KB of LDS
+__global__ __launch_bounds__(1024) void gather_cu(const int *__restrict__ idx, const double *__restrict__ tab,
+                                                  double *__restrict__ out, long long n) {
+    extern __shared__ double pin[];
+    const long long G = (long long)gridDim.x * blockDim.x;
+    long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    double acc = 0;
+    for (long long i = t; i < n; i += G * 8) {
+        int c[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            long long j = i + u * G;
+            c[u] = j < n ? __builtin_nontemporal_load(idx + j) : 0;
+        }
+        double g[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) g[u] = tab[c[u]];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc += g[u];
+    }
+    if (threadIdx.x == 0) pin[0] = acc;
+    if (acc == 1.2345) out[t] = acc + pin[0];
+}
+
+// gather<4> plus an extra 2 B + 8 B stream per gather (the CSS entry shape)
+__global__ __launch_bounds__(256) void gather_css_shape(const int *__restrict__ idx, const unsigned short *__restrict__ slot,
+                                                        const double *__restrict__ vals, const double *__restrict__ tab,
+                                                        double *__restrict__ out, long long n, int with_stream) {
+    const long long G = (long long)gridDim.x * blockDim.x;
+    long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    double acc = 0;
+    for (long long i = t; i < n; i += G * 4) {
+        int c[4];
+        double v[4];
+        int r[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            long long j = i + u * G;
+            j = j < n ? j : 0;
+            c[u] = __builtin_nontemporal_load(idx + j);
+            if (with_stream) {
+                r[u] = __builtin_nontemporal_load(slot + j);
+                v[u] = __builtin_nontemporal_load(vals + j);
+            } else {
+                r[u] = 1;
+                v[u] = 1.0;
+            }
+        }
+        double g[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) g[u] = tab[c[u]];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc += g[u] * v[u] + r[u];
+    }
+    if (acc == 1.2345) out[t] = acc;
+}
+
+// groups of k consecutive indices share one random 128 B line
+__global__ void make_idx_lines(int *idx, long long n, long long tab_elems, int k) {
+    const long long lines = tab_elems / 16;
+    long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; i < n; i += (long long)gridDim.x * blockDim.x)
+        idx[i] = (int)((long long)(mix((unsigned long long)(i / k)) % (unsigned long long)lines) * 16 + (i % k));
 }
 
 template <int U>
@@ -155,6 +228,114 @@ int main(int argc, char **argv) {
         CK(hipEventElapsedTime(&ms, a, b));
         if (ms < best) best = ms;
     }
-    std::printf("], \"e3_stream_GBs\": %.1f}\n", TMAX / (best * 1e-3) / 1e9);
+    std::printf("], \"e3_stream_GBs\": %.1f", TMAX / (best * 1e-3) / 1e9);
+    std::printf(", \"e4\": [");
+    first = true;
+    const long long kbs[] = {4, 16, 32, 64, 128, 256, 1024};
+    for (long long kb : kbs) {
+        const long long te = (kb << 10) / 8;
+        hipLaunchKernelGGL(make_idx, dim3(4096), dim3(256), 0, 0, idx, N, te, te);
+        CK(hipDeviceSynchronize());
+        const float ms = time_gather(idx, tab, out, N, blocks);
+        std::printf("%s{\"table_KB\": %lld, \"ms\": %.4f, \"Ggather_s\": %.2f}", first ? "" : ", ", kb, ms,
+                    N / (ms * 1e-3) / 1e9);
+        first = false;
+        std::fflush(stdout);
+    }
+    std::printf("], \"e5\": [");
+    first = true;
+    {
+        const long long te = (1LL << 20) / 8;
+        hipLaunchKernelGGL(make_idx, dim3(4096), dim3(256), 0, 0, idx, N, te, te);
+        CK(hipDeviceSynchronize());
+        const int bl[] = {256 * 8, 256 * 4, 256, 128, 64, 32};
+        for (int nb : bl) {
+            const float ms = time_gather(idx, tab, out, N / 4, nb);
+            std::printf("%s{\"blocks\": %d, \"ms\": %.4f, \"Ggather_s\": %.2f}", first ? "" : ", ", nb, ms,
+                        N / 4 / (ms * 1e-3) / 1e9);
+            first = false;
+            std::fflush(stdout);
+        }
+    }
+    std::printf("], \"e6\": [");
+    first = true;
+    {
+        const long long te = (64LL << 20) / 8;
+        const int ks[] = {1, 2, 4, 8, 16};
+        for (int k : ks) {
+            hipLaunchKernelGGL(make_idx_lines, dim3(4096), dim3(256), 0, 0, idx, N, te, k);
+            CK(hipDeviceSynchronize());
+            const float ms = time_gather(idx, tab, out, N, blocks);
+            std::printf("%s{\"lanes_per_line\": %d, \"ms\": %.4f, \"Ggather_s\": %.2f}", first ? "" : ", ", k,
+                        ms, N / (ms * 1e-3) / 1e9);
+            first = false;
+            std::fflush(stdout);
+        }
+    }
+    std::printf("], \"e8\": [");
+    {
+        const long long te = (1LL << 20) / 8;
+        const long long n = N;
+        hipLaunchKernelGGL(make_idx, dim3(4096), dim3(256), 0, 0, idx, n, te, te);
+        CK(hipDeviceSynchronize());
+        unsigned short *slot;
+        double *vals;
+        CK(hipMalloc(&slot, 2 * n));
+        CK(hipMalloc(&vals, 8 * n));
+        CK(hipMemset(slot, 0, 2 * n));
+        CK(hipMemset(vals, 0, 8 * n));
+        for (int ws = 0; ws < 2; ++ws) {
+            hipEvent_t a2, b2;
+            CK(hipEventCreate(&a2));
+            CK(hipEventCreate(&b2));
+            float bm = 1e30f;
+            for (int r = 0; r < 4; ++r) {
+                CK(hipEventRecord(a2));
+                hipLaunchKernelGGL(gather_css_shape, dim3(blocks), dim3(256), 0, 0, idx, slot, vals, tab, out, n, ws);
+                CK(hipEventRecord(b2));
+                CK(hipEventSynchronize(b2));
+                float ms;
+                CK(hipEventElapsedTime(&ms, a2, b2));
+                if (r && ms < bm) bm = ms;
+            }
+            std::printf("%s{\"entry_stream\": %d, \"ms\": %.4f, \"Ggather_s\": %.2f}", ws ? ", " : "", ws, bm,
+                        n / (bm * 1e-3) / 1e9);
+            std::fflush(stdout);
+        }
+        CK(hipFree(slot));
+        CK(hipFree(vals));
+    }
+    std::printf("], \"e7\": [");
+    first = true;
+    {
+        const long long te = (1LL << 20) / 8;
+        hipLaunchKernelGGL(make_idx, dim3(4096), dim3(256), 0, 0, idx, N, te, te);
+        CK(hipDeviceSynchronize());
+        CK(hipFuncSetAttribute((const void *)gather_cu, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024));
+        const int cus[] = {256, 128, 64, 32, 16};
+        for (int nc : cus) {
+            const long long n = N / 16;
+            hipEvent_t a2, b2;
+            CK(hipEventCreate(&a2));
+            CK(hipEventCreate(&b2));
+            hipLaunchKernelGGL(gather_cu, dim3(nc), dim3(1024), 96 * 1024, 0, idx, tab, out, n);
+            CK(hipDeviceSynchronize());
+            float bm = 1e30f;
+            for (int r = 0; r < 3; ++r) {
+                CK(hipEventRecord(a2));
+                hipLaunchKernelGGL(gather_cu, dim3(nc), dim3(1024), 96 * 1024, 0, idx, tab, out, n);
+                CK(hipEventRecord(b2));
+                CK(hipEventSynchronize(b2));
+                float ms;
+                CK(hipEventElapsedTime(&ms, a2, b2));
+                if (ms < bm) bm = ms;
+            }
+            std::printf("%s{\"cus\": %d, \"ms\": %.4f, \"Ggather_s\": %.2f, \"per_cu_G\": %.3f}",
+                        first ? "" : ", ", nc, bm, n / (bm * 1e-3) / 1e9, n / (bm * 1e-3) / 1e9 / nc);
+            first = false;
+            std::fflush(stdout);
+        }
+    }
+    std::printf("]}\n");
     return 0;
 }
