@@ -12,6 +12,8 @@ import sys
 import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+if os.environ.get("TUNE_PKG_ROOT"):  # A/B against another build of the package
+    sys.path.insert(0, os.environ["TUNE_PKG_ROOT"])
 
 
 def main():
