@@ -120,7 +120,10 @@ static int dispatch(const spmv_plan_s *p, const double *x, double *y) {
         case SPMV_FORMAT_DIA: return launch_dia(p, x, y);
         case SPMV_FORMAT_CSS: return launch_css(p, x, y);
         case SPMV_FORMAT_COO: return launch_coo(p, x, y);
-        case SPMV_FORMAT_JDS: return launch_ell(p, x, y);
+        case SPMV_FORMAT_JDS:
+            SPMV_RETURN_IF(launch_ell(p, x, y));
+            phase_mark(p);  // ell | overflow
+            return launch_hyb_overflow(p, x, y);
     }
     set_error("plan has an unknown format");
     return SPMV_ERROR_INVALID_VALUE;
@@ -332,7 +335,7 @@ int spmv_time(spmv_plan_t p, const double *x_dev, double *y_dev, int32_t iters, 
 static const char *const kPhases[][3] = {
     {"", "", ""},           {"csr", "", ""},   {"ell", "", ""},     {"tile", "fixup", ""},
     {"dia", "", ""},        {"ell", "overflow", ""}, {"sweep", "", ""}, {"zero_y", "segment", ""},
-    {"ell", "", ""}};
+    {"ell", "overflow", ""}};
 
 const char *spmv_phase_name(spmv_plan_t p, int32_t k) {
     if (!p || k < 0 || k > 2 || p->format < 0 || p->format > SPMV_FORMAT_JDS) return "";

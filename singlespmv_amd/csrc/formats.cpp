@@ -163,15 +163,59 @@ int build_ell(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &, int cap,
 // opt_jds (src/opt_jds.cpp:29-71): rows sorted by decreasing length (stable),
 // stored as 64-row jagged slices of the sliced-ELL layout; y is written back
 // through the permutation.  Each row is still summed in its own order.
+// The entries of rows longer than K beyond their first K go to a CSR over
+// those rows only (the HYB overflow), finished by hyb_overflow_kernel.
+static int build_overflow(spmv_plan_s *p, const HostCsr &A, int K) {
+    HybDev &h = p->hyb;
+    std::vector<int32_t> rows;
+    std::vector<int64_t> rp(1, 0);
+    for (int64_t r = 0; r < A.m; ++r) {
+        const int64_t len = A.row_ptr[r + 1] - A.row_ptr[r];
+        if (len > K) {
+            rows.push_back((int32_t)r);
+            rp.push_back(rp.back() + (len - K));
+        }
+    }
+    h.n_rows = (int64_t)rows.size();
+    h.nnz = rp.back();
+    std::vector<int32_t> col((size_t)h.nnz);
+    std::vector<double> val((size_t)h.nnz);
+#pragma omp parallel for schedule(dynamic, 16)
+    for (int64_t i = 0; i < h.n_rows; ++i) {
+        const int64_t src = A.row_ptr[rows[i]] + K;
+        std::memcpy(&col[rp[i]], A.col + src, sizeof(int32_t) * (size_t)(rp[i + 1] - rp[i]));
+        std::memcpy(&val[rp[i]], A.val + src, sizeof(double) * (size_t)(rp[i + 1] - rp[i]));
+    }
+    SPMV_RETURN_IF(upload(p, &h.rows, rows.data(), h.n_rows));
+    SPMV_RETURN_IF(upload(p, &h.row_ptr, rp.data(), h.n_rows + 1));
+    SPMV_RETURN_IF(upload(p, &h.col, col.data(), h.nnz, kPad));
+    SPMV_RETURN_IF(upload(p, &h.val, val.data(), h.nnz, kPad));
+    return SPMV_SUCCESS;
+}
+
+// ---------------------------------------------------------------- JDS
+// opt_jds (src/opt_jds.cpp:29-71, 75-104): rows sorted by length (stable,
+// longest first), jagged diagonals = sliced ELL over the sorted rows, y
+// written back through the permutation.  Jagged diagonals are capped at K
+// (default max(64, 4 x mean row length)); the entries of longer rows beyond K
+// are finished by the overflow kernel, so the longest-row slices do not run
+// as single waves.  Rows of length <= K are the sequential sum, bit for bit.
 int build_jds(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
     std::vector<int32_t> order((size_t)std::max<int64_t>(A.m, 1));
     std::iota(order.begin(), order.begin() + A.m, 0);
     std::stable_sort(order.begin(), order.begin() + A.m, [&](int32_t a, int32_t b) {
         return A.row_ptr[a + 1] - A.row_ptr[a] > A.row_ptr[b + 1] - A.row_ptr[b];
     });
-    SPMV_RETURN_IF(build_ell(p, A, o, INT32_MAX, order.data()));
+    const double mean = A.m ? (double)A.nnz / (double)A.m : 0.0;
+    const int K = o.ell_width > 0 ? (int)round_up(o.ell_width, 4)
+                                  : (int)std::max<int64_t>(64, round_up((int64_t)std::ceil(4.0 * mean), 4));
+    SPMV_RETURN_IF(build_ell(p, A, o, K, order.data()));
+    const int64_t ell_slots = p->stored_slots;
     SPMV_RETURN_IF(upload(p, &p->ell.perm, order.data(), A.m));
-    p->algo_bytes += 4 * A.m;
+    SPMV_RETURN_IF(build_overflow(p, A, K));
+    p->stored_slots = ell_slots + p->hyb.nnz;
+    p->algo_bytes = 12 * A.nnz + 8 * A.n + 8 * A.m + 4 * A.m + 12 * p->hyb.n_rows;
+    p->n_kernels = p->hyb.n_rows ? 2 : 1;
     p->kernel_name = "ell_slice_kernel<perm>";
     return SPMV_SUCCESS;
 }
@@ -231,29 +275,7 @@ int build_hyb(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
     SPMV_RETURN_IF(build_ell(p, A, o, K));
     const int64_t ell_slots = p->stored_slots;
     HybDev &h = p->hyb;
-    std::vector<int32_t> rows;
-    std::vector<int64_t> rp(1, 0);
-    for (int64_t r = 0; r < A.m; ++r) {
-        const int64_t len = A.row_ptr[r + 1] - A.row_ptr[r];
-        if (len > K) {
-            rows.push_back((int32_t)r);
-            rp.push_back(rp.back() + (len - K));
-        }
-    }
-    h.n_rows = (int64_t)rows.size();
-    h.nnz = rp.back();
-    std::vector<int32_t> col((size_t)h.nnz);
-    std::vector<double> val((size_t)h.nnz);
-#pragma omp parallel for schedule(dynamic, 16)
-    for (int64_t i = 0; i < h.n_rows; ++i) {
-        const int64_t src = A.row_ptr[rows[i]] + K;
-        std::memcpy(&col[rp[i]], A.col + src, sizeof(int32_t) * (size_t)(rp[i + 1] - rp[i]));
-        std::memcpy(&val[rp[i]], A.val + src, sizeof(double) * (size_t)(rp[i + 1] - rp[i]));
-    }
-    SPMV_RETURN_IF(upload(p, &h.rows, rows.data(), h.n_rows));
-    SPMV_RETURN_IF(upload(p, &h.row_ptr, rp.data(), h.n_rows + 1));
-    SPMV_RETURN_IF(upload(p, &h.col, col.data(), h.nnz, kPad));
-    SPMV_RETURN_IF(upload(p, &h.val, val.data(), h.nnz, kPad));
+    SPMV_RETURN_IF(build_overflow(p, A, K));
     p->ell.max_width = K;
     p->stored_slots = ell_slots + h.nnz;
     p->algo_bytes = 12 * A.nnz + 8 * A.n + 8 * A.m + 12 * h.n_rows;

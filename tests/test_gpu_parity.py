@@ -81,7 +81,8 @@ def test_golden(name, fmt):
     elif not signed:
         check_close(y, yref, what=f"{name}/{fmt}")
     info = plan.info()
-    sequential = info["format"] in ("ell", "dia", "jds") or (info["format"] == "csr" and info["csr_lanes"] == 1) \
+    sequential = info["format"] in ("ell", "dia") or (info["format"] == "csr" and info["csr_lanes"] == 1) \
+        or (info["format"] == "jds" and info["overflow_nnz"] == 0) \
         or (info["format"] == "css" and info["css_split_rows"] == 0)
     if sequential:
         assert np.array_equal(y, yref), f"{info['format']} is sequential: must be bit-exact"
@@ -205,7 +206,8 @@ def test_css_multi_pass():
 
 
 def test_jds_permutation_and_coo_atomics():
-    """JDS (rows sorted by length, y permuted back) is the sequential row sum;
+    """JDS (rows sorted by length, y permuted back) is the sequential row sum
+    for rows up to its jagged-diagonal cap, within 1e-12 beyond;
     COO (one f64 atomic per row run per wave) is within 1e-12 and
     reproducible for every row that sits inside one 64-entry step."""
     m = 50000
@@ -214,7 +216,13 @@ def test_jds_permutation_and_coo_atomics():
     x = sp.generate_vector(m, seed=79)
     yo = oracle_y(rp, col, val, x)
     pj = sp.Plan.from_csr(m, m, rp, col, val, "jds")
-    assert np.array_equal(run_plan(pj, x, m), yo)
+    yj = run_plan(pj, x, m)
+    check_close(yj, yo, what="jds")
+    short = np.diff(rp) <= 64
+    assert np.array_equal(yj[short], yo[short])
+    assert pj.info()["overflow_nnz"] > 0
+    pj1 = sp.Plan.from_csr(m, m, rp, col, val, "jds", ell_width=2000)  # no overflow: all sequential
+    assert np.array_equal(run_plan(pj1, x, m), yo)
     pc = sp.Plan.from_csr(m, m, rp, col, val, "coo")
     y = np.full(m, np.nan)
     pc.execute(x, y)
@@ -388,7 +396,7 @@ def test_profile_phases():
     rp, col, val = sp.generate_csr(sp.gen_spec("powerlaw", m, max_len=2000, seed=4))
     x = torch.from_numpy(sp.generate_vector(m, seed=5)).cuda()
     y = torch.empty(m, dtype=torch.float64, device="cuda")
-    want = {"csr": ["csr"], "ell": ["ell"], "jds": ["ell"], "hyb": ["ell", "overflow"],
+    want = {"csr": ["csr"], "ell": ["ell"], "jds": ["ell", "overflow"], "hyb": ["ell", "overflow"],
             "ss": ["tile", "fixup"], "css": ["sweep"], "coo": ["zero_y", "segment"]}
     for fmt, names in want.items():
         plan = sp.Plan.from_csr(m, m, rp, col, val, fmt, ell_width=8 if fmt == "hyb" else 0)
