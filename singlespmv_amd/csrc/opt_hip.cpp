@@ -23,6 +23,12 @@ static int opt_hip_format() {
     f = SPMV_FORMAT_DIA;
 #elif defined(OPT_HIP_HYB)
     f = SPMV_FORMAT_HYB;
+#elif defined(OPT_HIP_CSS)
+    f = SPMV_FORMAT_CSS;
+#elif defined(OPT_HIP_COO)
+    f = SPMV_FORMAT_COO;
+#elif defined(OPT_HIP_JDS)
+    f = SPMV_FORMAT_JDS;
 #endif
     const char *e = std::getenv("SPMV_HIP_FORMAT");
     if (e && *e) {
@@ -31,6 +37,9 @@ static int opt_hip_format() {
         else if (!strcasecmp(e, "ss")) f = SPMV_FORMAT_SS;
         else if (!strcasecmp(e, "dia")) f = SPMV_FORMAT_DIA;
         else if (!strcasecmp(e, "hyb")) f = SPMV_FORMAT_HYB;
+        else if (!strcasecmp(e, "css")) f = SPMV_FORMAT_CSS;
+        else if (!strcasecmp(e, "coo")) f = SPMV_FORMAT_COO;
+        else if (!strcasecmp(e, "jds")) f = SPMV_FORMAT_JDS;
         else f = SPMV_FORMAT_AUTO;
     }
     return f;

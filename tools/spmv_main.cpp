@@ -8,7 +8,7 @@
 // with GPU additions: AchievedGB/s against the plan's algorithmic bytes and
 // the MI355X 8 TB/s HBM roofline.
 //
-// Usage: spmv <matrix.mtx> [--format crs|ell|ss|dia|hyb|auto] [--resident]
+// Usage: spmv <matrix.mtx> [--format crs|ell|ss|dia|hyb|css|coo|jds|auto] [--resident]
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -20,7 +20,7 @@
 int main(int argc, char **argv) {
     srand(3);  // src/main.cpp:18
     if (argc < 2) {
-        std::printf("Usage: %s <matrix> [--format crs|ell|ss|dia|hyb|auto] [--resident]\n", argv[0]);
+        std::printf("Usage: %s <matrix> [--format crs|ell|ss|dia|hyb|css|coo|jds|auto] [--resident]\n", argv[0]);
         return 1;
     }
     const std::string matFile = argv[1];
