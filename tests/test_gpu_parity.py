@@ -320,15 +320,16 @@ def test_dropin_optimizeproblem_spmv():
     L.SpMVRelease(C.byref(Ao))
 
 
-def test_driver_binary_reports_block():
+@pytest.mark.parametrize("fmt,name", [("ss", "SS"), ("css", "CSS"), ("jds", "JDS"), ("coo", "COO")])
+def test_driver_binary_reports_block(fmt, name):
     import subprocess
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     mtx = os.path.join(root, "tests", "golden", "mtx", "random.mtx")
-    out = subprocess.run([os.path.join(root, "bin", "spmv"), mtx, "--format", "ss"],
+    out = subprocess.run([os.path.join(root, "bin", "spmv"), mtx, "--format", fmt],
                          capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stderr + out.stdout
     assert "++++" in out.stdout and "Performance(GFLOPS)" in out.stdout
-    assert "MatrixFormat\tSS" in out.stdout.replace(" ", "")
+    assert f"MatrixFormat\t{name}" in out.stdout.replace(" ", "")
 
 
 def _with_empty_rows(rp, col, val, frac, seed):

@@ -68,7 +68,7 @@ int main(int argc, char **argv) {
 
     spmv_plan_info_t info;
     spmv_plan_info(A_opt.plan, &info);
-    static const char *names[] = {"AUTO", "CRS", "ELL", "SS", "DIA", "HYB"};
+    static const char *names[] = {"AUTO", "CRS", "ELL", "SS", "DIA", "HYB", "CSS", "COO", "JDS"};
     const double gflops = (double)A.nNnz * 2.0 / best / 1e9;
     const double gbs = (double)info.algo_bytes / best / 1e9;
     std::printf("++++++++++++++++++++++++++++++++++++++++\n");
