@@ -41,6 +41,16 @@ CONFIGS = {
 }
 
 
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -214,11 +224,16 @@ def main():
             row_idx = np.repeat(np.arange(rows, dtype=np.int32), np.diff(rp))
             t_cpu, loop, y_cpu = oracle.ref_time("crs", rows, n_glob, row_idx, col, val, x_host,
                                                  min_seconds=args.cpu_seconds, ntry=3)
+            # the 1-thread figure BASELINE.md §4 asks for (short doubling
+            # warm-up, one trial: a bounded sample of the same matrix)
+            t_cpu1, _, _ = oracle.ref_time("crs", rows, n_glob, row_idx, col, val, x_host,
+                                           min_seconds=0.5, ntry=1, nthreads=1)
             del row_idx
             kind_cpu, what = "reference", "reference opt_crs (src/opt_crs.cpp:44-70) built from its sources"
         else:
             t_cpu, loop, y_cpu = oracle.csr_time(rp, col, val, x_host, nthreads=nthreads,
                                                  min_seconds=args.cpu_seconds, ntry=3)
+            t_cpu1, _, _ = oracle.csr_time(rp, col, val, x_host, nthreads=1, min_seconds=0.5, ntry=1)
             kind_cpu, what = "port", "oracle opt_crs restatement (OpenMP static)"
         ygpu = y_head.cpu().numpy()
         max_rel = float(np.max(np.abs(ygpu - y_cpu) / np.maximum(np.abs(y_cpu), 1e-300)))
@@ -229,7 +244,10 @@ def main():
                "sample": f"full {rows}-row matrix, {what}, "
                          f"{loop} calls x 3 trials after a {args.cpu_seconds:.0f} s doubling warm-up, "
                          f"min mean per call",
-               "ms_per_call": t_cpu * 1e3}
+               "ms_per_call": t_cpu * 1e3,
+               "gbs": (12 * nnz_local + 4 * (rows + 1) + 16 * rows) / t_cpu / 1e9,
+               "value_1thread": 2.0 * nnz_local / t_cpu1 / 1e9,
+               "cpu_model": cpu_model()}
 
     achieved = r["achieved_gbs"]
     # measured STREAM-read ceiling of this GPU (reported beside the spec peak)

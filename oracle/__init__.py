@@ -220,6 +220,7 @@ def ref_lib(fmt: str):
     L.ref_time.argtypes = [C.c_int, C.c_int, C.c_int, _I32P, _I32P, _F64P, _F64P, _F64P,
                            C.c_double, C.c_int, C.POINTER(C.c_int)]
     L.ref_time.restype = C.c_double
+    L.ref_set_threads.argtypes = [C.c_int]
     _ref_libs[fmt] = L
     return L
 
@@ -261,15 +262,19 @@ def ref_spmv(fmt: str, m, n, row, col, val, x, y_init=None, calls: int = 2
     return y[:m], bool(ok)
 
 
-def ref_time(fmt: str, m, n, row, col, val, x, min_seconds: float = 1.0, ntry: int = 10):
+def ref_time(fmt: str, m, n, row, col, val, x, min_seconds: float = 1.0, ntry: int = 10,
+             nthreads: int = 0):
     """The reference driver's timing (src/main.cpp:58-102) of the REFERENCE's
-    own plugin `fmt` (compiled from its sources): (seconds per call, loop, y)."""
+    own plugin `fmt` (compiled from its sources): (seconds per call, loop, y).
+    nthreads > 0 sets the OpenMP thread count for the call (0 = default)."""
     L = ref_lib(fmt)
+    L.ref_set_threads(int(nthreads))
     y = np.empty(max(m, 1))
     loop = C.c_int()
     t = L.ref_time(m, n, len(val), np.ascontiguousarray(row, np.int32), np.ascontiguousarray(col, np.int32),
                    np.ascontiguousarray(val, np.float64), np.ascontiguousarray(x, np.float64), y,
                    float(min_seconds), int(ntry), C.byref(loop))
+    L.ref_set_threads(0)
     return t, loop.value, y[:m]
 
 

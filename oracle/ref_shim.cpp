@@ -9,6 +9,8 @@
 //
 // Outputs go to oracle/_ref/ (git-ignored).  Never shipped, never used by the
 // product path.
+#include <omp.h>
+
 #include <cstdlib>
 #include <cstring>
 #include <vector>
@@ -81,6 +83,12 @@ int ref_run(int m, int n, int nnz, const int *row_idx, const int *col_idx,
     for (int i = 0; i < calls; i++) SpMV(A_opt, x_opt, yv);
     // VerifyResult on the last call (src/util.cpp:67-83): 1 = pass
     return VerifyResult(A, xv, yv) ? 1 : 0;
+}
+
+// thread count of the reference's OpenMP regions (0 = runtime default)
+void ref_set_threads(int n) {
+    static const int dflt = omp_get_max_threads();
+    omp_set_num_threads(n > 0 ? n : dflt);
 }
 
 // The reference driver's timing of a plugin (src/main.cpp:36, 58-102):

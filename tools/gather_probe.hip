@@ -16,6 +16,8 @@
 //       does the vector memory path merge same-line lanes of one instruction?
 //   e8: 1 MB table, gathers + the CSS entry stream (4 B col + 2 B slot + 8 B
 //       value per gather) vs the 4 B index stream alone
+//   e9: 1 MB table, gathers issued through the SCALAR cache (readlane + s_load)
+//       alone and mixed 1:3 with vector gathers: is it a second request path?
 //   e7: 1 MB table, one 1024-thread workgroup per CU (LDS-pinned), 256 .. 16
 //       CUs: does the per-CU rate rise when fewer CUs share the L2?
 #include <hip/hip_runtime.h>
@@ -104,6 +106,42 @@ __global__ __launch_bounds__(256) void gather_css_shape(const int *__restrict__ 
         for (int u = 0; u < 4; ++u) g[u] = tab[c[u]];
 #pragma unroll
         for (int u = 0; u < 4; ++u) acc += g[u] * v[u] + r[u];
+    }
+    if (acc == 1.2345) out[t] = acc;
+}
+
+// scalar-path gathers: every lane's index is read into an SGPR and gathered
+// with a scalar load; SCAL_OF_4 of every 4 index groups go the scalar way
+template <int SCAL_OF_4>
+__global__ __launch_bounds__(256) void gather_scalar(const int *__restrict__ idx, const double *__restrict__ tab,
+                                                     double *__restrict__ out, long long n) {
+    const long long G = (long long)gridDim.x * blockDim.x;
+    const int lane = threadIdx.x & 63;
+    long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    double acc = 0;
+    for (long long i = t; i < n; i += G * 4) {
+        int c[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            long long j = i + u * G;
+            c[u] = __builtin_nontemporal_load(idx + (j < n ? j : 0));
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (u < SCAL_OF_4) {
+                double mine = 0;
+                for (int k0 = 0; k0 < 64; k0 += 16) {
+                    double v[16];
+#pragma unroll
+                    for (int k = 0; k < 16; ++k) v[k] = tab[__builtin_amdgcn_readlane(c[u], k0 + k)];  // s_load
+#pragma unroll
+                    for (int k = 0; k < 16; ++k) mine = lane == k0 + k ? v[k] : mine;
+                }
+                acc += mine;
+            } else {
+                acc += tab[c[u]];
+            }
+        }
     }
     if (acc == 1.2345) out[t] = acc;
 }
@@ -304,6 +342,34 @@ int main(int argc, char **argv) {
         }
         CK(hipFree(slot));
         CK(hipFree(vals));
+    }
+    std::printf("], \"e9\": [");
+    {
+        const long long te = (1LL << 20) / 8;
+        const long long n = N / 4;
+        hipLaunchKernelGGL(make_idx, dim3(4096), dim3(256), 0, 0, idx, n, te, te);
+        CK(hipDeviceSynchronize());
+        for (int mode = 0; mode < 4; ++mode) {
+            hipEvent_t a2, b2;
+            CK(hipEventCreate(&a2));
+            CK(hipEventCreate(&b2));
+            float bm = 1e30f;
+            for (int r = 0; r < 4; ++r) {
+                CK(hipEventRecord(a2));
+                if (mode == 0) hipLaunchKernelGGL(gather_scalar<0>, dim3(blocks), dim3(256), 0, 0, idx, tab, out, n);
+                else if (mode == 1) hipLaunchKernelGGL(gather_scalar<1>, dim3(blocks), dim3(256), 0, 0, idx, tab, out, n);
+                else if (mode == 2) hipLaunchKernelGGL(gather_scalar<2>, dim3(blocks), dim3(256), 0, 0, idx, tab, out, n);
+                else hipLaunchKernelGGL(gather_scalar<4>, dim3(blocks), dim3(256), 0, 0, idx, tab, out, n);
+                CK(hipEventRecord(b2));
+                CK(hipEventSynchronize(b2));
+                float ms;
+                CK(hipEventElapsedTime(&ms, a2, b2));
+                if (r && ms < bm) bm = ms;
+            }
+            std::printf("%s{\"scalar_of_4\": %d, \"ms\": %.4f, \"Ggather_s\": %.2f}", mode ? ", " : "",
+                        mode == 3 ? 4 : mode, bm, n / (bm * 1e-3) / 1e9);
+            std::fflush(stdout);
+        }
     }
     std::printf("], \"e7\": [");
     first = true;
