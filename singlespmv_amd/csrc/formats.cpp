@@ -398,6 +398,7 @@ int build_dia(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
             val[(size_t)(di * d.mp + r)] += A.val[j];  // duplicates are summed
         }
     SPMV_RETURN_IF(upload(p, &d.off, offs.data(), d.n_diags));
+    if (const char *e = std::getenv("SPMV_DIA_DEBUG")) d.dbg = std::atoi(e);
     SPMV_RETURN_IF(upload(p, &d.val, val.data(), slots));
     p->stored_slots = slots;
     p->algo_bytes = 8 * A.nnz + 4 * (int64_t)d.n_diags + 8 * A.n + 8 * A.m;

@@ -132,6 +132,7 @@ struct DiaDev {
     std::vector<int32_t> off_host;
     double *val = nullptr;   // [n_diags * mp]
     int64_t mp = 0;          // diagonal stride: m rounded up to even
+    int dbg = 0;             // SPMV_DIA_DEBUG (internal): 1 = x from global memory, no LDS window
 };
 
 // Column-slab sweep (CSS, k_css.hip).  Per (pass p, workgroup b, worker wave

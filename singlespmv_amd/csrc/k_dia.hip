@@ -17,16 +17,31 @@ namespace spmv {
 
 // Two rows per lane: one 16-byte load of val[d*mp + r .. r+1] per diagonal
 // (mp = m rounded up to even), so a wave instruction streams 1 KiB.
-template <int UNROLL>
+//
+// LDSX: the workgroup's 512 rows need x over ONE contiguous column window
+// [r0 + off_min, r0 + 511 + off_max + 1]; it is staged once into LDS with
+// coalesced loads and every diagonal reads its pair x[c], x[c+1] from there,
+// so the only HBM stream left is val (and x once).  Without LDSX (diagonal
+// span too wide for the window) x is read from global memory per diagonal.
+template <int UNROLL, bool LDSX>
 __global__ __launch_bounds__(256) void dia_kernel(int64_t m, int64_t mp, int64_t n, int n_diags,
-                                                  const int32_t *__restrict__ off,
+                                                  const int32_t *__restrict__ off, int32_t off_min, int32_t win,
                                                   const double *__restrict__ val,
                                                   const double *__restrict__ x,
                                                   double *__restrict__ y) {
-    const int64_t r = 2 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x);
+    extern __shared__ double xs[];
+    const int64_t r0 = 2 * (int64_t)blockIdx.x * blockDim.x;
+    const int64_t r = r0 + 2 * threadIdx.x;
+    auto xat = [&](int64_t c) { return x[c < 0 ? 0 : (c >= n ? n - 1 : c)]; };
+    if (LDSX) {
+        // out-of-range columns only meet zero-filled slots: any finite x works
+        const int64_t c0 = r0 + off_min;
+        for (int i = threadIdx.x; i < win; i += blockDim.x) xs[i] = xat(c0 + i);
+        __syncthreads();
+    }
     if (r >= m) return;
     double acc0 = 0.0, acc1 = 0.0;
-    auto xat = [&](int64_t c) { return x[c < 0 ? 0 : (c >= n ? n - 1 : c)]; };
+    const int lbase = 2 * threadIdx.x - off_min;  // LDS index of column r + 0
     int d = 0;
     for (; d + UNROLL <= n_diags; d += UNROLL) {
         f64x2 v[UNROLL];
@@ -35,9 +50,15 @@ __global__ __launch_bounds__(256) void dia_kernel(int64_t m, int64_t mp, int64_t
         for (int u = 0; u < UNROLL; ++u) v[u] = ld_stream2(val + (int64_t)(d + u) * mp + r);
 #pragma unroll
         for (int u = 0; u < UNROLL; ++u) {
-            const int64_t c = r + off[d + u];
-            g0[u] = xat(c);
-            g1[u] = xat(c + 1);
+            if (LDSX) {
+                const int li = lbase + off[d + u];
+                g0[u] = xs[li];
+                g1[u] = xs[li + 1];
+            } else {
+                const int64_t c = r + off[d + u];
+                g0[u] = xat(c);
+                g1[u] = xat(c + 1);
+            }
         }
 #pragma unroll
         for (int u = 0; u < UNROLL; ++u) {
@@ -47,21 +68,43 @@ __global__ __launch_bounds__(256) void dia_kernel(int64_t m, int64_t mp, int64_t
     }
     for (; d < n_diags; ++d) {
         const f64x2 v = ld_stream2(val + (int64_t)d * mp + r);
-        const int64_t c = r + off[d];
-        acc0 = madd(v.x, xat(c), acc0);
-        acc1 = madd(v.y, xat(c + 1), acc1);
+        double a, b;
+        if (LDSX) {
+            const int li = lbase + off[d];
+            a = xs[li];
+            b = xs[li + 1];
+        } else {
+            const int64_t c = r + off[d];
+            a = xat(c);
+            b = xat(c + 1);
+        }
+        acc0 = madd(v.x, a, acc0);
+        acc1 = madd(v.y, b, acc1);
     }
     y[r] = acc0;
     if (r + 1 < m) y[r + 1] = acc1;
 }
 
+// LDS x window of a 512-row workgroup: 512 rows + diagonal span + 1
+constexpr int kDiaMaxWin = 8192;  // doubles (64 KB)
+
 int launch_dia(const spmv_plan_s *p, const double *x, double *y) {
     const DiaDev &d = p->dia;
     if (p->m == 0) return SPMV_SUCCESS;
+    if (d.n_diags == 0) {  // no stored diagonal: y = 0
+        SPMV_HIP_TRY(hipMemsetAsync(y, 0, sizeof(double) * (size_t)p->m, p->stream));
+        return SPMV_SUCCESS;
+    }
     const int64_t pairs = (p->m + 1) / 2;
     const int64_t blocks = (pairs + 255) / 256;
-    hipLaunchKernelGGL((dia_kernel<8>), dim3((unsigned)blocks), dim3(256), 0, p->stream, p->m, d.mp,
-                       p->n, d.n_diags, d.off, d.val, x, y);
+    const int32_t off_min = d.off_host.front(), off_max = d.off_host.back();
+    const int64_t win = 512 + (int64_t)off_max - off_min + 1;
+    if (win <= kDiaMaxWin && !(p->dia.dbg & 1))
+        hipLaunchKernelGGL((dia_kernel<8, true>), dim3((unsigned)blocks), dim3(256), sizeof(double) * (size_t)win,
+                           p->stream, p->m, d.mp, p->n, d.n_diags, d.off, off_min, (int32_t)win, d.val, x, y);
+    else
+        hipLaunchKernelGGL((dia_kernel<8, false>), dim3((unsigned)blocks), dim3(256), 0, p->stream, p->m, d.mp,
+                           p->n, d.n_diags, d.off, off_min, 0, d.val, x, y);
     SPMV_HIP_TRY(hipGetLastError());
     return SPMV_SUCCESS;
 }
