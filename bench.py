@@ -252,6 +252,14 @@ def main():
     achieved = r["achieved_gbs"]
     # measured STREAM-read ceiling of this GPU (reported beside the spec peak)
     stream_gbs = sp.stream_probe(local, 2 << 30, 10)
+    # and the measured ceiling of random 8-byte x gathers that hit L2: every
+    # format here issues one x gather per nnz, so this bounds the gather side
+    gather_gps = sp.gather_probe(local, 64 << 20, 1 << 20)
+    gathers_gps = nnz_local / (r["event_ms_per_launch"] * 1e-3)
+    gather_fields = {}
+    if r["format"] != "dia":  # DIA reads x from an LDS window, not by gathers
+        gather_fields = {"x_gathers_per_s": gathers_gps, "gather_ceiling_per_s": gather_gps,
+                         "frac_of_gather_ceiling": gathers_gps / gather_gps}
     # the reference's CSR5 byte model (CSR5_cuda/detail/utils.h:10-14), which
     # charges x per nnz -- for comparability with published CSR5 numbers only
     csr5_bytes = (rows + 1 + nnz_local) * 4 + (2 * nnz_local + rows) * 8
@@ -278,6 +286,7 @@ def main():
                      "kernel": r["kernel"], "algo_bytes_per_launch": r["algo_bytes"],
                      "launch_ms": r["event_ms_per_launch"],
                      "stream_ceiling_gbs": stream_gbs, "frac_of_stream": achieved / stream_gbs,
+                     **gather_fields,
                      "csr5_model_gbs": csr5_bytes / (r["event_ms_per_launch"] * 1e-3) / 1e9},
         "cpu_baseline": cpu,
         "formats": results,

@@ -141,6 +141,11 @@ const char *spmv_phase_name(spmv_plan_t plan, int32_t k);
  * of a `bytes` buffer (use >> 256 MB), `iters` launches timed with events. */
 int spmv_stream_probe(int32_t device, int64_t bytes, int32_t iters, double *read_gbs);
 
+/* Measured ceiling of random 8-byte gathers (gathers/s): n streamed int32
+ * indices into a `table_bytes` table (1 MB: L2-resident, the best case of a
+ * gather-bound SpMV), 8 gathers in flight per lane, best of 5 launches. */
+int spmv_gather_probe(int32_t device, int64_t n, int64_t table_bytes, double *g_per_s);
+
 /* ---- execution ----------------------------------------------------------- */
 #define SPMV_X_DEVICE 0x1u /* x is a device pointer (else host: H2D per call) */
 #define SPMV_Y_DEVICE 0x2u /* y is a device pointer (else host: D2H per call) */

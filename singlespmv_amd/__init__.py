@@ -81,7 +81,7 @@ class GenSpec(C.Structure):
 EXPORTS = [
     "spmv_options_default", "spmv_plan_create_coo", "spmv_plan_create_csr",
     "spmv_plan_create_csr32", "spmv_plan_create_csr_device", "spmv_plan_destroy", "spmv_execute", "spmv_set_stream",
-    "spmv_time", "spmv_profile", "spmv_phase_name", "spmv_stream_probe", "spmv_plan_info", "spmv_status_string", "spmv_last_error",
+    "spmv_time", "spmv_profile", "spmv_phase_name", "spmv_stream_probe", "spmv_gather_probe", "spmv_plan_info", "spmv_status_string", "spmv_last_error",
     "spmv_load_mtx", "spmv_load_mtx_csr", "spmv_free_host", "spmv_srand", "spmv_rand_vector", "spmv_verify_coo",
     "spmv_coo_to_csr", "spmv_gen_count", "spmv_gen_fill", "spmv_gen_vector",
     "spmv_partition_rows", "spmv_save_csr_bin", "spmv_load_csr_bin",
@@ -112,6 +112,7 @@ def lib():
     L.spmv_time.argtypes = [vp, vp, vp, i32, C.POINTER(f64)]
     L.spmv_profile.argtypes = [vp, vp, vp, i32, C.POINTER(f64), i32, C.POINTER(i32)]
     L.spmv_stream_probe.argtypes = [i32, i64, i32, C.POINTER(f64)]
+    L.spmv_gather_probe.argtypes = [i32, i64, i64, C.POINTER(f64)]
     L.spmv_phase_name.argtypes = [vp, i32]
     L.spmv_phase_name.restype = C.c_char_p
     L.spmv_plan_info.argtypes = [vp, C.POINTER(PlanInfo)]
@@ -269,6 +270,13 @@ def stream_probe(device: int = 0, bytes_: int = 2 << 30, iters: int = 10) -> flo
     """Measured STREAM-read GB/s of the device (the practical HBM ceiling)."""
     g = C.c_double()
     _check(lib().spmv_stream_probe(device, bytes_, iters, C.byref(g)), "spmv_stream_probe")
+    return g.value
+
+
+def gather_probe(device: int = 0, n: int = 64 << 20, table_bytes: int = 1 << 20) -> float:
+    """Measured random 8-byte gathers/s from an L2-resident table."""
+    g = C.c_double()
+    _check(lib().spmv_gather_probe(device, n, table_bytes, C.byref(g)), "spmv_gather_probe")
     return g.value
 
 
