@@ -42,8 +42,9 @@ constexpr int kCssRing = 512;  // slab arrival ring in LDS (aliasing only blurs 
 
 struct CssChunk {
     int32_t c[4];
-    int32_t r[4];
+    uint32_t r2[2];  // the four 16-bit LDS slots, two per register
     double v[4];
+    __device__ __forceinline__ int slot(int u) const { return (int)((r2[u >> 1] >> (16 * (u & 1))) & 0xFFFFu); }
 };
 
 // One 256-entry chunk, branch-free (so the compiler's in-order vmcnt
@@ -54,27 +55,32 @@ __device__ __forceinline__ void css_load(CssChunk &k, int64_t j0, int64_t e1, in
                                          const int32_t *__restrict__ col,
                                          const uint16_t *__restrict__ row,
                                          const double *__restrict__ val) {
+    uint32_t r[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
         const int64_t j = j0 + u * 64 + lane;
         const int64_t jj = j < e1 ? j : 0;
         if (NT) {
             k.c[u] = ld_stream(col + jj);
-            k.r[u] = (int32_t)__builtin_nontemporal_load(row + jj);
+            r[u] = __builtin_nontemporal_load(row + jj);
             k.v[u] = ld_stream(val + jj);
         } else {
             k.c[u] = col[jj];
-            k.r[u] = (int32_t)row[jj];
+            r[u] = row[jj];
             k.v[u] = val[jj];
         }
     }
+    k.r2[0] = r[0] | (r[1] << 16);
+    k.r2[1] = r[2] | (r[3] << 16);
 }
 
 __device__ __forceinline__ void css_mask(CssChunk &k, int64_t j0, int64_t e1, int lane) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
         const bool ok = j0 + u * 64 + lane < e1;
-        k.r[u] = ok ? k.r[u] : kCssMaxRows;
+        const uint32_t keep = ok ? 0xFFFFu : 0u, dummy = ok ? 0u : (uint32_t)kCssMaxRows;
+        const int sh = 16 * (u & 1);
+        k.r2[u >> 1] = (k.r2[u >> 1] & ~(0xFFFFu << sh)) | ((((k.r2[u >> 1] >> sh) & keep) | dummy) << sh);
         k.v[u] = ok ? k.v[u] : 0.0;
     }
 }
@@ -191,16 +197,20 @@ __global__ __launch_bounds__(kCssThreads) void css_sweep_kernel(
             // so two chunks of gathers and two of stream loads stay in flight
             // while the atomics of chunk k run.  Lanes past e1 are masked in
             // the loads (slot -1) and gather x[0].
-            CssChunk L0, L1, L2, L3;
+            // DBG & 128 (ablation): matrix stream prefetched 3 chunks ahead
+            constexpr int AHEAD = (DBG & 128) ? 3 : 2;
+            CssChunk L0, L1, L2, L3, L4;
             double g0[4], g1[4];
             css_load<NT>(L0, e0, e1, lane, col, row, val);
             css_load<NT>(L1, e0 + 256, e1, lane, col, row, val);
+            if (AHEAD == 3) css_load<NT>(L2, e0 + 512, e1, lane, col, row, val);
             if (e0 < e1) {
                 const int s0 = __builtin_amdgcn_readfirstlane(L0.c[0]) >> slab_shift;
                 if (s0 > cur) enter(s0);
             }
             css_gather<DBG>(g0, L0, x);
-            css_load<NT>(L2, e0 + 512, e1, lane, col, row, val);
+            if (AHEAD == 3) css_load<NT>(L3, e0 + 768, e1, lane, col, row, val);
+            else css_load<NT>(L2, e0 + 512, e1, lane, col, row, val);
             for (int64_t j0 = e0; j0 < e1; j0 += 256) {
                 __builtin_amdgcn_sched_barrier(0);
                 if (j0 + 256 < e1) {
@@ -209,19 +219,21 @@ __global__ __launch_bounds__(kCssThreads) void css_sweep_kernel(
                 }
                 css_gather<DBG>(g1, L1, x);
                 __builtin_amdgcn_sched_barrier(0);
-                css_load<NT>(L3, j0 + 768, e1, lane, col, row, val);
+                if (AHEAD == 3) css_load<NT>(L4, j0 + 1024, e1, lane, col, row, val);
+                else css_load<NT>(L3, j0 + 768, e1, lane, col, row, val);
                 __builtin_amdgcn_sched_barrier(0);
                 css_mask(L0, j0, e1, lane);
                 if (DBG & 2) {
 #pragma unroll
-                    for (int u = 0; u < 4; ++u) dsink += __dmul_rn(L0.v[u], g0[u]) * (double)L0.r[u];
+                    for (int u = 0; u < 4; ++u) dsink += __dmul_rn(L0.v[u], g0[u]) * (double)L0.slot(u);
                 } else {
 #pragma unroll
-                    for (int u = 0; u < 4; ++u) atomicAdd(&ylds[L0.r[u]], __dmul_rn(L0.v[u], g0[u]));
+                    for (int u = 0; u < 4; ++u) atomicAdd(&ylds[L0.slot(u)], __dmul_rn(L0.v[u], g0[u]));
                 }
                 L0 = L1;
                 L1 = L2;
                 L2 = L3;
+                if (AHEAD == 3) L3 = L4;
 #pragma unroll
                 for (int u = 0; u < 4; ++u) g0[u] = g1[u];
             }
@@ -269,7 +281,8 @@ int launch_css(const spmv_plan_s *p, const double *x, double *y) {
     const uint64_t seq = mp->css.launches++;
     // ablations (SPMV_CSS_DEBUG, internal): 1 no gathers, 2 no LDS atomics,
     // 8 default cache policy on the matrix stream, 16 all gathers in 1 MiB
-    switch (c.dbg & 19) {
+    switch (c.dbg & 147) {
+        case 128: launch_css_t<true, 128>(p, x, y, seq); break;
         case 1: launch_css_t<true, 1>(p, x, y, seq); break;
         case 2: launch_css_t<true, 2>(p, x, y, seq); break;
         case 16: launch_css_t<true, 16>(p, x, y, seq); break;
