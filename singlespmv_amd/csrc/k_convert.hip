@@ -58,8 +58,8 @@ int exclusive_scan(spmv_plan_s *p, const int64_t *in, int64_t *out, int64_t n, h
     const int64_t nb = (n + kScanBlock - 1) / kScanBlock;
     int64_t *sums, *offs;
     SPMV_HIP_TRY(hipMalloc(&sums, sizeof(int64_t) * nb));
-    SPMV_HIP_TRY(hipMalloc(&offs, sizeof(int64_t) * nb));
     tmp.push_back(sums);
+    SPMV_HIP_TRY(hipMalloc(&offs, sizeof(int64_t) * nb));
     tmp.push_back(offs);
     hipLaunchKernelGGL(scan_block_sums, dim3((unsigned)nb), dim3(kScanBlock), 0, st, in, n, sums);
     if (nb > 1) SPMV_RETURN_IF(exclusive_scan(p, sums, offs, nb, st, tmp));
@@ -223,11 +223,16 @@ int build_ss_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, c
     }
     const int64_t m = p->m, nnz = p->nnz, T = 64 * (int64_t)s.sigma;
     s.n_tiles = (nnz + T - 1) / T;
-    std::vector<void *> tmp;
-    auto cleanup = [&]() {
-        (void)hipStreamSynchronize(st);
-        for (void *t : tmp) (void)hipFree(t);
-    };
+    // scratch freed on every exit path (after the stream drains)
+    struct Scratch {
+        hipStream_t st;
+        std::vector<void *> v;
+        ~Scratch() {
+            (void)hipStreamSynchronize(st);
+            for (void *t : v) (void)hipFree(t);
+        }
+    } scratch{st, {}};
+    std::vector<void *> &tmp = scratch.v;
     // non-empty ordinals
     int64_t *flg = nullptr, *nzord = nullptr;
     SPMV_HIP_TRY(hipMalloc(&flg, 8 * (size_t)std::max<int64_t>(m + 1, 1)));
@@ -236,11 +241,7 @@ int build_ss_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, c
     tmp.push_back(nzord);
     hipLaunchKernelGGL(nonempty_flags, dim3(grid_for(m)), dim3(256), 0, st, d_rp, m, flg);
     SPMV_HIP_TRY(hipMemsetAsync(flg + m, 0, 8, st));
-    int st_scan = exclusive_scan(p, flg, nzord, m + 1, st, tmp);
-    if (st_scan != SPMV_SUCCESS) {
-        cleanup();
-        return st_scan;
-    }
+    SPMV_RETURN_IF(exclusive_scan(p, flg, nzord, m + 1, st, tmp));
     SPMV_HIP_TRY(hipMemcpyAsync(&s.n_nonempty, nzord + m, 8, hipMemcpyDeviceToHost, st));
     SPMV_HIP_TRY(hipStreamSynchronize(st));
     s.n_empty = m - s.n_nonempty;
@@ -274,7 +275,7 @@ int build_ss_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, c
     SPMV_RETURN_IF(p->arena.alloc(&q, 4 * (size_t)std::max<int64_t>(s.n_tiles, 1)));
     s.tail_ord = (int32_t *)q;
     hipError_t e = hipGetLastError();
-    cleanup();
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
     if (e != hipSuccess) {
         set_error(std::string("device SS conversion: ") + hipGetErrorString(e));
         return SPMV_ERROR_HIP;
