@@ -27,7 +27,7 @@ KERN_OBJ  = $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(KERN_SRC))
 HDRS      = include/spmv_hip.h include/opt_hip.h include/spmv_util.h \
             $(CSRC)/internal.hpp $(CSRC)/device.hpp
 
-all: $(LIB) $(OPTLIB) bin/spmv bin/gather_probe oracle
+all: $(LIB) $(OPTLIB) bin/spmv bin/csr5_api bin/gather_probe oracle
 
 $(OBJDIR):
 	mkdir -p $(OBJDIR)
@@ -47,6 +47,12 @@ bin/spmv: tools/spmv_main.cpp $(CSRC)/opt_hip.cpp $(LIB) $(HDRS)
 	mkdir -p bin
 	$(HIPCC) $(CXXFLAGS) -x c++ -D__HIP_PLATFORM_AMD__ -o $@ tools/spmv_main.cpp \
 	    $(CSRC)/opt_hip.cpp -Lsinglespmv_amd -lspmv_hip -Wl,-rpath,'$$ORIGIN/../singlespmv_amd'
+
+# the CSR5 benchmark's driver flow over include/csr5_hip.h (anonymouslibHandle)
+bin/csr5_api: tools/csr5_api_main.cpp include/csr5_hip.h $(LIB) $(HDRS)
+	mkdir -p bin
+	$(HIPCC) $(CXXFLAGS) -x c++ -D__HIP_PLATFORM_AMD__ -o $@ tools/csr5_api_main.cpp \
+	    -Lsinglespmv_amd -lspmv_hip -Wl,-rpath,'$$ORIGIN/../singlespmv_amd'
 
 # the drop-in as a shared object (format from SPMV_HIP_FORMAT) for ABI tests
 $(OPTLIB): $(CSRC)/opt_hip.cpp $(LIB) $(HDRS)

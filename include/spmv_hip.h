@@ -125,6 +125,12 @@ int spmv_plan_create_csr_device(int64_t m, int64_t n, int64_t nnz, const int64_t
                                 const int32_t *d_col_idx, const double *d_val,
                                 const spmv_options_t *opt, spmv_plan_t *plan);
 
+/* The same from 32-bit device row pointers (the CSR5 handle's inputCSR,
+ * CSR5_cuda/anonymouslib_cuda.h:60-73, takes int arrays on the device). */
+int spmv_plan_create_csr32_device(int32_t m, int32_t n, int32_t nnz, const int32_t *d_row_ptr,
+                                  const int32_t *d_col_idx, const double *d_val,
+                                  const spmv_options_t *opt, spmv_plan_t *plan);
+
 int spmv_plan_destroy(spmv_plan_t plan);
 
 /* ---- per-phase profile (replaces the g_profile / PROF_BEGIN instrumentation
@@ -155,6 +161,11 @@ int spmv_gather_probe(int32_t device, int64_t n, int64_t table_bytes, double *g_
 
 /* y = A * x.  x holds n doubles, y holds m doubles. */
 int spmv_execute(spmv_plan_t plan, const double *x, double *y, uint32_t flags);
+
+/* y = alpha * A * x (the CSR5 handle's spmv(alpha, y),
+ * CSR5_cuda/anonymouslib_cuda.h:262-284); alpha is applied to the finished
+ * row sums (one rounded multiply), beta = 0 as everywhere. */
+int spmv_execute_alpha(spmv_plan_t plan, double alpha, const double *x, double *y, uint32_t flags);
 
 /* Kernels are launched on this stream (a hipStream_t; NULL = null stream). */
 int spmv_set_stream(spmv_plan_t plan, void *hip_stream);

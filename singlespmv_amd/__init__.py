@@ -80,11 +80,13 @@ class GenSpec(C.Structure):
 # Exported symbols of include/spmv_hip.h (checked by tests/test_abi.py).
 EXPORTS = [
     "spmv_options_default", "spmv_plan_create_coo", "spmv_plan_create_csr",
-    "spmv_plan_create_csr32", "spmv_plan_create_csr_device", "spmv_plan_destroy", "spmv_execute", "spmv_set_stream",
-    "spmv_time", "spmv_profile", "spmv_phase_name", "spmv_stream_probe", "spmv_gather_probe", "spmv_plan_info", "spmv_status_string", "spmv_last_error",
-    "spmv_load_mtx", "spmv_load_mtx_csr", "spmv_free_host", "spmv_srand", "spmv_rand_vector", "spmv_verify_coo",
-    "spmv_coo_to_csr", "spmv_gen_count", "spmv_gen_fill", "spmv_gen_vector",
-    "spmv_partition_rows", "spmv_save_csr_bin", "spmv_load_csr_bin",
+    "spmv_plan_create_csr32", "spmv_plan_create_csr_device", "spmv_plan_create_csr32_device",
+    "spmv_plan_destroy", "spmv_execute", "spmv_execute_alpha", "spmv_set_stream", "spmv_time",
+    "spmv_profile", "spmv_phase_name", "spmv_stream_probe", "spmv_gather_probe", "spmv_plan_info",
+    "spmv_status_string", "spmv_last_error", "spmv_load_mtx", "spmv_load_mtx_csr", "spmv_free_host",
+    "spmv_srand", "spmv_rand_vector", "spmv_verify_coo", "spmv_coo_to_csr", "spmv_gen_count",
+    "spmv_gen_fill", "spmv_gen_vector", "spmv_partition_rows", "spmv_save_csr_bin",
+    "spmv_load_csr_bin",
 ]
 
 _lib = None
@@ -108,6 +110,8 @@ def lib():
                                               C.POINTER(vp)]
     L.spmv_plan_destroy.argtypes = [vp]
     L.spmv_execute.argtypes = [vp, vp, vp, C.c_uint32]
+    L.spmv_execute_alpha.argtypes = [vp, f64, vp, vp, C.c_uint32]
+    L.spmv_plan_create_csr32_device.argtypes = [i32, i32, i32, vp, vp, vp, C.POINTER(Options), C.POINTER(vp)]
     L.spmv_set_stream.argtypes = [vp, vp]
     L.spmv_time.argtypes = [vp, vp, vp, i32, C.POINTER(f64)]
     L.spmv_profile.argtypes = [vp, vp, vp, i32, C.POINTER(f64), i32, C.POINTER(i32)]
@@ -351,15 +355,20 @@ class Plan:
         return cls(h.value)
 
     # execution ------------------------------------------------------------
-    def execute(self, x, y, async_: bool = False) -> None:
-        """y = A x.  numpy arrays are host buffers (H2D x / D2H y per call, as
-        src/opt_cusparse.cpp:72,82); torch CUDA tensors are device buffers."""
+    def execute(self, x, y, async_: bool = False, alpha: float = 1.0) -> None:
+        """y = alpha * A x (alpha = 1: y = A x).  numpy arrays are host buffers
+        (H2D x / D2H y per call, as src/opt_cusparse.cpp:72,82); torch CUDA
+        tensors are device buffers."""
         flags = (X_DEVICE if _is_device(x) else 0) | (Y_DEVICE if _is_device(y) else 0)
         if async_:
             flags |= ASYNC
         if isinstance(y, np.ndarray) and not y.flags.c_contiguous:
             raise ValueError("y must be C-contiguous")
-        _check(lib().spmv_execute(self._h, _ptr(x), _ptr(y), flags), "spmv_execute")
+        if alpha == 1.0:
+            _check(lib().spmv_execute(self._h, _ptr(x), _ptr(y), flags), "spmv_execute")
+        else:
+            _check(lib().spmv_execute_alpha(self._h, float(alpha), _ptr(x), _ptr(y), flags),
+                   "spmv_execute_alpha")
 
     def __call__(self, x, y=None):
         if y is None:

@@ -234,6 +234,35 @@ int spmv_plan_create_csr_device(int64_t m, int64_t n, int64_t nnz, const int64_t
     return SPMV_SUCCESS;
 }
 
+int spmv_plan_create_csr32_device(int32_t m, int32_t n, int32_t nnz, const int32_t *d_row_ptr,
+                                  const int32_t *d_col_idx, const double *d_val, const spmv_options_t *opt,
+                                  spmv_plan_t *out) {
+    SPMV_CHECK_ARG(out != nullptr, "plan out-pointer is NULL");
+    *out = nullptr;
+    SPMV_CHECK_ARG(m >= 0 && n >= 0 && nnz >= 0 && d_row_ptr != nullptr, "bad dimensions or NULL row_ptr");
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count == 0) {
+        (void)hipGetLastError();
+        set_error("no HIP device visible (libspmv_hip needs an MI355X / gfx950)");
+        return SPMV_ERROR_NO_DEVICE;
+    }
+    int dev = opt && opt->device >= 0 ? opt->device : -1;
+    if (dev < 0) SPMV_HIP_TRY(hipGetDevice(&dev));
+    SPMV_RETURN_IF(check_device(dev));
+    SPMV_HIP_TRY(hipSetDevice(dev));
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, d_row_ptr) != hipSuccess || a.type != hipMemoryTypeDevice || a.device != dev) {
+        (void)hipGetLastError();
+        set_error("spmv_plan_create_csr32_device: arrays must be device memory on the plan's device");
+        return SPMV_ERROR_INVALID_VALUE;
+    }
+    int64_t *rp64 = nullptr;
+    SPMV_RETURN_IF(widen_row_ptr_device(d_row_ptr, m, &rp64));
+    const int st = spmv_plan_create_csr_device(m, n, nnz, rp64, d_col_idx, d_val, opt, out);
+    (void)hipFree(rp64);
+    return st;
+}
+
 int spmv_coo_to_csr(int32_t m, int64_t nnz, const int32_t *row_idx, int64_t *row_ptr) {
     SPMV_CHECK_ARG(m >= 0 && nnz >= 0 && row_ptr != nullptr, "bad arguments");
     SPMV_CHECK_ARG(nnz == 0 || row_idx != nullptr, "row_idx is NULL");
@@ -273,7 +302,17 @@ int spmv_set_stream(spmv_plan_t p, void *stream) {
     return SPMV_SUCCESS;
 }
 
+static int execute_impl(spmv_plan_t p, double alpha, const double *x, double *y, uint32_t flags);
+
 int spmv_execute(spmv_plan_t p, const double *x, double *y, uint32_t flags) {
+    return execute_impl(p, 1.0, x, y, flags);
+}
+
+int spmv_execute_alpha(spmv_plan_t p, double alpha, const double *x, double *y, uint32_t flags) {
+    return execute_impl(p, alpha, x, y, flags);
+}
+
+static int execute_impl(spmv_plan_t p, double alpha, const double *x, double *y, uint32_t flags) {
     SPMV_CHECK_ARG(p != nullptr, "plan is NULL");
     const bool staged = (flags & SPMV_X_STAGED) != 0;
     SPMV_CHECK_ARG((x != nullptr || p->n == 0 || staged) && (y != nullptr || p->m == 0), "x or y is NULL");
@@ -303,6 +342,7 @@ int spmv_execute(spmv_plan_t p, const double *x, double *y, uint32_t flags) {
         dy = p->y_stage;
     }
     SPMV_RETURN_IF(dispatch(p, dx, dy));
+    SPMV_RETURN_IF(launch_scale(p, dy, alpha));
     if (!(flags & SPMV_Y_DEVICE)) {
         // opt_cusparse.cpp:82 -- D2H copy of y on every call
         if (p->m) SPMV_HIP_TRY(hipMemcpyAsync(y, dy, sizeof(double) * p->m, hipMemcpyDeviceToHost, p->stream));

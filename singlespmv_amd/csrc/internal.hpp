@@ -210,6 +210,8 @@ int build_coo(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o);
 int build_jds(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o);
 // k_convert.hip -- device-input builders (the CSR already lives in HBM).
 int validate_csr_device(const int64_t *d_rp, int64_t m, const int32_t *d_col, int64_t nnz, int64_t n);
+int widen_row_ptr_device(const int32_t *d_rp32, int64_t m, int64_t **d_rp64);  // hipMalloc'd; caller frees
+int launch_scale(const spmv_plan_s *p, double *y, double alpha);              // y *= alpha on p->stream
 int build_csr_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, const double *d_val,
                      const spmv_options_t &o, double mean_row);
 int build_ss_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, const double *d_val,

@@ -152,9 +152,40 @@ __global__ void check_csr(const int64_t *__restrict__ rp, int64_t m, const int32
     if (b1) atomicAdd(&bad[1], b1);
 }
 
+__global__ void rp32_to_64(const int32_t *__restrict__ rp, int64_t n, int64_t *__restrict__ out) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        out[i] = rp[i];
+}
+
+__global__ void scale_kernel(double *__restrict__ y, int64_t n, double alpha) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        y[i] = __dmul_rn(alpha, y[i]);
+}
+
 inline unsigned grid_for(int64_t n) { return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 65536)); }
 
 }  // namespace
+
+int widen_row_ptr_device(const int32_t *d_rp32, int64_t m, int64_t **d_rp64) {
+    *d_rp64 = nullptr;
+    SPMV_HIP_TRY(hipMalloc(d_rp64, 8 * (size_t)(m + 1)));
+    hipLaunchKernelGGL(rp32_to_64, dim3(grid_for(m + 1)), dim3(256), 0, 0, d_rp32, m + 1, *d_rp64);
+    const hipError_t e = hipDeviceSynchronize();
+    if (e != hipSuccess) {
+        (void)hipFree(*d_rp64);
+        *d_rp64 = nullptr;
+        set_error(std::string("row_ptr widening: ") + hipGetErrorString(e));
+        return SPMV_ERROR_HIP;
+    }
+    return SPMV_SUCCESS;
+}
+
+int launch_scale(const spmv_plan_s *p, double *y, double alpha) {
+    if (p->m == 0 || alpha == 1.0) return SPMV_SUCCESS;
+    hipLaunchKernelGGL(scale_kernel, dim3(grid_for(p->m)), dim3(256), 0, p->stream, y, p->m, alpha);
+    SPMV_HIP_TRY(hipGetLastError());
+    return SPMV_SUCCESS;
+}
 
 int validate_csr_device(const int64_t *d_rp, int64_t m, const int32_t *d_col, int64_t nnz, int64_t n) {
     int64_t ends[2] = {0, 0};

@@ -406,3 +406,40 @@ def test_profile_phases():
         assert all(v >= 0 for v in prof.values()) and sum(prof.values()) > 0
         yo = oracle_y(rp, col, val, x.cpu().numpy())
         check_close(y.cpu().numpy(), yo, what=f"profile {fmt}")
+
+
+@pytest.mark.parametrize("args", [[], ["-", "1.0", "16"], ["-", "-0.5", "7"],
+                                  [os.path.join(os.path.dirname(__file__), "golden", "mtx", "random.mtx")]])
+def test_csr5_handle_api(args):
+    """include/csr5_hip.h: the CSR5 benchmark's anonymouslibHandle flow
+    (CSR5_cuda/main.cu call_anonymouslib) -- refuses spmv in CSR mode,
+    y = alpha*A*x within 1e-10 of the benchmark's own check, identical on
+    repeated calls, caller's arrays untouched."""
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([os.path.join(root, "bin", "csr5_api")] + args, capture_output=True, text=True,
+                         timeout=300)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "-> OK" in out.stdout
+
+
+def test_execute_alpha():
+    """spmv_execute_alpha: y = alpha * (A x), alpha applied to the finished row
+    sums (one rounded multiply), every format, host and device buffers."""
+    import torch
+    m = 30000
+    rp, col, val = sp.generate_csr(sp.gen_spec("powerlaw", m, max_len=900, seed=81))
+    x = sp.generate_vector(m, seed=83)
+    yo = oracle_y(rp, col, val, x)
+    for fmt in ["csr", "ell", "ss", "css", "jds"]:
+        plan = sp.Plan.from_csr(m, m, rp, col, val, fmt)
+        y1 = np.full(m, np.nan)
+        plan.execute(x, y1)
+        for alpha in (2.5, -1.0, 0.0):
+            y = np.full(m, np.nan)
+            plan.execute(x, y, alpha=alpha)
+            assert np.array_equal(y, alpha * y1), (fmt, alpha)
+        yd = torch.empty(m, dtype=torch.float64, device="cuda")
+        plan.execute(torch.from_numpy(x).cuda(), yd, alpha=3.0)
+        assert np.array_equal(yd.cpu().numpy(), 3.0 * y1)
+        check_close(y1, yo, what=fmt)
