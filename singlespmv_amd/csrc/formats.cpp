@@ -76,7 +76,9 @@ int auto_ss_sigma(double mean_row) {
 // ---------------------------------------------------------------- CSR
 int build_csr(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
     CsrDev &c = p->csr;
-    c.rp64 = A.nnz >= (int64_t)std::numeric_limits<int32_t>::max() - 64;
+    // 64-bit row pointers from 2^31 entries on; SPMV_CSR_FORCE_RP64 (internal)
+    // exercises that kernel instance on small matrices in the tests
+    c.rp64 = A.nnz >= (int64_t)std::numeric_limits<int32_t>::max() - 64 || std::getenv("SPMV_CSR_FORCE_RP64");
     if (c.rp64) {
         SPMV_RETURN_IF(upload(p, (int64_t **)&c.row_ptr, A.row_ptr, A.m + 1));
     } else {

@@ -443,3 +443,22 @@ def test_execute_alpha():
         plan.execute(torch.from_numpy(x).cuda(), yd, alpha=3.0)
         assert np.array_equal(yd.cpu().numpy(), 3.0 * y1)
         check_close(y1, yo, what=fmt)
+
+
+@pytest.mark.parametrize("lanes", [1, 4, 32])
+def test_csr_64bit_row_pointers(monkeypatch, lanes):
+    """The int64 row-pointer kernel instance (used from 2^31 nnz on), forced
+    on a small matrix: same y as the int32 instance, host and device builds."""
+    import torch
+    m = 40000
+    rp, col, val = sp.generate_csr(sp.gen_spec("powerlaw", m, max_len=1200, seed=91))
+    x = sp.generate_vector(m, seed=93)
+    y32 = run_plan(sp.Plan.from_csr(m, m, rp, col, val, "csr", csr_lanes=lanes), x, m)
+    monkeypatch.setenv("SPMV_CSR_FORCE_RP64", "1")
+    p64 = sp.Plan.from_csr(m, m, rp, col, val, "csr", csr_lanes=lanes)
+    assert p64.info()["row_ptr_bytes"] == 8
+    assert np.array_equal(run_plan(p64, x, m), y32)
+    pd = sp.Plan.from_device_csr(m, m, torch.from_numpy(rp).cuda(), torch.from_numpy(col).cuda(),
+                                 torch.from_numpy(val).cuda(), "csr", csr_lanes=lanes)
+    assert pd.info()["row_ptr_bytes"] == 8
+    assert np.array_equal(run_plan(pd, x, m), y32)
