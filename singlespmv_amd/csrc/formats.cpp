@@ -74,6 +74,80 @@ int auto_ss_sigma(double mean_row) {
 }
 
 // ---------------------------------------------------------------- CSR
+void csr_finish_info(spmv_plan_s *p) {
+    const CsrDev &c = p->csr;
+    p->stored_slots = p->nnz;
+    p->algo_bytes = 12 * p->nnz + (c.rp64 ? 8 : 4) * (p->m + 1) + 8 * p->n + 8 * p->m;
+    p->n_kernels = 1;
+    if (c.lanes > 0) {
+        p->kernel_name = "csr_vec4_kernel<" + std::to_string(c.lanes) + ">";
+    } else {
+        p->kernel_name = "csr_vec4_kernel<adaptive>";
+        p->algo_bytes += 4 * p->m;  // the bins' row lists
+        p->n_kernels = 0;
+        for (int b = 0; b < kCsrBins; ++b) p->n_kernels += c.bin_off[b + 1] > c.bin_off[b];
+    }
+}
+
+// Lanes per row.  An explicit csr_lanes applies to every row.  AUTO bins the
+// rows by length (L = smallest power of two with 4L >= len, capped at 64;
+// rows beyond 4096 entries get a whole workgroup) and, unless one bin holds
+// >= 99 % of the rows with no row needing more than 16 steps of its lanes
+// (then that L serves every row, no row list), keeps per-bin row lists.
+int csr_plan_lanes(spmv_plan_s *p, const int64_t *row_ptr, int64_t m, const spmv_options_t &o) {
+    CsrDev &c = p->csr;
+    if (o.csr_lanes > 0) {
+        c.lanes = o.csr_lanes;
+        if (c.lanes < 1 || c.lanes > 64 || (c.lanes & (c.lanes - 1))) {
+            set_error("csr_lanes must be a power of two in [1, 64]");
+            return SPMV_ERROR_INVALID_VALUE;
+        }
+        return SPMV_SUCCESS;
+    }
+    auto bin_of = [](int64_t len) {
+        if (len > 4096) return kCsrBins - 1;
+        int b = 0;
+        while (b < kCsrBins - 2 && 4 * (int64_t)kCsrBinLanes[b] < len) ++b;
+        return b;
+    };
+    std::vector<uint8_t> bin((size_t)std::max<int64_t>(m, 1));
+    int64_t cnt[kCsrBins] = {0};
+    int64_t maxlen = 0;
+#pragma omp parallel
+    {
+        int64_t lc[kCsrBins] = {0}, lmax = 0;
+#pragma omp for schedule(static)
+        for (int64_t r = 0; r < m; ++r) {
+            const int64_t len = row_ptr[r + 1] - row_ptr[r];
+            const int b = bin_of(len);
+            bin[(size_t)r] = (uint8_t)b;
+            ++lc[b];
+            lmax = std::max(lmax, len);
+        }
+#pragma omp critical
+        {
+            for (int b = 0; b < kCsrBins; ++b) cnt[b] += lc[b];
+            maxlen = std::max(maxlen, lmax);
+        }
+    }
+    int d = 0;
+    for (int b = 1; b < kCsrBins; ++b)
+        if (cnt[b] > cnt[d]) d = b;
+    if (m == 0 || (d < kCsrBins - 1 && (double)cnt[d] >= 0.99 * (double)m && cnt[kCsrBins - 1] == 0 &&
+                   maxlen <= 64 * (int64_t)kCsrBinLanes[d])) {
+        c.lanes = m ? kCsrBinLanes[d] : 1;
+        return SPMV_SUCCESS;
+    }
+    c.lanes = 0;
+    c.bin_off[0] = 0;
+    for (int b = 0; b < kCsrBins; ++b) c.bin_off[b + 1] = c.bin_off[b] + cnt[b];
+    std::vector<int32_t> rows((size_t)m);
+    int64_t pos[kCsrBins];
+    for (int b = 0; b < kCsrBins; ++b) pos[b] = c.bin_off[b];
+    for (int64_t r = 0; r < m; ++r) rows[(size_t)pos[bin[(size_t)r]]++] = (int32_t)r;
+    return upload(p, &c.bin_rows, rows.data(), m);
+}
+
 int build_csr(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
     CsrDev &c = p->csr;
     // 64-bit row pointers from 2^31 entries on; SPMV_CSR_FORCE_RP64 (internal)
@@ -89,16 +163,8 @@ int build_csr(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
     }
     SPMV_RETURN_IF(upload(p, &c.col, A.col, A.nnz, kPad));
     SPMV_RETURN_IF(upload(p, &c.val, A.val, A.nnz, kPad));
-    const double mean = A.m ? (double)A.nnz / (double)A.m : 0.0;
-    c.lanes = o.csr_lanes > 0 ? o.csr_lanes : auto_csr_lanes(mean);
-    if (c.lanes < 1 || c.lanes > 64 || (c.lanes & (c.lanes - 1))) {
-        set_error("csr_lanes must be a power of two in [1, 64]");
-        return SPMV_ERROR_INVALID_VALUE;
-    }
-    p->stored_slots = A.nnz;
-    p->algo_bytes = 12 * A.nnz + (c.rp64 ? 8 : 4) * (A.m + 1) + 8 * A.n + 8 * A.m;
-    p->n_kernels = 1;
-    p->kernel_name = "csr_vec4_kernel<" + std::to_string(c.lanes) + ">";
+    SPMV_RETURN_IF(csr_plan_lanes(p, A.row_ptr, A.m, o));
+    csr_finish_info(p);
     return SPMV_SUCCESS;
 }
 

@@ -56,12 +56,18 @@ struct DevArena {
 // int64), col_idx int32, val f64.  col/val are padded by kPad entries so the
 // 16-byte vector loads of the aligned-start kernel never leave the buffer.
 constexpr int kPad = 8;
+// Adaptive CSR (csr_lanes = AUTO on skewed rows): rows binned by length,
+// bin b summed by kCsrBinLanes[b] lanes per row (256 = one workgroup per row).
+constexpr int kCsrBins = 8;
+constexpr int kCsrBinLanes[kCsrBins] = {1, 2, 4, 8, 16, 32, 64, 256};
 struct CsrDev {
     void *row_ptr = nullptr;  // int32 or int64 [m+1]
     bool rp64 = false;
     int32_t *col = nullptr;   // [nnz + kPad]
     double *val = nullptr;    // [nnz + kPad]
-    int lanes = 4;            // lanes per row (1..64)
+    int lanes = 4;            // lanes per row (1..64); 0 = adaptive (bins)
+    int32_t *bin_rows = nullptr;        // rows of every bin, ascending within a bin
+    int64_t bin_off[kCsrBins + 1] = {};  // host: bin b = bin_rows[bin_off[b], bin_off[b+1])
 };
 
 // Sliced ELL (opt_ell, src/opt_ell.cpp): slices of 64 consecutive rows (one
@@ -218,6 +224,8 @@ int build_ss_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, c
                     const spmv_options_t &o, double mean_row);
 int choose_format(const HostCsr &A, const spmv_options_t &o);
 int auto_csr_lanes(double mean_row);
+int csr_plan_lanes(spmv_plan_s *p, const int64_t *row_ptr, int64_t m, const spmv_options_t &o);
+void csr_finish_info(spmv_plan_s *p);
 int auto_ss_sigma(double mean_row);
 
 // end of one phase of a multi-kernel launch (no-op unless profiling)

@@ -232,15 +232,12 @@ int build_csr_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, 
     SPMV_HIP_TRY(hipMemsetAsync(c.col + p->nnz, 0, 4 * kPad, st));
     SPMV_HIP_TRY(hipMemsetAsync(c.val + p->nnz, 0, 8 * kPad, st));
     SPMV_HIP_TRY(hipStreamSynchronize(st));
-    c.lanes = o.csr_lanes > 0 ? o.csr_lanes : auto_csr_lanes(mean_row);
-    if (c.lanes < 1 || c.lanes > 64 || (c.lanes & (c.lanes - 1))) {
-        set_error("csr_lanes must be a power of two in [1, 64]");
-        return SPMV_ERROR_INVALID_VALUE;
-    }
-    p->stored_slots = p->nnz;
-    p->algo_bytes = 12 * p->nnz + (c.rp64 ? 8 : 4) * (p->m + 1) + 8 * p->n + 8 * p->m;
-    p->n_kernels = 1;
-    p->kernel_name = "csr_vec4_kernel<" + std::to_string(c.lanes) + ">";
+    (void)mean_row;
+    // lanes per row / length bins from the row pointers (m+1 values to the host)
+    std::vector<int64_t> hrp((size_t)p->m + 1);
+    SPMV_HIP_TRY(hipMemcpy(hrp.data(), d_rp, 8 * (size_t)(p->m + 1), hipMemcpyDeviceToHost));
+    SPMV_RETURN_IF(csr_plan_lanes(p, hrp.data(), p->m, o));
+    csr_finish_info(p);
     return SPMV_SUCCESS;
 }
 

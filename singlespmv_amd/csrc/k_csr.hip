@@ -18,16 +18,19 @@
 
 namespace spmv {
 
-template <int L, typename RP>
-__global__ __launch_bounds__(256) void csr_vec4_kernel(int64_t m, const RP *__restrict__ rp,
+// LIST: the rows come from a length bin (rows[]), not 0..m-1 (adaptive CSR)
+template <int L, typename RP, bool LIST>
+__global__ __launch_bounds__(256) void csr_vec4_kernel(int64_t m, const int32_t *__restrict__ rows,
+                                                       const RP *__restrict__ rp,
                                                        const int32_t *__restrict__ col,
                                                        const double *__restrict__ val,
                                                        const double *__restrict__ x,
                                                        double *__restrict__ y) {
     const int64_t gtid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t row = gtid / L;
+    const int64_t g = gtid / L;
     const int lane = threadIdx.x & (L - 1);
-    if (row >= m) return;  // whole groups exit together (L | 256)
+    if (g >= m) return;  // whole groups exit together (L | 256)
+    const int64_t row = LIST ? (int64_t)rows[g] : g;
     const int64_t s = rp[row];
     const int64_t e = rp[row + 1];
     double acc = 0.0;
@@ -49,29 +52,81 @@ __global__ __launch_bounds__(256) void csr_vec4_kernel(int64_t m, const RP *__re
     if (lane == 0) y[row] = acc;
 }
 
+// One 256-thread workgroup per row (the longest-row bin of adaptive CSR):
+// four waves stride the row in 1 KiB chunks, each reduces with the fixed
+// butterfly, and the four wave sums are added in wave order (deterministic).
+template <typename RP>
+__global__ __launch_bounds__(256) void csr_block_kernel(const int32_t *__restrict__ rows, const RP *__restrict__ rp,
+                                                        const int32_t *__restrict__ col,
+                                                        const double *__restrict__ val,
+                                                        const double *__restrict__ x, double *__restrict__ y) {
+    __shared__ double part[4];
+    const int64_t row = rows[blockIdx.x];
+    const int64_t s = rp[row];
+    const int64_t e = rp[row + 1];
+    double acc = 0.0;
+    for (int64_t j = (s & ~(int64_t)3) + 4 * threadIdx.x; j < e; j += 4 * 256) {
+        const i32x4 c = ld_stream4(col + j);
+        const f64x2 v01 = ld_stream2(val + j);
+        const f64x2 v23 = ld_stream2(val + j + 2);
+        if (j + 0 >= s && j + 0 < e) acc = madd(v01.x, ld_x(x, c.x), acc);
+        if (j + 1 >= s && j + 1 < e) acc = madd(v01.y, ld_x(x, c.y), acc);
+        if (j + 2 >= s && j + 2 < e) acc = madd(v23.x, ld_x(x, c.z), acc);
+        if (j + 3 >= s && j + 3 < e) acc = madd(v23.y, ld_x(x, c.w), acc);
+    }
+    acc = group_sum<64>(acc);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) y[row] = __dadd_rn(__dadd_rn(part[0], part[1]), __dadd_rn(part[2], part[3]));
+}
+
 template <int L, typename RP>
-static int launch_csr_t(const spmv_plan_s *p, const double *x, double *y) {
-    const int64_t threads = p->m * L;
+static int launch_csr_t(const spmv_plan_s *p, int64_t nrows, const int32_t *rows, const double *x, double *y) {
+    const int64_t threads = nrows * L;
     const int64_t blocks = (threads + 255) / 256;
     if (blocks == 0) return SPMV_SUCCESS;
-    hipLaunchKernelGGL((csr_vec4_kernel<L, RP>), dim3((unsigned)blocks), dim3(256), 0, p->stream,
-                       p->m, (const RP *)p->csr.row_ptr, p->csr.col, p->csr.val, x, y);
+    if (rows)
+        hipLaunchKernelGGL((csr_vec4_kernel<L, RP, true>), dim3((unsigned)blocks), dim3(256), 0, p->stream, nrows,
+                           rows, (const RP *)p->csr.row_ptr, p->csr.col, p->csr.val, x, y);
+    else
+        hipLaunchKernelGGL((csr_vec4_kernel<L, RP, false>), dim3((unsigned)blocks), dim3(256), 0, p->stream, nrows,
+                           rows, (const RP *)p->csr.row_ptr, p->csr.col, p->csr.val, x, y);
     SPMV_HIP_TRY(hipGetLastError());
     return SPMV_SUCCESS;
 }
 
 template <typename RP>
-static int launch_csr_rp(const spmv_plan_s *p, const double *x, double *y) {
-    switch (p->csr.lanes) {
-        case 1: return launch_csr_t<1, RP>(p, x, y);
-        case 2: return launch_csr_t<2, RP>(p, x, y);
-        case 4: return launch_csr_t<4, RP>(p, x, y);
-        case 8: return launch_csr_t<8, RP>(p, x, y);
-        case 16: return launch_csr_t<16, RP>(p, x, y);
-        case 32: return launch_csr_t<32, RP>(p, x, y);
-        case 64: return launch_csr_t<64, RP>(p, x, y);
+static int launch_csr_lanes(const spmv_plan_s *p, int lanes, int64_t nrows, const int32_t *rows, const double *x,
+                            double *y) {
+    switch (lanes) {
+        case 1: return launch_csr_t<1, RP>(p, nrows, rows, x, y);
+        case 2: return launch_csr_t<2, RP>(p, nrows, rows, x, y);
+        case 4: return launch_csr_t<4, RP>(p, nrows, rows, x, y);
+        case 8: return launch_csr_t<8, RP>(p, nrows, rows, x, y);
+        case 16: return launch_csr_t<16, RP>(p, nrows, rows, x, y);
+        case 32: return launch_csr_t<32, RP>(p, nrows, rows, x, y);
+        case 64: return launch_csr_t<64, RP>(p, nrows, rows, x, y);
+        case 256:
+            if (nrows > 0) {
+                hipLaunchKernelGGL((csr_block_kernel<RP>), dim3((unsigned)nrows), dim3(256), 0, p->stream, rows,
+                                   (const RP *)p->csr.row_ptr, p->csr.col, p->csr.val, x, y);
+                SPMV_HIP_TRY(hipGetLastError());
+            }
+            return SPMV_SUCCESS;
         default: set_error("csr lanes must be a power of two in [1,64]"); return SPMV_ERROR_INVALID_VALUE;
     }
+}
+
+template <typename RP>
+static int launch_csr_rp(const spmv_plan_s *p, const double *x, double *y) {
+    const CsrDev &c = p->csr;
+    if (!c.bin_rows) return launch_csr_lanes<RP>(p, c.lanes, p->m, nullptr, x, y);
+    // adaptive: one launch per non-empty length bin, all on the plan's stream
+    for (int b = 0; b < kCsrBins; ++b) {
+        const int64_t n = c.bin_off[b + 1] - c.bin_off[b];
+        if (n) SPMV_RETURN_IF(launch_csr_lanes<RP>(p, kCsrBinLanes[b], n, c.bin_rows + c.bin_off[b], x, y));
+    }
+    return SPMV_SUCCESS;
 }
 
 int launch_csr(const spmv_plan_s *p, const double *x, double *y) {
