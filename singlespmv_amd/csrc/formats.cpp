@@ -602,7 +602,7 @@ int build_css(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
     } else {
         // narrowest slab that still gives every worker wave ~384 entries per
         // slab: pacing finer than that is pure overhead (measured sweep,
-        // profiles/r02: 2^18 columns for config 2, wider as n grows)
+        // profiles/round1/it2_css: 2^18 columns for config 2, wider as n grows)
         const double per_wave = (double)std::max<int64_t>(A.nnz, 1) / ((double)c.nwg * W * c.P * 384.0);
         c.slab_shift = 14;
         while (c.slab_shift < 24 && (double)((A.n + ((int64_t)1 << c.slab_shift) - 1) >> c.slab_shift) > per_wave)

@@ -5,7 +5,7 @@
 // stays cache resident).  Re-designed for the MI355X memory
 // hierarchy, where a random 8-byte x gather that misses the XCD's 4 MiB L2
 // costs a 64 B fabric request (~54 G gathers/s chip-wide, MALL or HBM alike)
-// while an L2 hit runs at ~190 G/s (profiles/r01_baseline/gather_probe.json).
+// while an L2 hit runs at ~190 G/s (profiles/round1/it1_baseline/gather_probe.json).
 //
 // Geometry (see CssDev):
 //  * one 1024-thread workgroup per CU: 15 WORKER waves + 1 PACER wave.  The
