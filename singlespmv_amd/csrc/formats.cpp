@@ -659,12 +659,39 @@ int build_css(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
             moff[(size_t)pb + 1] = (int64_t)merges[(size_t)pb].size() / 3;
         }
     }
-    for (int64_t L = 0; L < nlists; ++L) woff[L + 1] += woff[L];
+    // list lengths -> physical layout.  Contiguous: list L at woff[L].
+    // Interleaved (default): chunk k (256 entries) of list L of pass p at
+    // pbase + (k * lists_per_pass + L_local) * 256, so at any time all waves of
+    // the chip stream one contiguous band of the entry arrays (measured:
+    // tools/gather_probe.hip e10 vs e13); lists are padded to the longest of
+    // the pass with benign entries (col 0, dummy slot, val 0).
+    std::vector<int32_t> wlen((size_t)nlists);
+    for (int64_t L = 0; L < nlists; ++L) wlen[(size_t)L] = (int32_t)woff[(size_t)L + 1];
     for (int64_t b = 0; b < nblocks; ++b) moff[b + 1] += moff[b];
-    const int64_t total = woff[nlists];
-    std::vector<int32_t> col((size_t)std::max<int64_t>(total, 1));
-    std::vector<uint16_t> slot((size_t)std::max<int64_t>(total, 1));
-    std::vector<double> val((size_t)std::max<int64_t>(total, 1));
+    const int64_t lists_per_pass = (int64_t)c.nwg * W;
+    c.interleaved = true;
+    if (const char *e = std::getenv("SPMV_CSS_LAYOUT")) c.interleaved = std::atoi(e) != 0;
+    int64_t total = 0;
+    if (c.interleaved) {
+        for (int pp = 0; pp < c.P; ++pp) {
+            int64_t kmax = 0;
+            for (int64_t Lq = 0; Lq < lists_per_pass; ++Lq)
+                kmax = std::max<int64_t>(kmax, ((int64_t)wlen[(size_t)(pp * lists_per_pass + Lq)] + 255) / 256);
+            for (int64_t Lq = 0; Lq < lists_per_pass; ++Lq)
+                woff[(size_t)(pp * lists_per_pass + Lq)] = total + Lq * 256;
+            total += kmax * lists_per_pass * 256;
+        }
+        c.chunk_stride = lists_per_pass * 256;
+        woff[(size_t)nlists] = total;
+    } else {
+        woff[0] = 0;
+        for (int64_t L = 0; L < nlists; ++L) woff[(size_t)L + 1] = woff[(size_t)L] + wlen[(size_t)L];
+        total = woff[(size_t)nlists];
+        c.chunk_stride = 256;
+    }
+    std::vector<int32_t> col((size_t)std::max<int64_t>(total, 1), 0);
+    std::vector<uint16_t> slot((size_t)std::max<int64_t>(total, 1), (uint16_t)kCssMaxRows);
+    std::vector<double> val((size_t)std::max<int64_t>(total, 1), 0.0);
     std::vector<int32_t> merge((size_t)std::max<int64_t>(3 * moff[nblocks], 1));
 #pragma omp parallel
     {
@@ -676,12 +703,12 @@ int build_css(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
                 for (int64_t j = pc.begin; j < pc.end; ++j) in.push_back(CssEntry{A.col[j], (uint16_t)pc.slot, A.val[j]});
             // column order = slab order; stable keeps a row's CSR order
             std::stable_sort(in.begin(), in.end(), [](const CssEntry &a, const CssEntry &b) { return a.col < b.col; });
-            int64_t out = woff[L];
-            for (const CssEntry &e : in) {
-                col[out] = e.col;
-                slot[out] = e.slot;
-                val[out] = e.val;
-                ++out;
+            const int64_t base = woff[L];
+            for (size_t i = 0; i < in.size(); ++i) {
+                const int64_t out = base + (int64_t)(i / 256) * c.chunk_stride + (int64_t)(i % 256);
+                col[out] = in[i].col;
+                slot[out] = in[i].slot;
+                val[out] = in[i].val;
             }
             std::vector<CssPiece>().swap(wave_pieces[(size_t)L]);
         }
@@ -691,15 +718,17 @@ int build_css(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
     }
     c.split_rows = moff[nblocks];
     SPMV_RETURN_IF(upload(p, &c.woff, woff.data(), nlists + 1));
+    SPMV_RETURN_IF(upload(p, &c.wlen, wlen.data(), nlists));
     SPMV_RETURN_IF(upload(p, &c.bstart, roff.data(), nblocks + 1));
     c.rmap = nullptr;  // identity (rows in matrix order) unless long rows were dealt out
     if (!longs.empty()) SPMV_RETURN_IF(upload(p, &c.rmap, rmap.data(), (int64_t)rmap.size()));
     SPMV_RETURN_IF(upload(p, &c.moff, moff.data(), nblocks + 1));
     SPMV_RETURN_IF(upload(p, &c.merge, merge.data(), 3 * moff[nblocks]));
-    // +1 zeroed entry: masked lanes of the sweep load index 0 unconditionally
-    SPMV_RETURN_IF(upload(p, &c.col, col.data(), total, 1));
-    SPMV_RETURN_IF(upload(p, &c.row, slot.data(), total, 1));
-    SPMV_RETURN_IF(upload(p, &c.val, val.data(), total, 1));
+    // +256 entries: a contiguous list's last chunk may read past the array
+    // (masked lanes); zero col, val -- and slot 0, which masking overrides
+    SPMV_RETURN_IF(upload(p, &c.col, col.data(), total, 256));
+    SPMV_RETURN_IF(upload(p, &c.row, slot.data(), total, 256));
+    SPMV_RETURN_IF(upload(p, &c.val, val.data(), total, 256));
     std::vector<uint64_t> zeros(8 * 16, 0);
     SPMV_RETURN_IF(upload(p, &c.prog, zeros.data(), (int64_t)zeros.size()));
     c.launches = 0;

@@ -151,7 +151,10 @@ constexpr int kCssMaxRows = 19968;
 constexpr int kCssWorkers = 15;  // worker waves per workgroup (+1 pacer wave)
 struct CssDev {
     int nwg = 0, R = 0, P = 0, S = 0, slab_shift = 17, lag = 2, pace_all = 0;
-    int64_t *woff = nullptr;
+    int64_t *woff = nullptr;    // physical start of each list's chunk 0
+    int32_t *wlen = nullptr;    // entries of each list
+    int64_t chunk_stride = 256; // entries between a list's consecutive 256-entry chunks
+    bool interleaved = true;    // chunks of all lists of a pass interleaved
     int64_t *bstart = nullptr;  // [P*nwg + 1] offsets of each (pass, workgroup) block's rows in rmap
     int32_t *rmap = nullptr;    // block rows in slot order; null = identity (contiguous blocks)
     int64_t *moff = nullptr;    // [P*nwg + 1] merge-triple offsets per block

@@ -47,19 +47,22 @@ struct CssChunk {
     __device__ __forceinline__ int slot(int u) const { return (int)((r2[u >> 1] >> (16 * (u & 1))) & 0xFFFFu); }
 };
 
-// One 256-entry chunk, branch-free (so the compiler's in-order vmcnt
-// tracking stays exact across the pipeline): lanes past e1 load entry 0 and
-// are redirected to the dummy slot kCssMaxRows with value 0 by css_mask.
+// One 256-entry chunk of a wave's list, branch-free (so the compiler's
+// in-order vmcnt tracking stays exact across the pipeline).  Chunk kc of the
+// list starts at base + kc * stride (stride 256: contiguous lists; lists x 256:
+// interleaved layout); lanes past the list's end re-load the list's first
+// entry and are redirected to the dummy slot kCssMaxRows by css_mask.
 template <bool NT>
-__device__ __forceinline__ void css_load(CssChunk &k, int64_t j0, int64_t e1, int lane,
-                                         const int32_t *__restrict__ col,
+__device__ __forceinline__ void css_load(CssChunk &k, int64_t kc, int64_t base, int64_t stride, int64_t len,
+                                         int lane, const int32_t *__restrict__ col,
                                          const uint16_t *__restrict__ row,
                                          const double *__restrict__ val) {
     uint32_t r[4];
+    const int64_t cs = base + kc * stride;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-        const int64_t j = j0 + u * 64 + lane;
-        const int64_t jj = j < e1 ? j : 0;
+        const int64_t o = kc * 256 + u * 64 + lane;
+        const int64_t jj = o < len ? cs + u * 64 + lane : base;
         if (NT) {
             k.c[u] = ld_stream(col + jj);
             r[u] = __builtin_nontemporal_load(row + jj);
@@ -74,10 +77,10 @@ __device__ __forceinline__ void css_load(CssChunk &k, int64_t j0, int64_t e1, in
     k.r2[1] = r[2] | (r[3] << 16);
 }
 
-__device__ __forceinline__ void css_mask(CssChunk &k, int64_t j0, int64_t e1, int lane) {
+__device__ __forceinline__ void css_mask(CssChunk &k, int64_t kc, int64_t len, int lane) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-        const bool ok = j0 + u * 64 + lane < e1;
+        const bool ok = kc * 256 + u * 64 + lane < len;
         const uint32_t keep = ok ? 0xFFFFu : 0u, dummy = ok ? 0u : (uint32_t)kCssMaxRows;
         const int sh = 16 * (u & 1);
         k.r2[u >> 1] = (k.r2[u >> 1] & ~(0xFFFFu << sh)) | ((((k.r2[u >> 1] >> sh) & keep) | dummy) << sh);
@@ -99,7 +102,8 @@ template <bool NT, int DBG>
 __global__ __launch_bounds__(kCssThreads) void css_sweep_kernel(
     const int64_t *__restrict__ bstart, const int32_t *__restrict__ rmap, const int64_t *__restrict__ moff,
     const int32_t *__restrict__ merge, int32_t P, int32_t nwg, int32_t S, int32_t slab_shift, int32_t lag,
-    const int64_t *__restrict__ woff, const int32_t *__restrict__ col,
+    const int64_t *__restrict__ woff, const int32_t *__restrict__ wlen, int64_t stride,
+    const int32_t *__restrict__ col,
     const uint16_t *__restrict__ row, const double *__restrict__ val,
     const double *__restrict__ x, double *__restrict__ y, uint64_t *__restrict__ prog,
     uint64_t seq, int32_t pace_all, uint64_t *__restrict__ tstamp) {
@@ -171,8 +175,8 @@ __global__ __launch_bounds__(kCssThreads) void css_sweep_kernel(
         } else {
             // ---------------- worker waves ----------------------------------
             const int64_t list = ((int64_t)p * nwg + b) * kCssWorkers + w;
-            const int64_t e0 = woff[list];
-            const int64_t e1 = woff[list + 1];
+            const int64_t base = woff[list];
+            const int64_t len = wlen[list];
             int cur = -1;       // slab this wave has entered
             int budget = 4000;  // bounded total waiting per pass
             double dsink = 0.0;
@@ -195,34 +199,35 @@ __global__ __launch_bounds__(kCssThreads) void css_sweep_kernel(
             // Software pipeline, issue order per iteration k (in-order vmcnt):
             //   gathers(k+1) | loads(k+3) | wait gathers(k) | LDS atomics(k)
             // so two chunks of gathers and two of stream loads stay in flight
-            // while the atomics of chunk k run.  Lanes past e1 are masked in
+            // while the atomics of chunk k run.  Lanes past the list end are masked in
             // the loads (slot -1) and gather x[0].
             // DBG & 128 (ablation): matrix stream prefetched 3 chunks ahead
-            constexpr int AHEAD = (DBG & 128) ? 3 : 2;
-            CssChunk L0, L1, L2, L3, L4;
+            // Software pipeline, issue order per iteration: gathers(k+1) |
+            // loads(k+3) | LDS atomics(k).  (A statically rotated 4-way unroll
+            // that keeps more chunks in flight measured slower: more stream
+            // loads queue ahead of the gathers.)
+            CssChunk L0, L1, L2, L3;
             double g0[4], g1[4];
-            css_load<NT>(L0, e0, e1, lane, col, row, val);
-            css_load<NT>(L1, e0 + 256, e1, lane, col, row, val);
-            if (AHEAD == 3) css_load<NT>(L2, e0 + 512, e1, lane, col, row, val);
-            if (e0 < e1) {
+            css_load<NT>(L0, 0, base, stride, len, lane, col, row, val);
+            css_load<NT>(L1, 1, base, stride, len, lane, col, row, val);
+            if (len > 0) {
                 const int s0 = __builtin_amdgcn_readfirstlane(L0.c[0]) >> slab_shift;
                 if (s0 > cur) enter(s0);
             }
             css_gather<DBG>(g0, L0, x);
-            if (AHEAD == 3) css_load<NT>(L3, e0 + 768, e1, lane, col, row, val);
-            else css_load<NT>(L2, e0 + 512, e1, lane, col, row, val);
-            for (int64_t j0 = e0; j0 < e1; j0 += 256) {
+            css_load<NT>(L2, 2, base, stride, len, lane, col, row, val);
+            const int64_t nchunks = (len + 255) / 256;
+            for (int64_t kc = 0; kc < nchunks; ++kc) {
                 __builtin_amdgcn_sched_barrier(0);
-                if (j0 + 256 < e1) {
+                if (kc + 1 < nchunks) {
                     const int s1 = __builtin_amdgcn_readfirstlane(L1.c[0]) >> slab_shift;
                     if (s1 > cur) enter(s1);
                 }
                 css_gather<DBG>(g1, L1, x);
                 __builtin_amdgcn_sched_barrier(0);
-                if (AHEAD == 3) css_load<NT>(L4, j0 + 1024, e1, lane, col, row, val);
-                else css_load<NT>(L3, j0 + 768, e1, lane, col, row, val);
+                css_load<NT>(L3, kc + 3, base, stride, len, lane, col, row, val);
                 __builtin_amdgcn_sched_barrier(0);
-                css_mask(L0, j0, e1, lane);
+                css_mask(L0, kc, len, lane);
                 if (DBG & 2) {
 #pragma unroll
                     for (int u = 0; u < 4; ++u) dsink += __dmul_rn(L0.v[u], g0[u]) * (double)L0.slot(u);
@@ -233,7 +238,6 @@ __global__ __launch_bounds__(kCssThreads) void css_sweep_kernel(
                 L0 = L1;
                 L1 = L2;
                 L2 = L3;
-                if (AHEAD == 3) L3 = L4;
 #pragma unroll
                 for (int u = 0; u < 4; ++u) g0[u] = g1[u];
             }
@@ -266,7 +270,8 @@ template <bool NT, int DBG>
 static void launch_css_t(const spmv_plan_s *p, const double *x, double *y, uint64_t seq) {
     const CssDev &c = p->css;
     hipLaunchKernelGGL((css_sweep_kernel<NT, DBG>), dim3((unsigned)c.nwg), dim3(kCssThreads), 0, p->stream,
-                       c.bstart, c.rmap, c.moff, c.merge, c.P, c.nwg, c.S, c.slab_shift, c.lag, c.woff, c.col, c.row, c.val,
+                       c.bstart, c.rmap, c.moff, c.merge, c.P, c.nwg, c.S, c.slab_shift, c.lag, c.woff, c.wlen,
+                       c.chunk_stride, c.col, c.row, c.val,
                        x, y, c.prog, seq, c.pace_all, c.tstamp);
 }
 
@@ -281,8 +286,9 @@ int launch_css(const spmv_plan_s *p, const double *x, double *y) {
     const uint64_t seq = mp->css.launches++;
     // ablations (SPMV_CSS_DEBUG, internal): 1 no gathers, 2 no LDS atomics,
     // 8 default cache policy on the matrix stream, 16 all gathers in 1 MiB
-    switch (c.dbg & 147) {
-        case 128: launch_css_t<true, 128>(p, x, y, seq); break;
+    switch (c.dbg & 19) {
+        case 18: launch_css_t<true, 18>(p, x, y, seq); break;
+        case 3: launch_css_t<true, 3>(p, x, y, seq); break;
         case 1: launch_css_t<true, 1>(p, x, y, seq); break;
         case 2: launch_css_t<true, 2>(p, x, y, seq); break;
         case 16: launch_css_t<true, 16>(p, x, y, seq); break;

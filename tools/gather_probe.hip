@@ -18,6 +18,9 @@
 //       value per gather) vs the 4 B index stream alone
 //   e9: 1 MB table, gathers issued through the SCALAR cache (readlane + s_load)
 //       alone and mixed 1:3 with vector gathers: is it a second request path?
+//   e10: e8 with every wave streaming its OWN contiguous segment of the entry
+//       arrays (CSS's per-wave lists) instead of the grid-strided layout, in
+//       1024-thread workgroups pinned one per CU
 //   e7: 1 MB table, one 1024-thread workgroup per CU (LDS-pinned), 256 .. 16
 //       CUs: does the per-CU rate rise when fewer CUs share the L2?
 #include <hip/hip_runtime.h>
@@ -144,6 +147,107 @@ __global__ __launch_bounds__(256) void gather_scalar(const int *__restrict__ idx
         }
     }
     if (acc == 1.2345) out[t] = acc;
+}
+
+// e10: per-wave contiguous segments, 4 entries per lane per step (CSS shape)
+__global__ __launch_bounds__(1024) void gather_segments(const int *__restrict__ idx, const unsigned short *__restrict__ slot,
+                                                        const double *__restrict__ vals, const double *__restrict__ tab,
+                                                        double *__restrict__ out, long long n) {
+    extern __shared__ double pin[];
+    const long long waves = (long long)gridDim.x * (blockDim.x / 64);
+    const long long w = (long long)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const long long seg = (n + waves - 1) / waves;
+    const long long b = w * seg, e = b + seg < n ? b + seg : n;
+    double acc = 0;
+    for (long long j0 = b; j0 < e; j0 += 256) {
+        int c[4], r[4];
+        double v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            long long j = j0 + u * 64 + lane;
+            j = j < e ? j : b;
+            c[u] = __builtin_nontemporal_load(idx + j);
+            r[u] = __builtin_nontemporal_load(slot + j);
+            v[u] = __builtin_nontemporal_load(vals + j);
+        }
+        double g[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) g[u] = tab[c[u]];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc += g[u] * v[u] + r[u];
+    }
+    if (threadIdx.x == 0) pin[0] = acc;
+    if (acc == 1.2345) out[w & 2047] = acc + pin[0];
+}
+
+// e11: per-WORKGROUP contiguous segments, the 16 waves taking interleaved
+// 256-entry chunks (wave w: chunks w, w+16, ...), 1 WG of 1024 per CU
+__global__ __launch_bounds__(1024) void gather_wg_interleaved(const int *__restrict__ idx,
+                                                              const unsigned short *__restrict__ slot,
+                                                              const double *__restrict__ vals,
+                                                              const double *__restrict__ tab, double *__restrict__ out,
+                                                              long long n) {
+    extern __shared__ double pin[];
+    const int nw = blockDim.x / 64;
+    const int w = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    const long long seg = (n + gridDim.x - 1) / gridDim.x;
+    const long long b = (long long)blockIdx.x * seg, e = b + seg < n ? b + seg : n;
+    double acc = 0;
+    for (long long j0 = b + (long long)w * 256; j0 < e; j0 += (long long)nw * 256) {
+        int c[4], r[4];
+        double v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            long long j = j0 + u * 64 + lane;
+            j = j < e ? j : b;
+            c[u] = __builtin_nontemporal_load(idx + j);
+            r[u] = __builtin_nontemporal_load(slot + j);
+            v[u] = __builtin_nontemporal_load(vals + j);
+        }
+        double g[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) g[u] = tab[c[u]];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc += g[u] * v[u] + r[u];
+    }
+    if (threadIdx.x == 0) pin[0] = acc;
+    if (acc == 1.2345) out[blockIdx.x * 16 + w] = acc + pin[0];
+}
+
+// e13: chunks interleaved across EVERY wave of the chip (chunk k of wave g at
+// (k*W + g)*256): all waves stream one contiguous band, as in e8, but with
+// CSS's wave-owned 256-entry chunks; 1 WG of 1024 per CU
+__global__ __launch_bounds__(1024) void gather_chip_interleaved(const int *__restrict__ idx,
+                                                                const unsigned short *__restrict__ slot,
+                                                                const double *__restrict__ vals,
+                                                                const double *__restrict__ tab,
+                                                                double *__restrict__ out, long long n) {
+    extern __shared__ double pin[];
+    const long long W = (long long)gridDim.x * (blockDim.x / 64);
+    const long long g = (long long)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    double acc = 0;
+    for (long long j0 = g * 256; j0 < n; j0 += W * 256) {
+        int c[4], r[4];
+        double v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            long long j = j0 + u * 64 + lane;
+            j = j < n ? j : 0;
+            c[u] = __builtin_nontemporal_load(idx + j);
+            r[u] = __builtin_nontemporal_load(slot + j);
+            v[u] = __builtin_nontemporal_load(vals + j);
+        }
+        double gg[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) gg[u] = tab[c[u]];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc += gg[u] * v[u] + r[u];
+    }
+    if (threadIdx.x == 0) pin[0] = acc;
+    if (acc == 1.2345) out[g & 2047] = acc + pin[0];
 }
 
 // groups of k consecutive indices share one random 128 B line
@@ -339,6 +443,82 @@ int main(int argc, char **argv) {
             std::printf("%s{\"entry_stream\": %d, \"ms\": %.4f, \"Ggather_s\": %.2f}", ws ? ", " : "", ws, bm,
                         n / (bm * 1e-3) / 1e9);
             std::fflush(stdout);
+        }
+        // e10: same arrays, per-wave contiguous segments, 1 WG of 1024 per CU
+        CK(hipFuncSetAttribute((const void *)gather_segments, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024));
+        {
+            hipEvent_t a2, b2;
+            CK(hipEventCreate(&a2));
+            CK(hipEventCreate(&b2));
+            float bm = 1e30f;
+            for (int r = 0; r < 4; ++r) {
+                CK(hipEventRecord(a2));
+                hipLaunchKernelGGL(gather_segments, dim3(256), dim3(1024), 96 * 1024, 0, idx, slot, vals, tab, out, n);
+                CK(hipEventRecord(b2));
+                CK(hipEventSynchronize(b2));
+                float ms;
+                CK(hipEventElapsedTime(&ms, a2, b2));
+                if (r && ms < bm) bm = ms;
+            }
+            std::printf(", {\"per_wave_segments\": 1, \"ms\": %.4f, \"Ggather_s\": %.2f}", bm, n / (bm * 1e-3) / 1e9);
+        }
+        CK(hipFuncSetAttribute((const void *)gather_wg_interleaved, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               96 * 1024));
+        {
+            hipEvent_t a2, b2;
+            CK(hipEventCreate(&a2));
+            CK(hipEventCreate(&b2));
+            float bm = 1e30f;
+            for (int r = 0; r < 4; ++r) {
+                CK(hipEventRecord(a2));
+                hipLaunchKernelGGL(gather_wg_interleaved, dim3(256), dim3(1024), 96 * 1024, 0, idx, slot, vals, tab,
+                                   out, n);
+                CK(hipEventRecord(b2));
+                CK(hipEventSynchronize(b2));
+                float ms;
+                CK(hipEventElapsedTime(&ms, a2, b2));
+                if (r && ms < bm) bm = ms;
+            }
+            std::printf(", {\"per_wg_interleaved\": 1, \"ms\": %.4f, \"Ggather_s\": %.2f}", bm,
+                        n / (bm * 1e-3) / 1e9);
+        }
+        // e12: per-wave segments with TWO 1024-thread workgroups per CU (64 KB LDS each)
+        {
+            hipEvent_t a2, b2;
+            CK(hipEventCreate(&a2));
+            CK(hipEventCreate(&b2));
+            float bm = 1e30f;
+            for (int r = 0; r < 4; ++r) {
+                CK(hipEventRecord(a2));
+                hipLaunchKernelGGL(gather_segments, dim3(512), dim3(1024), 64 * 1024, 0, idx, slot, vals, tab, out, n);
+                CK(hipEventRecord(b2));
+                CK(hipEventSynchronize(b2));
+                float ms;
+                CK(hipEventElapsedTime(&ms, a2, b2));
+                if (r && ms < bm) bm = ms;
+            }
+            std::printf(", {\"per_wave_segments_2wg_per_cu\": 1, \"ms\": %.4f, \"Ggather_s\": %.2f}", bm,
+                        n / (bm * 1e-3) / 1e9);
+        }
+        CK(hipFuncSetAttribute((const void *)gather_chip_interleaved, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               96 * 1024));
+        {
+            hipEvent_t a2, b2;
+            CK(hipEventCreate(&a2));
+            CK(hipEventCreate(&b2));
+            float bm = 1e30f;
+            for (int r = 0; r < 4; ++r) {
+                CK(hipEventRecord(a2));
+                hipLaunchKernelGGL(gather_chip_interleaved, dim3(256), dim3(1024), 96 * 1024, 0, idx, slot, vals, tab,
+                                   out, n);
+                CK(hipEventRecord(b2));
+                CK(hipEventSynchronize(b2));
+                float ms;
+                CK(hipEventElapsedTime(&ms, a2, b2));
+                if (r && ms < bm) bm = ms;
+            }
+            std::printf(", {\"chip_interleaved_chunks\": 1, \"ms\": %.4f, \"Ggather_s\": %.2f}", bm,
+                        n / (bm * 1e-3) / 1e9);
         }
         CK(hipFree(slot));
         CK(hipFree(vals));
