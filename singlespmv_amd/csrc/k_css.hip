@@ -196,16 +196,13 @@ __global__ __launch_bounds__(kCssThreads) void css_sweep_kernel(
                     }
                 }
             };
-            // Software pipeline, issue order per iteration k (in-order vmcnt):
-            //   gathers(k+1) | loads(k+3) | wait gathers(k) | LDS atomics(k)
-            // so two chunks of gathers and two of stream loads stay in flight
-            // while the atomics of chunk k run.  Lanes past the list end are masked in
-            // the loads (slot -1) and gather x[0].
-            // DBG & 128 (ablation): matrix stream prefetched 3 chunks ahead
-            // Software pipeline, issue order per iteration: gathers(k+1) |
-            // loads(k+3) | LDS atomics(k).  (A statically rotated 4-way unroll
-            // that keeps more chunks in flight measured slower: more stream
-            // loads queue ahead of the gathers.)
+            // Software pipeline, issue order per iteration k: gathers(k+1) |
+            // stream loads(k+3) | LDS atomics(k), the stream loads of k+1 and
+            // k+2 already in flight.  The register rotation at the end of the
+            // iteration waits for gathers(k+1); a statically rotated 4-way
+            // unroll without that wait measured 6 % slower (more stream loads
+            // queue ahead of the gathers).  Lanes past the list end are masked
+            // (dummy slot, +0.0).
             CssChunk L0, L1, L2, L3;
             double g0[4], g1[4];
             css_load<NT>(L0, 0, base, stride, len, lane, col, row, val);
