@@ -298,15 +298,21 @@ def main():
     if shape_world != world:
         out["emulated_world"] = shape_world
         out["config"]["parallelism"] = f"EMULATED rank 0 of {shape_world} (development only)"
-    traffic_file = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(traffic_file):
+    # roofline.traffic: PMC bytes per launch of this kernel/config -- the
+    # calibrated figure where one exists (FETCH_SIZE calibrated on a known
+    # byte count of the same access pattern), else raw FETCH+WRITE
+    key = f"{args.config}:{rows}:{r['kernel']}"
+    for fname, kind in (("pmc_traffic_calibrated.json", "pmc_calibrated"), ("pmc_traffic.json", "pmc_raw")):
+        path = os.path.join(ROOT, "profiles", fname)
         try:
-            t = json.load(open(traffic_file))
-            key = f"{args.config}:{rows}:{r['kernel']}"
-            if key in t:
-                out["roofline"]["traffic"] = t[key]
-        except Exception:
-            pass
+            t = json.load(open(path)) if os.path.exists(path) else {}
+        except ValueError:
+            t = {}
+        if key in t:
+            v = t[key]
+            out["roofline"]["traffic"] = v["bytes"] if isinstance(v, dict) else v
+            out["roofline"]["traffic_kind"] = kind
+            break
     if rank == 0:
         print(json.dumps(out), flush=True)
     if distributed:
