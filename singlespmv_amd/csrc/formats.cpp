@@ -82,10 +82,9 @@ void csr_finish_info(spmv_plan_s *p) {
     if (c.lanes > 0) {
         p->kernel_name = "csr_vec4_kernel<" + std::to_string(c.lanes) + ">";
     } else {
-        p->kernel_name = "csr_vec4_kernel<adaptive>";
+        p->kernel_name = "csr_adaptive_kernel";
         p->algo_bytes += 4 * p->m;  // the bins' row lists
-        p->n_kernels = 0;
-        for (int b = 0; b < kCsrBins; ++b) p->n_kernels += c.bin_off[b + 1] > c.bin_off[b];
+        p->n_kernels = 1;
     }
 }
 

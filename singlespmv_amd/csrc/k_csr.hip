@@ -80,6 +80,92 @@ __global__ __launch_bounds__(256) void csr_block_kernel(const int32_t *__restric
     if (threadIdx.x == 0) y[row] = __dadd_rn(__dadd_rn(part[0], part[1]), __dadd_rn(part[2], part[3]));
 }
 
+// Adaptive CSR in ONE launch: workgroup ranges map to the length bins
+// (blk_off), so all bins run concurrently instead of back to back; the bin
+// test is workgroup-uniform (no divergence).  Bin b has L = kCsrBinLanes[b]
+// lanes per row; the last bin is one workgroup per row.
+struct CsrBinTable {
+    int64_t blk_off[kCsrBins + 1];  // first workgroup of each bin, in launch order
+    int64_t row_off[kCsrBins + 1];  // first row (in bin_rows) of each bin
+};
+// launch order: the longest rows first (their workgroups run longest), so
+// the short-row bins fill in behind them instead of forming the tail
+constexpr int kCsrLaunchOrder[kCsrBins] = {7, 6, 5, 4, 3, 2, 1, 0};
+
+template <int L, typename RP>
+__device__ __forceinline__ void csr_rows_body(int64_t wg, int64_t nrows, const int32_t *__restrict__ rows,
+                                              const RP *__restrict__ rp, const int32_t *__restrict__ col,
+                                              const double *__restrict__ val, const double *__restrict__ x,
+                                              double *__restrict__ y) {
+    const int64_t g = (wg * 256 + threadIdx.x) / L;
+    const int lane = threadIdx.x & (L - 1);
+    if (g >= nrows) return;
+    const int64_t row = rows[g];
+    const int64_t s = rp[row];
+    const int64_t e = rp[row + 1];
+    double acc = 0.0;
+    for (int64_t j = (s & ~(int64_t)3) + 4 * lane; j < e; j += 4 * L) {
+        const i32x4 c = ld_stream4(col + j);
+        const f64x2 v01 = ld_stream2(val + j);
+        const f64x2 v23 = ld_stream2(val + j + 2);
+        const double x0 = (j + 0 >= s && j + 0 < e) ? ld_x(x, c.x) : 0.0;
+        const double x1 = (j + 1 >= s && j + 1 < e) ? ld_x(x, c.y) : 0.0;
+        const double x2 = (j + 2 >= s && j + 2 < e) ? ld_x(x, c.z) : 0.0;
+        const double x3 = (j + 3 >= s && j + 3 < e) ? ld_x(x, c.w) : 0.0;
+        if (j + 0 >= s && j + 0 < e) acc = madd(v01.x, x0, acc);
+        if (j + 1 >= s && j + 1 < e) acc = madd(v01.y, x1, acc);
+        if (j + 2 >= s && j + 2 < e) acc = madd(v23.x, x2, acc);
+        if (j + 3 >= s && j + 3 < e) acc = madd(v23.y, x3, acc);
+    }
+    acc = group_sum<L>(acc);
+    if (lane == 0) y[row] = acc;
+}
+
+template <typename RP>
+__global__ __launch_bounds__(256) void csr_adaptive_kernel(CsrBinTable t, const int32_t *__restrict__ rows,
+                                                           const RP *__restrict__ rp,
+                                                           const int32_t *__restrict__ col,
+                                                           const double *__restrict__ val,
+                                                           const double *__restrict__ x, double *__restrict__ y) {
+    __shared__ double part[4];
+    const int64_t blk = blockIdx.x;
+    int k = 0;
+    while (k < kCsrBins - 1 && blk >= t.blk_off[k + 1]) ++k;  // uniform
+    const int b = kCsrLaunchOrder[k];
+    const int64_t wg = blk - t.blk_off[k];
+    const int32_t *br = rows + t.row_off[b];
+    const int64_t n = t.row_off[b + 1] - t.row_off[b];
+    switch (b) {
+        case 0: csr_rows_body<1, RP>(wg, n, br, rp, col, val, x, y); break;
+        case 1: csr_rows_body<2, RP>(wg, n, br, rp, col, val, x, y); break;
+        case 2: csr_rows_body<4, RP>(wg, n, br, rp, col, val, x, y); break;
+        case 3: csr_rows_body<8, RP>(wg, n, br, rp, col, val, x, y); break;
+        case 4: csr_rows_body<16, RP>(wg, n, br, rp, col, val, x, y); break;
+        case 5: csr_rows_body<32, RP>(wg, n, br, rp, col, val, x, y); break;
+        case 6: csr_rows_body<64, RP>(wg, n, br, rp, col, val, x, y); break;
+        default: {
+            // one workgroup per row: four wave sums added in wave order
+            const int64_t row = br[wg];
+            const int64_t s = rp[row];
+            const int64_t e = rp[row + 1];
+            double acc = 0.0;
+            for (int64_t j = (s & ~(int64_t)3) + 4 * threadIdx.x; j < e; j += 4 * 256) {
+                const i32x4 c = ld_stream4(col + j);
+                const f64x2 v01 = ld_stream2(val + j);
+                const f64x2 v23 = ld_stream2(val + j + 2);
+                if (j + 0 >= s && j + 0 < e) acc = madd(v01.x, ld_x(x, c.x), acc);
+                if (j + 1 >= s && j + 1 < e) acc = madd(v01.y, ld_x(x, c.y), acc);
+                if (j + 2 >= s && j + 2 < e) acc = madd(v23.x, ld_x(x, c.z), acc);
+                if (j + 3 >= s && j + 3 < e) acc = madd(v23.y, ld_x(x, c.w), acc);
+            }
+            acc = group_sum<64>(acc);
+            if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
+            __syncthreads();
+            if (threadIdx.x == 0) y[row] = __dadd_rn(__dadd_rn(part[0], part[1]), __dadd_rn(part[2], part[3]));
+        }
+    }
+}
+
 template <int L, typename RP>
 static int launch_csr_t(const spmv_plan_s *p, int64_t nrows, const int32_t *rows, const double *x, double *y) {
     const int64_t threads = nrows * L;
@@ -121,11 +207,20 @@ template <typename RP>
 static int launch_csr_rp(const spmv_plan_s *p, const double *x, double *y) {
     const CsrDev &c = p->csr;
     if (!c.bin_rows) return launch_csr_lanes<RP>(p, c.lanes, p->m, nullptr, x, y);
-    // adaptive: one launch per non-empty length bin, all on the plan's stream
-    for (int b = 0; b < kCsrBins; ++b) {
+    // adaptive: every bin in one launch (workgroup ranges per bin)
+    CsrBinTable t;
+    t.blk_off[0] = 0;
+    for (int b = 0; b <= kCsrBins; ++b) t.row_off[b] = c.bin_off[b];
+    for (int k = 0; k < kCsrBins; ++k) {
+        const int b = kCsrLaunchOrder[k];
         const int64_t n = c.bin_off[b + 1] - c.bin_off[b];
-        if (n) SPMV_RETURN_IF(launch_csr_lanes<RP>(p, kCsrBinLanes[b], n, c.bin_rows + c.bin_off[b], x, y));
+        const int L = kCsrBinLanes[b];
+        t.blk_off[k + 1] = t.blk_off[k] + (L >= 256 ? n : (n * L + 255) / 256);
     }
+    if (t.blk_off[kCsrBins] == 0) return SPMV_SUCCESS;
+    hipLaunchKernelGGL((csr_adaptive_kernel<RP>), dim3((unsigned)t.blk_off[kCsrBins]), dim3(256), 0, p->stream, t,
+                       c.bin_rows, (const RP *)c.row_ptr, c.col, c.val, x, y);
+    SPMV_HIP_TRY(hipGetLastError());
     return SPMV_SUCCESS;
 }
 
