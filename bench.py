@@ -62,6 +62,9 @@ def parse():
                     help="first entry is the headline plan; the rest are reported alongside")
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     ap.add_argument("--cpu-seconds", type=float, default=2.0)
+    ap.add_argument("--verify", action="store_true",
+                    help="gather y to rank 0 and compare with the oracle over the full matrix "
+                         "(tests; small sizes only)")
     ap.add_argument("--sim-world", type=int, default=0,
                     help="development: run rank 0's share of a K-GPU job on one GPU "
                          "(n = K * rows); the JSON marks it as emulated")
@@ -210,6 +213,17 @@ def main():
         torch.cuda.synchronize()
         coll_ms = (time.perf_counter() - tc) / reps * 1e3
 
+    verify_rel = None
+    if args.verify:
+        # the whole y (all ranks' slices, RCCL/gloo all_gather) vs the oracle's
+        # opt_crs restatement of the full global matrix
+        import oracle
+        y_full = sdist.gather_y(y_head, rows)[:m_glob].cpu().numpy() if distributed else y_head.cpu().numpy()
+        if rank == 0:
+            grp, gcol, gval = sp.generate_csr(spec)
+            yref = oracle.csr_spmv(grp, gcol, gval, x.cpu().numpy())
+            verify_rel = float(np.max(np.abs(y_full - yref) / np.maximum(np.abs(yref), 1e-300)))
+
     # CPU baseline: the oracle's restatement of opt_crs SpMV (OpenMP, all host
     # cores of this rank's affinity), reference timing method, rank 0 at N=1
     cpu = None
@@ -294,6 +308,7 @@ def main():
         "x_broadcast_ms": round(t_bcast * 1e3, 3) if distributed else None,
         "collective_ms": coll_ms,
         "max_rel_err_vs_cpu": max_rel,
+        "verify_max_rel": verify_rel,
     }
     if shape_world != world:
         out["emulated_world"] = shape_world
