@@ -753,11 +753,15 @@ int choose_format(const HostCsr &A, const spmv_options_t &o) {
         if (dia_offsets(A, 256, 1.25, offs)) return SPMV_FORMAT_DIA;
     }
     (void)o;
-    // x far beyond one XCD's 4 MiB L2 and enough rows to fill every CU:
-    // random gathers dominate -> column-slab sweep (L2-resident x slabs)
-    if (A.n * 8 > ((int64_t)16 << 20) && A.m >= 256 * 2048 && mean >= 2.0) return SPMV_FORMAT_CSS;
-    // near-uniform rows -> sliced ELL; skewed -> segmented sum
-    if ((double)maxlen <= 2.0 * mean + 8.0) return SPMV_FORMAT_ELL;
+    // x beyond one XCD's 4 MiB L2 and enough rows to fill every CU: random
+    // gathers dominate -> column-slab sweep (L2-resident x slabs).  Measured
+    // crossover (profiles/round1/probe/auto_sweep.jsonl): row-parallel formats
+    // win at n = 0.5 M (x = 4 MB), CSS from n = 1 M (x = 8 MB) on uniform and
+    // power-law rows alike.
+    if (A.n * 8 > ((int64_t)6 << 20) && A.m >= 256 * 1024 && mean >= 2.0) return SPMV_FORMAT_CSS;
+    // near-uniform rows -> CSR (one lane count fits every row; it matched or
+    // beat sliced ELL at every measured size); skewed -> segmented sum
+    if ((double)maxlen <= 2.0 * mean + 8.0) return SPMV_FORMAT_CSR;
     return SPMV_FORMAT_SS;
 }
 

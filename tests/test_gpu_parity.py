@@ -462,3 +462,22 @@ def test_csr_64bit_row_pointers(monkeypatch, lanes):
                                  torch.from_numpy(val).cuda(), "csr", csr_lanes=lanes)
     assert pd.info()["row_ptr_bytes"] == 8
     assert np.array_equal(run_plan(pd, x, m), y32)
+
+
+def test_auto_format_choice():
+    """AUTO follows the measured crossovers (profiles/round1/probe/
+    auto_sweep.jsonl): banded -> DIA; x beyond ~6 MB -> CSS; below that,
+    near-uniform rows -> CSR, skewed rows -> SS."""
+    cases = [(sp.gen_spec("banded", 300000, band_lo=-8, band_hi=8), "dia"),
+             (sp.gen_spec("uniform", 1_000_000, per_row=8, seed=1), "css"),
+             (sp.gen_spec("powerlaw", 1_000_000, max_len=500, seed=2), "css"),
+             (sp.gen_spec("uniform", 400_000, per_row=8, seed=3), "csr"),
+             (sp.gen_spec("powerlaw", 300_000, max_len=500, seed=4), "ss")]
+    for spec, want in cases:
+        rp, col, val = sp.generate_csr(spec)
+        m = len(rp) - 1
+        plan = sp.Plan.from_csr(m, m, rp, col, val, "auto")
+        assert plan.info()["format"] == want, (spec.kind, m, plan.info()["format"])
+        if m <= 400_000:
+            x = sp.generate_vector(m, seed=5)
+            check_close(run_plan(plan, x, m), oracle_y(rp, col, val, x), what=f"auto {want}")
