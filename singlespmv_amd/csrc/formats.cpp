@@ -88,6 +88,28 @@ void csr_finish_info(spmv_plan_s *p) {
     }
 }
 
+// Length bin of a row (adaptive CSR): L = smallest power of two with 4L >=
+// len (capped at 64), a whole workgroup beyond 4096 entries.
+static int csr_bin_of(int64_t len) {
+    if (len > 4096) return kCsrBins - 1;
+    int b = 0;
+    while (b < kCsrBins - 2 && 4 * (int64_t)kCsrBinLanes[b] < len) ++b;
+    return b;
+}
+
+// Rows 0..m-1 of a CSR grouped by length bin (ascending within a bin).
+static void csr_bin_rows(const int64_t *row_ptr, int64_t m, std::vector<int32_t> &rows,
+                         int64_t off[kCsrBins + 1]) {
+    int64_t cnt[kCsrBins] = {0};
+    for (int64_t r = 0; r < m; ++r) ++cnt[csr_bin_of(row_ptr[r + 1] - row_ptr[r])];
+    off[0] = 0;
+    for (int b = 0; b < kCsrBins; ++b) off[b + 1] = off[b] + cnt[b];
+    int64_t pos[kCsrBins];
+    for (int b = 0; b < kCsrBins; ++b) pos[b] = off[b];
+    rows.resize((size_t)m);
+    for (int64_t r = 0; r < m; ++r) rows[(size_t)pos[csr_bin_of(row_ptr[r + 1] - row_ptr[r])]++] = (int32_t)r;
+}
+
 // Lanes per row.  An explicit csr_lanes applies to every row.  AUTO bins the
 // rows by length (L = smallest power of two with 4L >= len, capped at 64;
 // rows beyond 4096 entries get a whole workgroup) and, unless one bin holds
@@ -255,6 +277,10 @@ static int build_overflow(spmv_plan_s *p, const HostCsr &A, int K) {
     }
     SPMV_RETURN_IF(upload(p, &h.rows, rows.data(), h.n_rows));
     SPMV_RETURN_IF(upload(p, &h.row_ptr, rp.data(), h.n_rows + 1));
+    // overflow rows binned by overflow length (adaptive kernel, y +=)
+    std::vector<int32_t> binned;
+    csr_bin_rows(rp.data(), h.n_rows, binned, h.bin_off);
+    SPMV_RETURN_IF(upload(p, &h.bin_rows, binned.data(), h.n_rows));
     SPMV_RETURN_IF(upload(p, &h.col, col.data(), h.nnz, kPad));
     SPMV_RETURN_IF(upload(p, &h.val, val.data(), h.nnz, kPad));
     return SPMV_SUCCESS;

@@ -89,6 +89,8 @@ struct EllDev {
 // HYB overflow: rows whose length exceeds K keep entries K.. in a CSR over
 // those rows only; a second kernel adds them (one writer per row).
 struct HybDev {
+    int32_t *bin_rows = nullptr;          // overflow rows (local) binned by length
+    int64_t bin_off[kCsrBins + 1] = {};   // host offsets per bin
     int64_t n_rows = 0;
     int32_t *rows = nullptr;     // [n_rows] global row ids
     int64_t *row_ptr = nullptr;  // [n_rows + 1]

@@ -92,11 +92,13 @@ struct CsrBinTable {
 // the short-row bins fill in behind them instead of forming the tail
 constexpr int kCsrLaunchOrder[kCsrBins] = {7, 6, 5, 4, 3, 2, 1, 0};
 
-template <int L, typename RP>
+// ADD: y[yrow[row]] += sum (the HYB/JDS overflow, one writer per row);
+// otherwise y[row] = sum
+template <int L, typename RP, bool ADD>
 __device__ __forceinline__ void csr_rows_body(int64_t wg, int64_t nrows, const int32_t *__restrict__ rows,
                                               const RP *__restrict__ rp, const int32_t *__restrict__ col,
                                               const double *__restrict__ val, const double *__restrict__ x,
-                                              double *__restrict__ y) {
+                                              double *__restrict__ y, const int32_t *__restrict__ yrow) {
     const int64_t g = (wg * 256 + threadIdx.x) / L;
     const int lane = threadIdx.x & (L - 1);
     if (g >= nrows) return;
@@ -118,15 +120,23 @@ __device__ __forceinline__ void csr_rows_body(int64_t wg, int64_t nrows, const i
         if (j + 3 >= s && j + 3 < e) acc = madd(v23.y, x3, acc);
     }
     acc = group_sum<L>(acc);
-    if (lane == 0) y[row] = acc;
+    if (lane == 0) {
+        if (ADD) {
+            const int64_t yi = yrow[row];
+            y[yi] = __dadd_rn(y[yi], acc);
+        } else {
+            y[row] = acc;
+        }
+    }
 }
 
-template <typename RP>
+template <typename RP, bool ADD>
 __global__ __launch_bounds__(256) void csr_adaptive_kernel(CsrBinTable t, const int32_t *__restrict__ rows,
                                                            const RP *__restrict__ rp,
                                                            const int32_t *__restrict__ col,
                                                            const double *__restrict__ val,
-                                                           const double *__restrict__ x, double *__restrict__ y) {
+                                                           const double *__restrict__ x, double *__restrict__ y,
+                                                           const int32_t *__restrict__ yrow) {
     __shared__ double part[4];
     const int64_t blk = blockIdx.x;
     int k = 0;
@@ -136,13 +146,13 @@ __global__ __launch_bounds__(256) void csr_adaptive_kernel(CsrBinTable t, const 
     const int32_t *br = rows + t.row_off[b];
     const int64_t n = t.row_off[b + 1] - t.row_off[b];
     switch (b) {
-        case 0: csr_rows_body<1, RP>(wg, n, br, rp, col, val, x, y); break;
-        case 1: csr_rows_body<2, RP>(wg, n, br, rp, col, val, x, y); break;
-        case 2: csr_rows_body<4, RP>(wg, n, br, rp, col, val, x, y); break;
-        case 3: csr_rows_body<8, RP>(wg, n, br, rp, col, val, x, y); break;
-        case 4: csr_rows_body<16, RP>(wg, n, br, rp, col, val, x, y); break;
-        case 5: csr_rows_body<32, RP>(wg, n, br, rp, col, val, x, y); break;
-        case 6: csr_rows_body<64, RP>(wg, n, br, rp, col, val, x, y); break;
+        case 0: csr_rows_body<1, RP, ADD>(wg, n, br, rp, col, val, x, y, yrow); break;
+        case 1: csr_rows_body<2, RP, ADD>(wg, n, br, rp, col, val, x, y, yrow); break;
+        case 2: csr_rows_body<4, RP, ADD>(wg, n, br, rp, col, val, x, y, yrow); break;
+        case 3: csr_rows_body<8, RP, ADD>(wg, n, br, rp, col, val, x, y, yrow); break;
+        case 4: csr_rows_body<16, RP, ADD>(wg, n, br, rp, col, val, x, y, yrow); break;
+        case 5: csr_rows_body<32, RP, ADD>(wg, n, br, rp, col, val, x, y, yrow); break;
+        case 6: csr_rows_body<64, RP, ADD>(wg, n, br, rp, col, val, x, y, yrow); break;
         default: {
             // one workgroup per row: four wave sums added in wave order
             const int64_t row = br[wg];
@@ -161,9 +171,38 @@ __global__ __launch_bounds__(256) void csr_adaptive_kernel(CsrBinTable t, const 
             acc = group_sum<64>(acc);
             if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
             __syncthreads();
-            if (threadIdx.x == 0) y[row] = __dadd_rn(__dadd_rn(part[0], part[1]), __dadd_rn(part[2], part[3]));
+            if (threadIdx.x == 0) {
+                const double sum = __dadd_rn(__dadd_rn(part[0], part[1]), __dadd_rn(part[2], part[3]));
+                if (ADD) {
+                    const int64_t yi = yrow[row];
+                    y[yi] = __dadd_rn(y[yi], sum);
+                } else {
+                    y[row] = sum;
+                }
+            }
         }
     }
+}
+
+// one launch of the adaptive kernel over length bins (bin_off: host offsets)
+template <typename RP, bool ADD>
+static int launch_adaptive(const spmv_plan_s *p, const int64_t *bin_off, const int32_t *bin_rows, const RP *rp,
+                           const int32_t *col, const double *val, const double *x, double *y,
+                           const int32_t *yrow) {
+    CsrBinTable t;
+    t.blk_off[0] = 0;
+    for (int b = 0; b <= kCsrBins; ++b) t.row_off[b] = bin_off[b];
+    for (int k = 0; k < kCsrBins; ++k) {
+        const int b = kCsrLaunchOrder[k];
+        const int64_t n = bin_off[b + 1] - bin_off[b];
+        const int L = kCsrBinLanes[b];
+        t.blk_off[k + 1] = t.blk_off[k] + (L >= 256 ? n : (n * L + 255) / 256);
+    }
+    if (t.blk_off[kCsrBins] == 0) return SPMV_SUCCESS;
+    hipLaunchKernelGGL((csr_adaptive_kernel<RP, ADD>), dim3((unsigned)t.blk_off[kCsrBins]), dim3(256), 0, p->stream,
+                       t, bin_rows, rp, col, val, x, y, yrow);
+    SPMV_HIP_TRY(hipGetLastError());
+    return SPMV_SUCCESS;
 }
 
 template <int L, typename RP>
@@ -208,20 +247,7 @@ static int launch_csr_rp(const spmv_plan_s *p, const double *x, double *y) {
     const CsrDev &c = p->csr;
     if (!c.bin_rows) return launch_csr_lanes<RP>(p, c.lanes, p->m, nullptr, x, y);
     // adaptive: every bin in one launch (workgroup ranges per bin)
-    CsrBinTable t;
-    t.blk_off[0] = 0;
-    for (int b = 0; b <= kCsrBins; ++b) t.row_off[b] = c.bin_off[b];
-    for (int k = 0; k < kCsrBins; ++k) {
-        const int b = kCsrLaunchOrder[k];
-        const int64_t n = c.bin_off[b + 1] - c.bin_off[b];
-        const int L = kCsrBinLanes[b];
-        t.blk_off[k + 1] = t.blk_off[k] + (L >= 256 ? n : (n * L + 255) / 256);
-    }
-    if (t.blk_off[kCsrBins] == 0) return SPMV_SUCCESS;
-    hipLaunchKernelGGL((csr_adaptive_kernel<RP>), dim3((unsigned)t.blk_off[kCsrBins]), dim3(256), 0, p->stream, t,
-                       c.bin_rows, (const RP *)c.row_ptr, c.col, c.val, x, y);
-    SPMV_HIP_TRY(hipGetLastError());
-    return SPMV_SUCCESS;
+    return launch_adaptive<RP, false>(p, c.bin_off, c.bin_rows, (const RP *)c.row_ptr, c.col, c.val, x, y, nullptr);
 }
 
 int launch_csr(const spmv_plan_s *p, const double *x, double *y) {
@@ -262,6 +288,8 @@ __global__ __launch_bounds__(256) void hyb_overflow_kernel(int64_t nrows, const 
 int launch_hyb_overflow(const spmv_plan_s *p, const double *x, double *y) {
     const HybDev &h = p->hyb;
     if (h.n_rows == 0) return SPMV_SUCCESS;
+    if (h.bin_rows)  // overflow rows binned by their overflow length
+        return launch_adaptive<int64_t, true>(p, h.bin_off, h.bin_rows, h.row_ptr, h.col, h.val, x, y, h.rows);
     const int L = 64;
     const int64_t blocks = (h.n_rows * L + 255) / 256;
     hipLaunchKernelGGL((hyb_overflow_kernel<64>), dim3((unsigned)blocks), dim3(256), 0, p->stream,
