@@ -194,6 +194,7 @@ int build_csr(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
 // order (JDS): slice row i is matrix row order[i]; nullptr = identity.
 int build_ell(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &, int cap, const int32_t *order) {
     EllDev &e = p->ell;
+    if (const char *u = std::getenv("SPMV_ELL_UNROLL")) e.unroll = std::atoi(u);
     auto src = [&](int64_t r) -> int64_t { return order ? (int64_t)order[r] : r; };
     e.n_slices = (A.m + 63) / 64;
     std::vector<int64_t> off((size_t)e.n_slices + 1, 0);
