@@ -58,7 +58,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--rows", type=int, default=0, help="rows per GPU (default: the config's)")
-    ap.add_argument("--formats", default="auto,csr,ell,ss,css",
+    ap.add_argument("--formats", default="auto,csr,ell,ss,css,bin",
                     help="first entry is the headline plan; the rest are reported alongside")
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     ap.add_argument("--cpu-seconds", type=float, default=2.0)
@@ -182,6 +182,8 @@ def main():
         }
         relevant = {"csr": ("csr_lanes",), "ss": ("ss_sigma",), "ell": ("ell_width",),
                     "hyb": ("ell_width",), "dia": ("n_diags",), "css": ("css_passes", "css_slabs")}
+        if info["format"] == "bin" and fi != 0:
+            r["phases_ms"] = plan.profile(x, y, 10)  # Mul / Sum split (opt_ss MulPerf / SumPerf)
         for k in relevant.get(info["format"], ()):
             r[k] = info[k]
         results[fmt if fmt not in results else f"{fmt}_{fi}"] = r

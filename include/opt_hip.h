@@ -8,7 +8,7 @@
  *       mangled _Z15OptimizeProblemRK5SpMatRK3VecR8SpMatOptR6VecOpt
  *   extern "C" void SpMV(const SpMatOpt&, const VecOpt&, Vec&);
  *
- * Format: the first of -DOPT_HIP_{CRS,ELL,SS,DIA,HYB,CSS,COO,JDS} that is defined
+ * Format: the first of -DOPT_HIP_{CRS,ELL,SS,DIA,HYB,CSS,COO,JDS,BIN} that is defined
  * (default AUTO); the environment variable SPMV_HIP_FORMAT
  * (crs|ell|ss|dia|hyb|auto) overrides it at run time.
  *

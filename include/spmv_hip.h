@@ -75,8 +75,11 @@ typedef enum spmv_format {
     SPMV_FORMAT_CSS = 6,  /* opt_css lineage: column-slab sweep, y in LDS, x    */
                           /* slab L2-resident per XCD (large random matrices)  */
     SPMV_FORMAT_COO = 7,  /* opt_coo   (src/opt_coo.cpp): f64 atomics per row segment */
-    SPMV_FORMAT_JDS = 8   /* opt_jds   (src/opt_jds.cpp): rows sorted by length,  */
+    SPMV_FORMAT_JDS = 8,  /* opt_jds   (src/opt_jds.cpp): rows sorted by length,  */
                           /* jagged 64-row slices, y permuted back             */
+    SPMV_FORMAT_BIN = 9   /* opt_ss Mul/Sum x opt_css column blocks: Mul with   */
+                          /* the x strip in LDS, products binned by row block,  */
+                          /* Sum per bin with y in LDS (large random matrices)  */
 } spmv_format_t;
 
 typedef struct spmv_plan_s *spmv_plan_t;
@@ -92,7 +95,9 @@ typedef struct spmv_options {
     int32_t css_slab_shift; /* CSS: slab = 2^shift columns (0 = 18, 2 MiB of x) */
     int32_t css_lag;        /* CSS: pacing slack in slabs (0 = 4, -1 = no pacing) */
     int32_t css_pace;       /* CSS: 0/1 pace against every XCD, 2 own XCD only */
-    int32_t reserved[5];
+    int32_t bin_strip_shift; /* BIN: x strip = 2^shift columns, 13 or 14 (0 = 14) */
+    int32_t bin_groups;      /* BIN: row groups sharing one product buffer (0 = 1) */
+    int32_t reserved[3];
 } spmv_options_t;
 
 /* Fill `opt` with defaults (AUTO format, current device, auto tuning). */
@@ -138,7 +143,8 @@ int spmv_plan_destroy(spmv_plan_t plan);
  * src/main.cpp:172-175).  Runs `iters` synchronised calls on device x/y and
  * returns the mean ms of each phase of the plan's launch sequence:
  *   CSR "csr" | ELL, JDS "ell" | HYB "ell","overflow" | SS "tile","fixup" |
- *   DIA "dia" | CSS "sweep" | COO "zero_y","segment". */
+ *   DIA "dia" | CSS "sweep" | COO "zero_y","segment" | BIN "mul","sum"
+ *   (repeated per row group). */
 int spmv_profile(spmv_plan_t plan, const double *x_dev, double *y_dev, int32_t iters,
                  double *phase_ms, int32_t max_phases, int32_t *n_phases);
 const char *spmv_phase_name(spmv_plan_t plan, int32_t k);

@@ -35,8 +35,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libspmv_hip.so")
 OPT_LIB_PATH = os.path.join(HERE, "libopt_hip.so")
 
-FORMATS = {"auto": 0, "csr": 1, "crs": 1, "ell": 2, "ss": 3, "dia": 4, "hyb": 5, "css": 6, "coo": 7, "jds": 8}
-FORMAT_NAMES = {0: "auto", 1: "csr", 2: "ell", 3: "ss", 4: "dia", 5: "hyb", 6: "css", 7: "coo", 8: "jds"}
+FORMATS = {"auto": 0, "csr": 1, "crs": 1, "ell": 2, "ss": 3, "dia": 4, "hyb": 5, "css": 6, "coo": 7, "jds": 8, "bin": 9}
+FORMAT_NAMES = {0: "auto", 1: "csr", 2: "ell", 3: "ss", 4: "dia", 5: "hyb", 6: "css", 7: "coo", 8: "jds", 9: "bin"}
 X_DEVICE, Y_DEVICE, ASYNC, X_STAGED = 0x1, 0x2, 0x4, 0x8
 GEN_UNIFORM, GEN_POWERLAW, GEN_BANDED = 1, 2, 3
 
@@ -53,7 +53,8 @@ class Options(C.Structure):
     _fields_ = [("format", C.c_int32), ("device", C.c_int32), ("csr_lanes", C.c_int32),
                 ("ell_width", C.c_int32), ("ss_sigma", C.c_int32), ("dia_max_diags", C.c_int32),
                 ("dia_max_fill", C.c_double), ("css_slab_shift", C.c_int32), ("css_lag", C.c_int32),
-                ("css_pace", C.c_int32), ("reserved", C.c_int32 * 5)]
+                ("css_pace", C.c_int32), ("bin_strip_shift", C.c_int32), ("bin_groups", C.c_int32),
+                ("reserved", C.c_int32 * 3)]
 
 
 class PlanInfo(C.Structure):
@@ -294,13 +295,15 @@ def coo_to_csr(m: int, row_idx: np.ndarray) -> np.ndarray:
 # ---------------------------------------------------------------- plans
 def make_options(fmt="auto", device: int = -1, csr_lanes: int = 0, ell_width: int = 0,
                  ss_sigma: int = 0, dia_max_diags: int = 0, dia_max_fill: float = 0.0,
-                 css_slab_shift: int = 0, css_lag: int = 0, css_pace: int = 0) -> Options:
+                 css_slab_shift: int = 0, css_lag: int = 0, css_pace: int = 0,
+                 bin_strip_shift: int = 0, bin_groups: int = 0) -> Options:
     o = Options()
     lib().spmv_options_default(C.byref(o))
     o.format = FORMATS[fmt] if isinstance(fmt, str) else int(fmt)
     o.device, o.csr_lanes, o.ell_width, o.ss_sigma = device, csr_lanes, ell_width, ss_sigma
     o.dia_max_diags, o.dia_max_fill = dia_max_diags, dia_max_fill
     o.css_slab_shift, o.css_lag, o.css_pace = css_slab_shift, css_lag, css_pace
+    o.bin_strip_shift, o.bin_groups = bin_strip_shift, bin_groups
     return o
 
 

@@ -1,0 +1,255 @@
+// build_bin.cpp -- host builder of the binned two-phase Mul/Sum format (BIN,
+// see internal.hpp BinDev and k_bin.hip).  The OptimizeProblem counterpart
+// (src/opt_ss.cpp:52-142 builds opt_ss's segments and val_buf, untimed, once);
+// OpenMP-parallel over bins, 64-bit offsets.
+#include <omp.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "internal.hpp"
+
+namespace spmv {
+
+template <typename T>
+static int upload_vec(spmv_plan_s *p, T **dst, const std::vector<T> &src) {
+    void *q = nullptr;
+    SPMV_RETURN_IF(p->arena.alloc(&q, sizeof(T) * std::max<size_t>(src.size(), 1)));
+    if (!src.empty()) SPMV_HIP_TRY(hipMemcpy(q, src.data(), sizeof(T) * src.size(), hipMemcpyHostToDevice));
+    *dst = (T *)q;
+    return SPMV_SUCCESS;
+}
+
+
+int build_bin(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
+    BinDev &B = p->bin;
+    if (const char *d = std::getenv("SPMV_BIN_DEBUG")) B.dbg = std::atoi(d);
+    int ncu = 0;
+    SPMV_HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, p->device));
+    if (ncu <= 0) ncu = 256;
+    B.strip_shift = o.bin_strip_shift ? o.bin_strip_shift : 14;
+    SPMV_CHECK_ARG(B.strip_shift == 13 || B.strip_shift == 14, "bin_strip_shift must be 13 or 14");
+    const int shift = B.strip_shift;
+    const int64_t C = (int64_t)1 << shift;
+    B.nwg1 = ncu * (shift == 13 ? 2 : 1);  // one (two) 1024-thread workgroups per CU
+    B.nwg2 = ncu;                           // 160 KB of LDS y slices per workgroup
+    // internal tuning knobs; defaults measured at config 2
+    // (profiles/round1/probe/bin_probe_c2.jsonl): 16-entry (128-B) product
+    // lines and 4 Sum waves (5119-row bins, ~1 KB segments) took Mul from
+    // 0.72 to 0.56-0.66 ms
+    B.pad_log = 4;
+    B.sum_waves = 4;
+    // 128-B product lines only when segments are long: the expected segment
+    // (nnz per strip x bin) is ~128 entries at config 2 (pad 16 best) and
+    // 16-64 on the N = 2..8 weak-scaling shapes (pad 8 best: 22 % padding
+    // instead of 43 % at N = 8, profiles/round1/probe/bin_wide.jsonl)
+    {
+        const int64_t S0 = std::max<int64_t>(1, (A.n + C - 1) / C);
+        const int64_t NB0 = std::max<int64_t>(1, (A.m + bin_max_rows(B.sum_waves) - 1) / bin_max_rows(B.sum_waves));
+        const double seg = (double)A.nnz / ((double)S0 * (double)NB0);
+        B.pad_log = seg >= 96.0 ? 4 : 3;
+    }
+    if (const char *e = std::getenv("SPMV_BIN_PADLOG")) B.pad_log = std::min(5, std::max(3, std::atoi(e)));
+    if (const char *e = std::getenv("SPMV_BIN_SUMWAVES")) {
+        const int w = std::atoi(e);
+        B.sum_waves = w == 2 || w == 4 ? w : 8;
+    }
+    B.max_rows = bin_max_rows(B.sum_waves);
+    const int max_rows = B.max_rows;
+    const int64_t PAD = (int64_t)1 << B.pad_log;
+    p->algo_bytes = 12 * A.nnz + 8 * A.n + 8 * A.m;
+    p->n_kernels = 2;
+    p->kernel_name = "bin_mul_kernel+bin_sum_kernel";
+    if (A.m == 0 || A.nnz == 0) {  // launch_bin only clears y
+        B.G = 0;
+        return SPMV_SUCCESS;
+    }
+    const int64_t S = std::max<int64_t>(1, (A.n + C - 1) / C);
+    B.n_strips = S;
+    auto rpad = [PAD](int64_t v) { return (v + PAD - 1) & ~(PAD - 1); };
+
+    // ---- bins: <= max_rows rows, cut at cumulative nnz targets; a
+    // multiple of the Sum kernel's wave count when there are enough rows
+    const int64_t waves = (int64_t)B.nwg2 * B.sum_waves;
+    int64_t nb = std::max<int64_t>(1, (A.m + max_rows - 1) / max_rows);
+    if (nb * 2 >= waves) nb = (nb + waves - 1) / waves * waves;
+    std::vector<int32_t> row0{0};
+    for (int64_t r = 0; r < A.m;) {
+        const int64_t b = (int64_t)row0.size() - 1;
+        int64_t r1;
+        if (b >= nb - 1) {
+            r1 = std::min<int64_t>(A.m, r + max_rows);
+        } else {
+            const int64_t tgt = (int64_t)((__int128)A.nnz * (b + 1) / nb);
+            r1 = std::lower_bound(A.row_ptr + r + 1, A.row_ptr + A.m + 1, tgt) - A.row_ptr;
+            r1 = std::max<int64_t>(r + 1, std::min<int64_t>(r1, r + max_rows));
+        }
+        row0.push_back((int32_t)r1);
+        r = r1;
+    }
+    const int64_t NB = (int64_t)row0.size() - 1;
+    B.n_bins = NB;
+
+    // ---- segment sizes (bin b, strip s)
+    std::vector<int32_t> cnt((size_t)(NB * S), 0);
+#pragma omp parallel for schedule(dynamic, 16)
+    for (int64_t b = 0; b < NB; ++b) {
+        int32_t *cb = cnt.data() + b * S;
+        for (int64_t j = A.row_ptr[row0[b]]; j < A.row_ptr[row0[b + 1]]; ++j) ++cb[A.col[j] >> shift];
+    }
+    std::vector<int64_t> bprod((size_t)NB, 0);
+#pragma omp parallel for schedule(static)
+    for (int64_t b = 0; b < NB; ++b) {
+        int64_t t = 0;
+        for (int64_t s = 0; s < S; ++s) t += rpad(cnt[(size_t)(b * S + s)]);
+        bprod[(size_t)b] = t;
+    }
+    int64_t E = 0;
+    for (int64_t b = 0; b < NB; ++b) E += bprod[(size_t)b];
+    B.n_entries = E;
+
+    // ---- row groups: contiguous bins, balanced by products
+    int G = o.bin_groups > 0 ? o.bin_groups : 1;
+    if (G > NB) G = (int)NB;
+    B.G = G;
+    if (const char *e = std::getenv("SPMV_BIN_REUSE")) B.reuse = std::atoi(e) != 0;
+    B.g_bin.assign((size_t)G + 1, NB);
+    B.g_prod.assign((size_t)G + 1, E);
+    B.g_bin[0] = 0;
+    B.g_prod[0] = 0;
+    {
+        int64_t cum = 0, b = 0;
+        for (int g = 1; g < G; ++g) {
+            const int64_t tgt = (int64_t)((__int128)E * g / G);
+            while (b < NB - (G - g) && (cum < tgt || b <= B.g_bin[(size_t)g - 1])) cum += bprod[(size_t)b++];
+            B.g_bin[(size_t)g] = b;
+            B.g_prod[(size_t)g] = cum;
+        }
+    }
+
+    // ---- offsets: Sum order [b][s] (global), Mul order [g][s][b]
+    std::vector<int64_t> off2((size_t)(NB * S)), off1((size_t)(NB * S));
+    {
+        int64_t cur = 0;
+        for (int64_t i = 0; i < NB * S; ++i) {
+            off2[(size_t)i] = cur;
+            cur += rpad(cnt[(size_t)i]);
+        }
+    }
+    std::vector<int64_t> strip_start((size_t)G * (S + 1));  // Mul-order start of (g, s)
+    for (int g = 0; g < G; ++g) {
+        int64_t cur = B.g_prod[(size_t)g];
+        for (int64_t s = 0; s < S; ++s) {
+            strip_start[(size_t)(g * (S + 1) + s)] = cur;
+            for (int64_t b = B.g_bin[(size_t)g]; b < B.g_bin[(size_t)g + 1]; ++b) {
+                off1[(size_t)(b * S + s)] = cur;
+                cur += rpad(cnt[(size_t)(b * S + s)]);
+            }
+        }
+        strip_start[(size_t)(g * (S + 1) + S)] = cur;
+    }
+    std::vector<int64_t> bin_off((size_t)NB + 1);
+    for (int64_t b = 0; b < NB; ++b) bin_off[(size_t)b] = off2[(size_t)(b * S)];
+    bin_off[(size_t)NB] = E;
+
+    // ---- fill both orders
+    std::vector<double> val1((size_t)E);
+    std::vector<uint16_t> cs1((size_t)E), slot2((size_t)E);
+    std::vector<int32_t> dst1((size_t)(E >> B.pad_log));
+    std::vector<int> gof((size_t)NB);
+    for (int g = 0; g < G; ++g)
+        for (int64_t b = B.g_bin[(size_t)g]; b < B.g_bin[(size_t)g + 1]; ++b) gof[(size_t)b] = g;
+#pragma omp parallel
+    {
+        std::vector<int32_t> cur((size_t)S);
+#pragma omp for schedule(dynamic, 8)
+        for (int64_t b = 0; b < NB; ++b) {
+            std::fill(cur.begin(), cur.end(), 0);
+            const int64_t *o1 = off1.data() + b * S, *o2 = off2.data() + b * S;
+            for (int64_t r = row0[b]; r < row0[b + 1]; ++r) {
+                const uint16_t slot = (uint16_t)(r - row0[b]);
+                for (int64_t j = A.row_ptr[r]; j < A.row_ptr[r + 1]; ++j) {
+                    const int32_t c = A.col[j];
+                    const int64_t s = c >> shift, k = cur[(size_t)s]++;
+                    val1[(size_t)(o1[s] + k)] = A.val[j];
+                    cs1[(size_t)(o1[s] + k)] = (uint16_t)(c & (C - 1));
+                    slot2[(size_t)(o2[s] + k)] = slot;
+                }
+            }
+            const int64_t pb = B.reuse ? B.g_prod[(size_t)gof[(size_t)b]] : 0;
+            for (int64_t s = 0; s < S; ++s) {
+                const int64_t n0 = cnt[(size_t)(b * S + s)], n8 = rpad(n0);
+                for (int64_t k = n0; k < n8; ++k) {
+                    val1[(size_t)(o1[s] + k)] = 0.0;
+                    cs1[(size_t)(o1[s] + k)] = 0;
+                    slot2[(size_t)(o2[s] + k)] = (uint16_t)max_rows;
+                }
+                for (int64_t t = 0; t < n8; t += PAD)
+                    dst1[(size_t)((o1[s] + t) >> B.pad_log)] = (int32_t)((o2[s] + t - pb) >> B.pad_log);
+            }
+        }
+    }
+    std::vector<int64_t>().swap(off1);
+    std::vector<int64_t>().swap(off2);
+
+    // ---- Mul pieces: each workgroup takes an nnz-balanced range of its
+    // group's Mul-ordered entries (cut at 64-entry multiples), split at strips
+    std::vector<int64_t> piece_off{0}, pbeg, pend;
+    std::vector<int32_t> pstrip;
+    for (int g = 0; g < G; ++g) {
+        const int64_t g0 = B.g_prod[(size_t)g], g1 = B.g_prod[(size_t)g + 1];
+        const int64_t *ss = strip_start.data() + (size_t)g * (S + 1);
+        int64_t s = 0;
+        for (int k = 0; k < B.nwg1; ++k) {
+            const int64_t a = g0 + (int64_t)(((__int128)(g1 - g0) * k / B.nwg1) & ~(__int128)63);
+            const int64_t z = k + 1 == B.nwg1 ? g1 : g0 + (int64_t)(((__int128)(g1 - g0) * (k + 1) / B.nwg1) & ~(__int128)63);
+            while (s < S && ss[s + 1] <= a) ++s;
+            for (int64_t t = s; t < S && ss[t] < z; ++t) {
+                const int64_t lo = std::max(a, ss[t]), hi = std::min(z, ss[t + 1]);
+                if (lo < hi) {
+                    pstrip.push_back((int32_t)t);
+                    pbeg.push_back(lo);
+                    pend.push_back(hi);
+                }
+            }
+            piece_off.push_back((int64_t)pstrip.size());
+        }
+    }
+
+    B.prod_cap = B.reuse ? 0 : E;
+    if (B.reuse)
+        for (int g = 0; g < G; ++g) B.prod_cap = std::max(B.prod_cap, B.g_prod[(size_t)g + 1] - B.g_prod[(size_t)g]);
+    auto alloc_prod = [&]() -> int {
+        void *q = nullptr;
+        const size_t bytes = sizeof(double) * (size_t)std::max<int64_t>(B.prod_cap, 1);
+        // physically contiguous product buffer: the Mul writes scatter 1-KB
+        // segments over all of it; measured 0.96 ms steady vs 0.95-0.99 ms
+        // depending on placement (profiles/round1/probe/bin_placement.jsonl)
+        if ((B.dbg & 64) || p->arena.alloc_flags(&q, bytes, hipDeviceMallocContiguous) != SPMV_SUCCESS)
+            SPMV_RETURN_IF(p->arena.alloc(&q, bytes));
+        B.prod = (double *)q;
+        return SPMV_SUCCESS;
+    };
+    if (B.dbg & 32) SPMV_RETURN_IF(alloc_prod());
+    SPMV_RETURN_IF(upload_vec(p, &B.piece_off, piece_off));
+    SPMV_RETURN_IF(upload_vec(p, &B.piece_strip, pstrip));
+    SPMV_RETURN_IF(upload_vec(p, &B.piece_begin, pbeg));
+    SPMV_RETURN_IF(upload_vec(p, &B.piece_end, pend));
+    SPMV_RETURN_IF(upload_vec(p, &B.val1, val1));
+    SPMV_RETURN_IF(upload_vec(p, &B.cs1, cs1));
+    SPMV_RETURN_IF(upload_vec(p, &B.dst1, dst1));
+    SPMV_RETURN_IF(upload_vec(p, &B.slot2, slot2));
+    SPMV_RETURN_IF(upload_vec(p, &B.bin_off, bin_off));
+    SPMV_RETURN_IF(upload_vec(p, &B.bin_row0, row0));
+    if (!(B.dbg & 32)) SPMV_RETURN_IF(alloc_prod());
+    if (B.dbg & 16)
+        std::fprintf(stderr, "[bin] val1 %p cs1 %p dst1 %p slot2 %p prod %p (E %lld)\n", (void *)B.val1, (void *)B.cs1,
+                     (void *)B.dst1, (void *)B.slot2, (void *)B.prod, (long long)E);
+    p->stored_slots = E;
+    p->n_kernels = B.reuse ? 2 * G : G + 1;
+    return SPMV_SUCCESS;
+}
+
+}  // namespace spmv

@@ -94,6 +94,7 @@ static int create_from_csr(const HostCsr &A, const spmv_options_t *opt_in, spmv_
         case SPMV_FORMAT_CSS: st = build_css(p, A, o); break;
         case SPMV_FORMAT_COO: st = build_coo(p, A, o); break;
         case SPMV_FORMAT_JDS: st = build_jds(p, A, o); break;
+        case SPMV_FORMAT_BIN: st = build_bin(p, A, o); break;
         default:
             set_error("unknown format");
             st = SPMV_ERROR_INVALID_VALUE;
@@ -124,6 +125,7 @@ static int dispatch(const spmv_plan_s *p, const double *x, double *y) {
             SPMV_RETURN_IF(launch_ell(p, x, y));
             phase_mark(p);  // ell | overflow
             return launch_hyb_overflow(p, x, y);
+        case SPMV_FORMAT_BIN: return launch_bin(p, x, y);
     }
     set_error("plan has an unknown format");
     return SPMV_ERROR_INVALID_VALUE;
@@ -378,6 +380,11 @@ static const char *const kPhases[][3] = {
     {"ell", "overflow", ""}};
 
 const char *spmv_phase_name(spmv_plan_t p, int32_t k) {
+    static const char *const kBinPhases[8] = {"mul", "sum", "mul.1", "sum.1", "mul.2", "sum.2", "mul.3", "sum.3"};
+    if (p && p->format == SPMV_FORMAT_BIN) {
+        if (!p->bin.reuse) return k == 0 ? "mul" : k == 1 ? "sum" : "";  // groups' Mul launches: one phase
+        return k >= 0 && k < 8 && k < 2 * p->bin.G ? kBinPhases[k] : "";
+    }
     if (!p || k < 0 || k > 2 || p->format < 0 || p->format > SPMV_FORMAT_JDS) return "";
     return kPhases[p->format][k];
 }

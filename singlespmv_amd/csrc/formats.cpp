@@ -31,6 +31,21 @@ int DevArena::alloc(void **p, size_t n) {
     return SPMV_SUCCESS;
 }
 
+int DevArena::alloc_flags(void **p, size_t n, unsigned flags) {
+    if (n == 0) n = 16;
+    void *q = nullptr;
+    hipError_t e = hipExtMallocWithFlags(&q, n, flags);
+    if (e != hipSuccess) {
+        set_error(std::string("hipExtMallocWithFlags(") + std::to_string(n) + "): " + hipGetErrorString(e));
+        (void)hipGetLastError();
+        return e == hipErrorOutOfMemory ? SPMV_ERROR_OUT_OF_MEMORY : SPMV_ERROR_HIP;
+    }
+    ptrs.push_back(q);
+    bytes += (int64_t)n;
+    *p = q;
+    return SPMV_SUCCESS;
+}
+
 void DevArena::release() {
     for (void *q : ptrs) (void)hipFree(q);
     ptrs.clear();
@@ -785,6 +800,12 @@ int choose_format(const HostCsr &A, const spmv_options_t &o) {
     // crossover (profiles/round1/probe/auto_sweep.jsonl): row-parallel formats
     // win at n = 0.5 M (x = 4 MB), CSS from n = 1 M (x = 8 MB) on uniform and
     // power-law rows alike.
+    // Larger still: the binned Mul/Sum (x strips in LDS, no gathers at all)
+    // beats the column-slab sweep from ~3.5 M columns and ~20 M entries
+    // (profiles/round1/probe/bin_vs_css_sizes.jsonl: 0.50 vs 0.58 ms at
+    // 5 M x 5 M uniform, 0.25 vs 0.28 ms at config 3; CSS wins at 1-2 M), and
+    // its advantage grows with n (1.2 vs 2.6 ms at 10 M x 80 M)
+    if (A.n >= 3500000 && A.nnz >= 20000000 && mean >= 2.0) return SPMV_FORMAT_BIN;
     if (A.n * 8 > ((int64_t)6 << 20) && A.m >= 256 * 1024 && mean >= 2.0) return SPMV_FORMAT_CSS;
     // near-uniform rows -> CSR (one lane count fits every row; it matched or
     // beat sliced ELL at every measured size); skewed -> segmented sum

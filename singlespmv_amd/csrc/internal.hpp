@@ -47,6 +47,7 @@ struct DevArena {
     std::vector<void *> ptrs;
     int64_t bytes = 0;
     int alloc(void **p, size_t n);  // hipMalloc, zero-size safe
+    int alloc_flags(void **p, size_t n, unsigned flags);  // hipExtMallocWithFlags
     void release();
 };
 
@@ -173,6 +174,50 @@ struct CssDev {
     uint64_t *tstamp = nullptr;  // dbg & 32: [P*nwg][kCssWorkers + 2] s_memrealtime stamps
 };
 
+// Binned two-phase Mul/Sum (BIN, k_bin.hip) -- opt_ss's Mul -> val_buf ->
+// Sum split (src/opt_ss.cpp:188-221) crossed with opt_css's column blocks
+// (src/opt_css.cpp:33-45).  Columns are cut into strips of 2^strip_shift
+// (the x strip sits in LDS), rows into bins of <= kBinMaxRows (one wave's
+// LDS y slice).  Entries are grouped into segments (strip s, bin b), each
+// sorted by (row, col) and padded to a multiple of 8:
+//   Mul order  [group][s][b][k]: val1 f64, cs1 u16 (column - strip start),
+//              dst1 int32 per 8 entries (8-entry index in the group's product buffer)
+//   Sum order  [group][b][s][k]: slot2 u16 (row - bin start; kBinMaxRows = pad)
+// Mul: prod[dst] = val1 * xs[cs1] (x strip in LDS, coalesced 64-B product lines);
+// Sum: one wave per bin adds its products in order into its LDS slice with
+// ds_add_f64 and writes y -> deterministic, and an unsplit row's sum is the
+// sequential opt_crs sum (column order) bit for bit.  Row groups bound the
+// product buffer (re-used by every group: it can stay in the Infinity Cache).
+constexpr int kBinLdsDoubles = 20480;  // Sum: 160 KB of LDS y slices per workgroup
+constexpr int kBinMulThreads = 1024;
+// Sum waves per workgroup W2 (4 or 8): a wave's slice holds kBinLdsDoubles/W2
+// doubles = bin rows + one dummy slot (padding entries add +0.0 there)
+inline int bin_max_rows(int w2) { return kBinLdsDoubles / w2 - 1; }
+struct BinDev {
+    int strip_shift = 14;  // 13 or 14 (x strip 64 / 128 KB of LDS)
+    int pad_log = 3;       // segments padded to 2^pad_log entries (8: 64-B product lines)
+    int sum_waves = 8;     // W2
+    int max_rows = 0;      // bin_max_rows(W2) = the dummy slot
+    int G = 1;             // row groups: one Mul launch each (write locality)
+    bool reuse = false;    // one product buffer re-used per group (Sum per group)
+    int nwg1 = 0, nwg2 = 0;
+    int64_t n_bins = 0, n_strips = 0, n_entries = 0;
+    std::vector<int64_t> g_bin;    // host [G+1]: bin range of each group
+    std::vector<int64_t> g_prod;   // host [G+1]: product (= Mul entry) range of each group
+    int64_t *piece_off = nullptr;  // [G*nwg1 + 1]: pieces of (group, workgroup)
+    int32_t *piece_strip = nullptr;
+    int64_t *piece_begin = nullptr, *piece_end = nullptr;
+    double *val1 = nullptr;
+    uint16_t *cs1 = nullptr;
+    int32_t *dst1 = nullptr;       // per 2^pad_log entries
+    uint16_t *slot2 = nullptr;
+    int64_t *bin_off = nullptr;   // [n_bins + 1] product offsets (global)
+    int32_t *bin_row0 = nullptr;  // [n_bins + 1]
+    double *prod = nullptr;       // product buffer (largest group)
+    int64_t prod_cap = 0;
+    int dbg = 0;  // SPMV_BIN_DEBUG (internal)
+};
+
 }  // namespace spmv
 
 struct spmv_plan_s {
@@ -188,6 +233,7 @@ struct spmv_plan_s {
     spmv::DiaDev dia;
     spmv::CssDev css;
     spmv::CooDev coo;
+    spmv::BinDev bin;
     double *x_stage = nullptr;  // host-x staging (opt_cusparse.cpp:44-45)
     double *y_stage = nullptr;
     int64_t stored_slots = 0;
@@ -221,6 +267,7 @@ int build_dia(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o);
 int build_css(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o);
 int build_coo(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o);
 int build_jds(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o);
+int build_bin(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o);  // build_bin.cpp
 // k_convert.hip -- device-input builders (the CSR already lives in HBM).
 int validate_csr_device(const int64_t *d_rp, int64_t m, const int32_t *d_col, int64_t nnz, int64_t n);
 int widen_row_ptr_device(const int32_t *d_rp32, int64_t m, int64_t **d_rp64);  // hipMalloc'd; caller frees
@@ -248,5 +295,6 @@ int launch_ss(const spmv_plan_s *p, const double *x, double *y);
 int launch_dia(const spmv_plan_s *p, const double *x, double *y);
 int launch_css(const spmv_plan_s *p, const double *x, double *y);
 int launch_coo(const spmv_plan_s *p, const double *x, double *y);
+int launch_bin(const spmv_plan_s *p, const double *x, double *y);
 
 }  // namespace spmv

@@ -1,0 +1,213 @@
+// k_bin.hip -- binned two-phase Mul/Sum SpMV ("BIN") for gfx950.
+//
+// Lineage: opt_ss splits SpMV into Mul (val_buf[i] = val[i] * x[col[i]],
+// src/opt_ss.cpp:225-239) and Sum (per-row reduction of val_buf,
+// src/opt_ss.cpp:241-303); opt_css cuts the columns into blocks so the x block
+// stays cache resident (src/opt_css.cpp:33-45).  Re-designed for MI355X, where
+// a random 8-byte gather costs one L1 line request (~0.9 G/s per CU even when
+// it hits L2, profiles/round1/probe/gather_probe.json) but an LDS read of the
+// same value costs a few clocks:
+//
+//  * Mul (bin_mul_kernel): a workgroup walks its nnz-balanced range of the
+//    Mul-ordered entry stream strip by strip.  Per strip it stages the
+//    2^SHIFT-column x strip in LDS, then every entry gathers x from LDS and
+//    writes its product to the product buffer at the entry's place in Sum
+//    order.  The entry stream is ordered [strip][bin][row, col] and padded per
+//    (strip, bin) segment to 8 entries, so 8 consecutive lanes write one
+//    aligned 64-byte product line;
+//  * Sum (bin_sum_kernel): one wave per bin (<= kBinMaxRows rows) streams the
+//    bin's products -- contiguous, ordered [strip][row, col] -- and adds them
+//    with ds_add_f64 into its own LDS y slice, then writes the bin's y rows.
+//
+// HBM bytes per nnz: Mul 8 (val) + 2 (column in strip) + 0.5 (destination)
+// + 8 (product), Sum 8 (product) + 2 (row in bin): ~28.5 B, streamed and
+// fully coalesced, against 12 B + an uncoalesced gather for row-parallel
+// kernels.  With row groups (G > 1) the product buffer is re-used by every
+// group so its write/read round trip can stay in the 256 MB Infinity Cache.
+//
+// Determinism / exactness: a bin is owned by one wave, which adds its
+// products in Sum order = column order within each row (strips ascending,
+// columns ascending within a segment); lanes of one ds_add_f64 that hit the
+// same slot are applied in lane order (as k_css.hip relies on, checked bit for
+// bit by the tests); slots start at +0.0 and products are rounded multiplies,
+// so every row is the sequential opt_crs sum (src/opt_crs.cpp:61-66) bit for
+// bit, and repeated calls are identical.
+#include "device.hpp"
+#include "internal.hpp"
+
+namespace spmv {
+
+// MODE (SPMV_BIN_DEBUG, internal ablations): 1 nontemporal product stores,
+// 2 no product stores (value kept alive).  PL: segments padded to 2^PL entries.
+template <int SHIFT, int U, int MODE, int PL>
+__global__ __launch_bounds__(kBinMulThreads) void bin_mul_kernel(
+    const int64_t *__restrict__ piece_off, int64_t q_base, const int32_t *__restrict__ piece_strip,
+    const int64_t *__restrict__ piece_begin, const int64_t *__restrict__ piece_end,
+    const double *__restrict__ val1, const uint16_t *__restrict__ cs1, const int32_t *__restrict__ dst1,
+    const double *__restrict__ x, int64_t n, double *__restrict__ prod) {
+    __shared__ double xs[1 << SHIFT];
+    constexpr int NW = kBinMulThreads / 64;
+    const int w = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    const int64_t q0 = piece_off[q_base + blockIdx.x], q1 = piece_off[q_base + blockIdx.x + 1];
+    for (int64_t q = q0; q < q1; ++q) {
+        // consecutive pieces of a workgroup are consecutive strips: stage x
+        const int64_t c0 = (int64_t)piece_strip[q] << SHIFT;
+        const int64_t e0 = piece_begin[q], e1 = piece_end[q];
+        const int cw = (int)(n - c0 < (1 << SHIFT) ? n - c0 : (1 << SHIFT));
+        __syncthreads();  // the previous strip's readers are done
+        for (int i = threadIdx.x; i < cw; i += kBinMulThreads) xs[i] = x[c0 + i];
+        __syncthreads();
+        for (int64_t base = e0 + (int64_t)w * 64 * U; base < e1; base += (int64_t)NW * 64 * U) {
+            double v[U];
+            uint32_t c[U];
+            int32_t d[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t e = base + u * 64 + lane;
+                const int64_t ee = e < e1 ? e : e0;
+                v[u] = ld_stream(val1 + ee);
+                c[u] = __builtin_nontemporal_load(cs1 + ee);
+                d[u] = ld_stream(dst1 + (ee >> PL));
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t e = base + u * 64 + lane;
+                if (e < e1) {
+                    const double pr = __dmul_rn(v[u], xs[c[u]]);
+                    double *dp = prod + ((int64_t)d[u] << PL) + (e & ((1 << PL) - 1));
+                    if (MODE & 2) {
+                        if (pr == 1.2345e300) *dp = pr;
+                    } else if (MODE & 1) {
+                        __builtin_nontemporal_store(pr, dp);
+                    } else {
+                        *dp = pr;
+                    }
+                }
+            }
+        }
+    }
+}
+
+// MODE (internal ablations): 1 nontemporal product loads, 2 no LDS atomics.
+// W2 waves per workgroup, each owning a slice of kBinLdsDoubles / W2 doubles.
+template <int W2, int U, int MODE>
+__global__ __launch_bounds__(64 * W2) void bin_sum_kernel(
+    int64_t b0, int64_t b1, const int64_t *__restrict__ bin_off, const int32_t *__restrict__ bin_row0,
+    int64_t pbase, const uint16_t *__restrict__ slot2, const double *__restrict__ prod, double *__restrict__ y) {
+    constexpr int SLICE = kBinLdsDoubles / W2;
+    __shared__ double ylds[kBinLdsDoubles];
+    const int w = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    double *ys = ylds + w * SLICE;
+    for (int64_t b = b0 + (int64_t)blockIdx.x * W2 + w; b < b1; b += (int64_t)gridDim.x * W2) {
+        const int64_t r0 = bin_row0[b];
+        const int rows = (int)(bin_row0[b + 1] - r0);
+        for (int i = lane; i < rows; i += 64) ys[i] = 0.0;
+        const int64_t p0 = bin_off[b], p1 = bin_off[b + 1];
+        double sink = 0.0;
+        for (int64_t base = p0; base < p1; base += 64 * U) {
+            double v[U];
+            uint32_t s[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t e = base + u * 64 + lane;
+                const int64_t ee = e < p1 ? e : p0;
+                v[u] = (MODE & 1) ? ld_stream(prod + (ee - pbase)) : prod[ee - pbase];
+                s[u] = __builtin_nontemporal_load(slot2 + ee);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                // masked lanes (past the bin) add +0.0 to the dummy slot
+                const bool ok = base + u * 64 + lane < p1;
+                if (MODE & 2) sink += v[u] * (double)s[u];
+                else atomicAdd(&ys[ok ? s[u] : SLICE - 1], ok ? v[u] : 0.0);
+            }
+        }
+        if ((MODE & 2) && sink == 1.2345e300) ys[0] = sink;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        for (int i = lane; i < rows; i += 64) y[r0 + i] = ys[i];
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    }
+}
+
+template <int SHIFT, int MODE, int PL>
+static void launch_mul_t(const spmv_plan_s *p, int g, const double *x) {
+    const BinDev &B = p->bin;
+    hipLaunchKernelGGL((bin_mul_kernel<SHIFT, 8, MODE, PL>), dim3((unsigned)B.nwg1), dim3(kBinMulThreads), 0,
+                       p->stream, B.piece_off, (int64_t)g * B.nwg1, B.piece_strip, B.piece_begin, B.piece_end,
+                       B.val1, B.cs1, B.dst1, x, p->n, B.prod);
+}
+
+template <int SHIFT, int PL>
+static void launch_mul_p(const spmv_plan_s *p, int g, const double *x) {
+    // SPMV_BIN_DEBUG bits 0-1 -> Mul MODE; default: nontemporal stores
+    // (measured 0.81 -> 0.71 ms at config 2, profiles/round1/probe/bin_probe_c2.jsonl)
+    switch (p->bin.dbg & 3) {
+        case 1: launch_mul_t<SHIFT, 0, PL>(p, g, x); break;
+        case 2: launch_mul_t<SHIFT, 2, PL>(p, g, x); break;
+        default: launch_mul_t<SHIFT, 1, PL>(p, g, x);
+    }
+}
+
+template <int SHIFT>
+static void launch_mul(const spmv_plan_s *p, int g, const double *x) {
+    if (p->bin.pad_log == 5) launch_mul_p<SHIFT, 5>(p, g, x);
+    else if (p->bin.pad_log == 4) launch_mul_p<SHIFT, 4>(p, g, x);
+    else launch_mul_p<SHIFT, 3>(p, g, x);
+}
+
+// Sum over the bins of group g (g < 0: every bin, product buffer = all products)
+template <int W2, int U, int MODE>
+static void launch_sum_t(const spmv_plan_s *p, int g, double *y) {
+    const BinDev &B = p->bin;
+    const int64_t b0 = g < 0 ? 0 : B.g_bin[g], b1 = g < 0 ? B.n_bins : B.g_bin[g + 1];
+    const int64_t pbase = g < 0 ? 0 : B.g_prod[g];
+    hipLaunchKernelGGL((bin_sum_kernel<W2, U, MODE>), dim3((unsigned)B.nwg2), dim3(64 * W2), 0, p->stream,
+                       b0, b1, B.bin_off, B.bin_row0, pbase, B.slot2, B.prod, y);
+}
+
+template <int W2, int U>
+static void launch_sum_w(const spmv_plan_s *p, int g, double *y) {
+    // SPMV_BIN_DEBUG bits 2-3 -> Sum MODE
+    switch ((p->bin.dbg >> 2) & 3) {
+        case 1: launch_sum_t<W2, U, 1>(p, g, y); break;
+        case 2: launch_sum_t<W2, U, 2>(p, g, y); break;
+        default: launch_sum_t<W2, U, 0>(p, g, y);
+    }
+}
+
+int launch_bin(const spmv_plan_s *p, const double *x, double *y) {
+    const BinDev &B = p->bin;
+    if (p->m == 0) return SPMV_SUCCESS;
+    if (p->nnz == 0) {  // no entries: y = 0 (and x may be empty)
+        SPMV_HIP_TRY(hipMemsetAsync(y, 0, sizeof(double) * (size_t)p->m, p->stream));
+        return SPMV_SUCCESS;
+    }
+    auto sum = [&](int g) {
+        if (B.sum_waves == 2) launch_sum_w<2, 64>(p, g, y);
+        else if (B.sum_waves == 4) launch_sum_w<4, 32>(p, g, y);
+        else launch_sum_w<8, 16>(p, g, y);
+    };
+    // Mul per row group (all groups' writes go to one product buffer unless
+    // it is re-used per group), then Sum
+    for (int g = 0; g < B.G; ++g) {
+        if (B.strip_shift == 13) launch_mul<13>(p, g, x);
+        else launch_mul<14>(p, g, x);
+        SPMV_HIP_TRY(hipGetLastError());
+        if (B.reuse) {
+            phase_mark(p);  // mul | sum
+            sum(g);
+            SPMV_HIP_TRY(hipGetLastError());
+            if (g + 1 < B.G) phase_mark(p);
+        }
+    }
+    if (!B.reuse) {
+        phase_mark(p);  // mul | sum
+        sum(-1);
+        SPMV_HIP_TRY(hipGetLastError());
+    }
+    return SPMV_SUCCESS;
+}
+
+}  // namespace spmv

@@ -29,6 +29,8 @@ static int opt_hip_format() {
     f = SPMV_FORMAT_COO;
 #elif defined(OPT_HIP_JDS)
     f = SPMV_FORMAT_JDS;
+#elif defined(OPT_HIP_BIN)
+    f = SPMV_FORMAT_BIN;
 #endif
     const char *e = std::getenv("SPMV_HIP_FORMAT");
     if (e && *e) {
@@ -40,6 +42,7 @@ static int opt_hip_format() {
         else if (!strcasecmp(e, "css")) f = SPMV_FORMAT_CSS;
         else if (!strcasecmp(e, "coo")) f = SPMV_FORMAT_COO;
         else if (!strcasecmp(e, "jds")) f = SPMV_FORMAT_JDS;
+        else if (!strcasecmp(e, "bin")) f = SPMV_FORMAT_BIN;
         else f = SPMV_FORMAT_AUTO;
     }
     return f;

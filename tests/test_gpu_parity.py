@@ -22,7 +22,7 @@ from conftest import golden_names, load_golden
 
 pytestmark = pytest.mark.gpu
 
-FORMATS = ["csr", "ell", "ss", "hyb", "dia", "css", "coo", "jds", "auto"]
+FORMATS = ["csr", "ell", "ss", "hyb", "dia", "css", "coo", "jds", "bin", "auto"]
 REL = 1e-12
 
 
@@ -83,7 +83,7 @@ def test_golden(name, fmt):
     info = plan.info()
     sequential = info["format"] in ("ell", "dia") or (info["format"] == "csr" and info["csr_lanes"] == 1) \
         or (info["format"] == "jds" and info["overflow_nnz"] == 0) \
-        or (info["format"] == "css" and info["css_split_rows"] == 0)
+        or (info["format"] == "css" and info["css_split_rows"] == 0) or info["format"] == "bin"
     if sequential:
         assert np.array_equal(y, yref), f"{info['format']} is sequential: must be bit-exact"
 
@@ -466,9 +466,11 @@ def test_csr_64bit_row_pointers(monkeypatch, lanes):
 
 def test_auto_format_choice():
     """AUTO follows the measured crossovers (profiles/round1/probe/
-    auto_sweep.jsonl): banded -> DIA; x beyond ~6 MB -> CSS; below that,
+    auto_sweep.jsonl, bin_vs_css_sizes.jsonl): banded -> DIA; >= 3.5 M
+    columns and 20 M entries -> BIN; x beyond ~6 MB -> CSS; below that,
     near-uniform rows -> CSR, skewed rows -> SS."""
     cases = [(sp.gen_spec("banded", 300000, band_lo=-8, band_hi=8), "dia"),
+             (sp.gen_spec("uniform", 4_000_000, per_row=6, seed=6), "bin"),
              (sp.gen_spec("uniform", 1_000_000, per_row=8, seed=1), "css"),
              (sp.gen_spec("powerlaw", 1_000_000, max_len=500, seed=2), "css"),
              (sp.gen_spec("uniform", 400_000, per_row=8, seed=3), "csr"),
@@ -481,3 +483,81 @@ def test_auto_format_choice():
         if m <= 400_000:
             x = sp.generate_vector(m, seed=5)
             check_close(run_plan(plan, x, m), oracle_y(rp, col, val, x), what=f"auto {want}")
+
+
+# ---------------------------------------------------------------- BIN
+def _bin_matrix(kind, m, n, seed):
+    if kind == "empty_rows":
+        spec = sp.gen_spec("powerlaw", m, n, max_len=700, seed=seed)
+        rp, col, val = sp.generate_csr(spec)
+        rng = np.random.default_rng(seed)
+        lens = np.diff(rp)
+        zero = rng.random(m) < 0.2
+        zero[:11] = True
+        zero[-13:] = True
+        keep = np.repeat(~zero, lens)
+        col, val = np.ascontiguousarray(col[keep]), np.ascontiguousarray(val[keep])
+        rp = np.concatenate([[0], np.cumsum(np.where(zero, 0, lens))]).astype(np.int64)
+        return rp, col, val
+    spec = sp.gen_spec(kind, m, n, per_row=11, max_len=5000, seed=seed)
+    return sp.generate_csr(spec)
+
+
+@pytest.mark.parametrize("shape", [(40_000, 40_000), (30_011, 100_003), (70_001, 9_000), (5, 3), (1, 70_000)])
+@pytest.mark.parametrize("kind", ["uniform", "powerlaw", "empty_rows"])
+@pytest.mark.parametrize("opts", [{}, {"bin_strip_shift": 13}, {"bin_groups": 3}])
+def test_bin_bit_exact(shape, kind, opts):
+    """BIN (binned Mul/Sum): every row is the sequential opt_crs sum bit for
+    bit (one wave per bin adds its products in column order), for partial
+    strips, rectangular shapes, empty rows, long rows and row groups."""
+    m, n = shape
+    rp, col, val = _bin_matrix(kind, m, n, seed=m % 97 + len(opts))
+    x = sp.generate_vector(n, seed=31)
+    plan = sp.Plan.from_csr(m, n, rp, col, val, "bin", **opts)
+    y = run_plan(plan, x, m)
+    assert np.array_equal(y, oracle_y(rp, col, val, x)), f"bin {shape} {kind} {opts}"
+
+
+@pytest.mark.parametrize("env", [{"SPMV_BIN_PADLOG": "3"}, {"SPMV_BIN_PADLOG": "5"}, {"SPMV_BIN_SUMWAVES": "2"},
+                                 {"SPMV_BIN_SUMWAVES": "8"}, {"SPMV_BIN_REUSE": "1"},
+                                 {"SPMV_BIN_DEBUG": "1"}])
+def test_bin_layout_knobs(env, monkeypatch):
+    """The internal layout knobs (product-line padding, Sum waves / bin rows,
+    a product buffer re-used per row group, plain stores) change speed only."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    m = 120_000
+    rp, col, val = _bin_matrix("powerlaw", m, m, seed=41)
+    x = sp.generate_vector(m, seed=43)
+    plan = sp.Plan.from_csr(m, m, rp, col, val, "bin", bin_groups=2)
+    assert np.array_equal(run_plan(plan, x, m), oracle_y(rp, col, val, x)), env
+
+
+def test_bin_edge_cases():
+    """No entries (y = 0), a single column, signed values (VerifyResult), the
+    Mul/Sum profile split, and the option check."""
+    m = 5000
+    rp0 = np.zeros(m + 1, np.int64)
+    plan = sp.Plan.from_csr(m, 10, rp0, np.zeros(0, np.int32), np.zeros(0), "bin")
+    y = run_plan(plan, np.ones(10), m)
+    assert not y.any()
+    rp = np.arange(m + 1, dtype=np.int64)
+    col = np.zeros(m, np.int32)
+    val = np.linspace(-1.0, 1.0, m)
+    plan = sp.Plan.from_csr(m, 1, rp, col, val, "bin")
+    assert np.array_equal(run_plan(plan, np.array([3.0]), m), val * 3.0)
+    rng = np.random.default_rng(7)
+    spec = sp.gen_spec("uniform", 50_000, per_row=9, seed=3)
+    rp, col, val = sp.generate_csr(spec)
+    val = val * np.where(rng.random(len(val)) < 0.5, -1.0, 1.0)
+    x = sp.generate_vector(50_000, seed=9) - 0.5
+    plan = sp.Plan.from_csr(50_000, 50_000, rp, col, val, "bin")
+    y = run_plan(plan, x, 50_000)
+    assert np.array_equal(y, oracle_y(rp, col, val, x))
+    import torch
+    xd = torch.from_numpy(x).cuda()
+    yd = torch.empty(50_000, dtype=torch.float64, device="cuda")
+    ph = plan.profile(xd, yd, 3)
+    assert list(ph) == ["mul", "sum"], ph
+    with pytest.raises(sp.SpmvError):
+        sp.Plan.from_csr(50_000, 50_000, rp, col, val, "bin", bin_strip_shift=12)

@@ -58,8 +58,22 @@ def main(src, tag, config_key_prefix):
     for k, s in summary.items():
         short = k.split("(")[0].replace("void ", "").replace("spmv::", "")
         for kern, algo in stream_bytes.items():
-            if kern.split("<")[0] in short:
+            if "+" not in kern and kern.split("<")[0] in short:
                 traffic[f"{config_key_prefix}:{kern}"] = s["traffic_raw"]
+    # multi-kernel formats ("a+b", e.g. BIN's Mul + Sum): bytes of one
+    # execute = the sum of each kernel's mean bytes per launch
+    for kern in stream_bytes:
+        if "+" in kern:
+            parts = kern.split("+")
+            tot, found = 0.0, 0
+            for part in parts:
+                for k, s in summary.items():
+                    if part in k.split("(")[0]:
+                        tot += s["traffic_raw"]
+                        found += 1
+                        break
+            if found == len(parts):
+                traffic[f"{config_key_prefix}:{kern}"] = tot
     json.dump(traffic, open(tfile, "w"), indent=1, sort_keys=True)
     print(json.dumps(summary, indent=1))
 

@@ -8,7 +8,7 @@
 // with GPU additions: AchievedGB/s against the plan's algorithmic bytes and
 // the MI355X 8 TB/s HBM roofline.
 //
-// Usage: spmv <matrix.mtx> [--format crs|ell|ss|dia|hyb|css|coo|jds|auto] [--resident]
+// Usage: spmv <matrix.mtx> [--format crs|ell|ss|dia|hyb|css|coo|jds|bin|auto] [--resident]
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -20,7 +20,7 @@
 int main(int argc, char **argv) {
     srand(3);  // src/main.cpp:18
     if (argc < 2) {
-        std::printf("Usage: %s <matrix> [--format crs|ell|ss|dia|hyb|css|coo|jds|auto] [--resident]\n", argv[0]);
+        std::printf("Usage: %s <matrix> [--format crs|ell|ss|dia|hyb|css|coo|jds|bin|auto] [--resident]\n", argv[0]);
         return 1;
     }
     const std::string matFile = argv[1];
@@ -68,7 +68,7 @@ int main(int argc, char **argv) {
 
     spmv_plan_info_t info;
     spmv_plan_info(A_opt.plan, &info);
-    static const char *names[] = {"AUTO", "CRS", "ELL", "SS", "DIA", "HYB", "CSS", "COO", "JDS"};
+    static const char *names[] = {"AUTO", "CRS", "ELL", "SS", "DIA", "HYB", "CSS", "COO", "JDS", "BIN"};
     const double gflops = (double)A.nNnz * 2.0 / best / 1e9;
     const double gbs = (double)info.algo_bytes / best / 1e9;
     std::printf("++++++++++++++++++++++++++++++++++++++++\n");

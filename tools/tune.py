@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--grid", default="")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--check", action="store_true", help="max rel err (and bit-equality) vs the oracle")
     a = ap.parse_args()
     import torch
     import singlespmv_amd as sp
@@ -53,8 +54,20 @@ def main():
         for i, (kw, p, _) in enumerate(plans):
             p.time(x, y, 3)
             res[i].append(p.time(x, y, a.iters) / a.iters)
+    yref = None
+    if a.check:
+        import numpy as np
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        import oracle
+        yref = oracle.csr_spmv(rp, col, val, x.cpu().numpy())
     for i, (kw, p, tb) in enumerate(plans):
         ms = min(res[i])
+        if yref is not None:
+            y.fill_(float("nan"))
+            p.execute(x, y)
+            yg = y.cpu().numpy()
+            kw = dict(kw, max_rel=float(np.max(np.abs(yg - yref) / np.maximum(np.abs(yref), 1e-300))),
+                      bit_exact=bool(np.array_equal(yg, yref)))
         print(json.dumps({"fmt": a.fmt, **kw, "ms": round(ms, 4), "median_ms": round(sorted(res[i])[len(res[i]) // 2], 4),
                           "gflops": round(2 * nnz / ms / 1e6, 1), "build_s": round(tb, 2),
                           "info": {k: v for k, v in p.info().items() if k in ("css_passes", "css_slabs", "kernel")}}),
