@@ -35,6 +35,13 @@ int build_bin(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
     const int64_t C = (int64_t)1 << shift;
     B.nwg1 = ncu * (shift == 13 ? 2 : 1);  // one (two) 1024-thread workgroups per CU
     B.nwg2 = ncu;                           // 160 KB of LDS y slices per workgroup
+    if (const char *e = std::getenv("SPMV_BIN_CUS")) {  // experiment: a subset of the CUs
+        const int k = std::atoi(e);
+        if (k > 0 && k < ncu) {
+            B.nwg1 = k * (shift == 13 ? 2 : 1);
+            B.nwg2 = k;
+        }
+    }
     // internal tuning knobs; defaults measured at config 2
     // (profiles/round1/probe/bin_probe_c2.jsonl): 16-entry (128-B) product
     // lines and 4 Sum waves (5119-row bins, ~1 KB segments) took Mul from
@@ -221,18 +228,17 @@ int build_bin(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
     B.prod_cap = B.reuse ? 0 : E;
     if (B.reuse)
         for (int g = 0; g < G; ++g) B.prod_cap = std::max(B.prod_cap, B.g_prod[(size_t)g + 1] - B.g_prod[(size_t)g]);
+    const size_t prod_bytes = sizeof(double) * (size_t)std::max<int64_t>(B.prod_cap, 1);
     auto alloc_prod = [&]() -> int {
+        // plain hipMalloc.  (hipDeviceMallocContiguous was tried for the
+        // product buffer: plans built after another plan was freed returned
+        // WRONG sums -- the buffer behaved as if aliased -- so it is not used;
+        // tools/dbg_bin.py reproduces it.)
         void *q = nullptr;
-        const size_t bytes = sizeof(double) * (size_t)std::max<int64_t>(B.prod_cap, 1);
-        // physically contiguous product buffer: the Mul writes scatter 1-KB
-        // segments over all of it; measured 0.96 ms steady vs 0.95-0.99 ms
-        // depending on placement (profiles/round1/probe/bin_placement.jsonl)
-        if ((B.dbg & 64) || p->arena.alloc_flags(&q, bytes, hipDeviceMallocContiguous) != SPMV_SUCCESS)
-            SPMV_RETURN_IF(p->arena.alloc(&q, bytes));
+        SPMV_RETURN_IF(p->arena.alloc(&q, prod_bytes));
         B.prod = (double *)q;
         return SPMV_SUCCESS;
     };
-    if (B.dbg & 32) SPMV_RETURN_IF(alloc_prod());
     SPMV_RETURN_IF(upload_vec(p, &B.piece_off, piece_off));
     SPMV_RETURN_IF(upload_vec(p, &B.piece_strip, pstrip));
     SPMV_RETURN_IF(upload_vec(p, &B.piece_begin, pbeg));
@@ -243,10 +249,46 @@ int build_bin(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
     SPMV_RETURN_IF(upload_vec(p, &B.slot2, slot2));
     SPMV_RETURN_IF(upload_vec(p, &B.bin_off, bin_off));
     SPMV_RETURN_IF(upload_vec(p, &B.bin_row0, row0));
-    if (!(B.dbg & 32)) SPMV_RETURN_IF(alloc_prod());
-    if (B.dbg & 16)
-        std::fprintf(stderr, "[bin] val1 %p cs1 %p dst1 %p slot2 %p prod %p (E %lld)\n", (void *)B.val1, (void *)B.cs1,
-                     (void *)B.dst1, (void *)B.slot2, (void *)B.prod, (long long)E);
+    // Product-buffer placement.  The Mul writes 1-KB segments scattered over
+    // the whole buffer; with some allocations of the same size it runs ~15 %
+    // slower (config 2: 0.66 vs 0.56 ms for ONE plan whose buffer was
+    // re-allocated between timings, profiles/round1/probe/bin_realloc.jsonl).
+    // For large buffers keep the fastest of K candidates, each timed with a
+    // Mul pass over a zero x at build time (results never depend on it).
+    int K = prod_bytes >= ((size_t)256 << 20) ? 3 : 1;
+    if (const char *e = std::getenv("SPMV_BIN_PLACEMENT")) K = std::max(1, std::min(8, std::atoi(e)));
+    if (K == 1) {
+        SPMV_RETURN_IF(alloc_prod());
+    } else {
+        double *xz = nullptr;
+        SPMV_HIP_TRY(hipMalloc(&xz, sizeof(double) * (size_t)std::max<int64_t>(A.n, 1)));
+        SPMV_HIP_TRY(hipMemset(xz, 0, sizeof(double) * (size_t)std::max<int64_t>(A.n, 1)));
+        std::vector<double *> cand;
+        std::vector<float> t;
+        int st = SPMV_SUCCESS;
+        for (int k = 0; k < K && st == SPMV_SUCCESS; ++k) {
+            st = alloc_prod();
+            if (st != SPMV_SUCCESS) break;
+            float ms = 0;
+            st = bin_time_mul(p, xz, &ms);
+            cand.push_back(B.prod);
+            t.push_back(ms);
+        }
+        (void)hipFree(xz);
+        if (cand.empty()) return st;
+        (void)hipGetLastError();
+        const size_t best = (size_t)(std::min_element(t.begin(), t.end()) - t.begin());
+        for (size_t k = 0; k < cand.size(); ++k)
+            if (k != best) p->arena.free(cand[k]);
+        B.prod = cand[best];
+        B.placement_ms.assign(t.begin(), t.end());
+    }
+    if (B.dbg & 16) {
+        std::fprintf(stderr, "[bin] val1 %p cs1 %p dst1 %p slot2 %p prod %p (E %lld) placement ms:", (void *)B.val1,
+                     (void *)B.cs1, (void *)B.dst1, (void *)B.slot2, (void *)B.prod, (long long)E);
+        for (float t : B.placement_ms) std::fprintf(stderr, " %.4f", t);
+        std::fprintf(stderr, "\n");
+    }
     p->stored_slots = E;
     p->n_kernels = B.reuse ? 2 * G : G + 1;
     return SPMV_SUCCESS;

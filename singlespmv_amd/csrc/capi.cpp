@@ -442,6 +442,16 @@ int spmv_css_layout(spmv_plan_t p, int64_t *bstart, int64_t *woff) {
     return 0;
 }
 
+// internal (experiment): give the BIN product buffer a fresh allocation (the
+// old one is kept until the plan is destroyed, so the new one lands elsewhere)
+int spmv_bin_realloc_prod(spmv_plan_t p) {
+    if (!p || p->format != SPMV_FORMAT_BIN || !p->bin.prod) return -1;
+    void *q = nullptr;
+    if (p->arena.alloc(&q, sizeof(double) * (size_t)std::max<int64_t>(p->bin.prod_cap, 1)) != SPMV_SUCCESS) return -1;
+    p->bin.prod = (double *)q;
+    return 0;
+}
+
 int spmv_plan_info(spmv_plan_t p, spmv_plan_info_t *info) {
     SPMV_CHECK_ARG(p != nullptr && info != nullptr, "NULL argument");
     std::memset(info, 0, sizeof(*info));

@@ -31,19 +31,16 @@ int DevArena::alloc(void **p, size_t n) {
     return SPMV_SUCCESS;
 }
 
-int DevArena::alloc_flags(void **p, size_t n, unsigned flags) {
-    if (n == 0) n = 16;
-    void *q = nullptr;
-    hipError_t e = hipExtMallocWithFlags(&q, n, flags);
-    if (e != hipSuccess) {
-        set_error(std::string("hipExtMallocWithFlags(") + std::to_string(n) + "): " + hipGetErrorString(e));
-        (void)hipGetLastError();
-        return e == hipErrorOutOfMemory ? SPMV_ERROR_OUT_OF_MEMORY : SPMV_ERROR_HIP;
-    }
-    ptrs.push_back(q);
-    bytes += (int64_t)n;
-    *p = q;
-    return SPMV_SUCCESS;
+void DevArena::free(void *p) {
+    for (size_t i = 0; i < ptrs.size(); ++i)
+        if (ptrs[i] == p) {
+            size_t n = 0;
+            (void)hipMemPtrGetInfo(p, &n);
+            (void)hipFree(p);
+            bytes -= (int64_t)n;
+            ptrs.erase(ptrs.begin() + (long)i);
+            return;
+        }
 }
 
 void DevArena::release() {

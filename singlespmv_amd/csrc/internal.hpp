@@ -47,7 +47,7 @@ struct DevArena {
     std::vector<void *> ptrs;
     int64_t bytes = 0;
     int alloc(void **p, size_t n);  // hipMalloc, zero-size safe
-    int alloc_flags(void **p, size_t n, unsigned flags);  // hipExtMallocWithFlags
+    void free(void *p);             // hipFree one allocation of this arena
     void release();
 };
 
@@ -216,6 +216,7 @@ struct BinDev {
     double *prod = nullptr;       // product buffer (largest group)
     int64_t prod_cap = 0;
     int dbg = 0;  // SPMV_BIN_DEBUG (internal)
+    std::vector<float> placement_ms;  // Mul ms of each product-buffer candidate
 };
 
 }  // namespace spmv
@@ -296,5 +297,6 @@ int launch_dia(const spmv_plan_s *p, const double *x, double *y);
 int launch_css(const spmv_plan_s *p, const double *x, double *y);
 int launch_coo(const spmv_plan_s *p, const double *x, double *y);
 int launch_bin(const spmv_plan_s *p, const double *x, double *y);
+int bin_time_mul(const spmv_plan_s *p, const double *x, float *ms);  // one timed Mul pass (build-time)
 
 }  // namespace spmv

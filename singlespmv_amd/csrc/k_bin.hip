@@ -37,6 +37,52 @@
 
 namespace spmv {
 
+// One batch of U entries per lane (entry base + u*64 + lane), loaded ahead
+// of its use: the kernels ping-pong two batches so a wave always has one
+// batch of loads in flight while it consumes the other (the single-batch
+// loop drained the memory pipe every iteration: BIN lost 25 % on 160 CUs
+// instead of 256, profiles/round1/probe/bin_cus.jsonl).
+template <int U>
+struct MulBatch {
+    double v[U];
+    uint32_t c[U];
+    int32_t d[U];
+};
+
+template <int U, int PL>
+__device__ __forceinline__ void mul_load(MulBatch<U> &B, int64_t base, int64_t e0, int64_t e1, int lane,
+                                         const double *__restrict__ val1, const uint16_t *__restrict__ cs1,
+                                         const int32_t *__restrict__ dst1) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int64_t e = base + u * 64 + lane;
+        const int64_t ee = e < e1 ? e : e0;
+        B.v[u] = ld_stream(val1 + ee);
+        B.c[u] = __builtin_nontemporal_load(cs1 + ee);
+        B.d[u] = ld_stream(dst1 + (ee >> PL));
+    }
+}
+
+template <int U, int MODE, int PL>
+__device__ __forceinline__ void mul_store(const MulBatch<U> &B, int64_t base, int64_t e1, int lane,
+                                          const double *xs, double *__restrict__ prod) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int64_t e = base + u * 64 + lane;
+        if (e < e1) {
+            const double pr = __dmul_rn(B.v[u], xs[B.c[u]]);
+            double *dp = prod + ((int64_t)B.d[u] << PL) + (e & ((1 << PL) - 1));
+            if (MODE & 2) {
+                if (pr == 1.2345e300) *dp = pr;
+            } else if (MODE & 1) {
+                __builtin_nontemporal_store(pr, dp);
+            } else {
+                *dp = pr;
+            }
+        }
+    }
+}
+
 // MODE (SPMV_BIN_DEBUG, internal ablations): 1 nontemporal product stores,
 // 2 no product stores (value kept alive).  PL: segments padded to 2^PL entries.
 template <int SHIFT, int U, int MODE, int PL>
@@ -47,6 +93,7 @@ __global__ __launch_bounds__(kBinMulThreads) void bin_mul_kernel(
     const double *__restrict__ x, int64_t n, double *__restrict__ prod) {
     __shared__ double xs[1 << SHIFT];
     constexpr int NW = kBinMulThreads / 64;
+    constexpr int64_t STEP = (int64_t)NW * 64 * U;
     const int w = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
     const int64_t q0 = piece_off[q_base + blockIdx.x], q1 = piece_off[q_base + blockIdx.x + 1];
@@ -58,34 +105,50 @@ __global__ __launch_bounds__(kBinMulThreads) void bin_mul_kernel(
         __syncthreads();  // the previous strip's readers are done
         for (int i = threadIdx.x; i < cw; i += kBinMulThreads) xs[i] = x[c0 + i];
         __syncthreads();
-        for (int64_t base = e0 + (int64_t)w * 64 * U; base < e1; base += (int64_t)NW * 64 * U) {
-            double v[U];
-            uint32_t c[U];
-            int32_t d[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int64_t e = base + u * 64 + lane;
-                const int64_t ee = e < e1 ? e : e0;
-                v[u] = ld_stream(val1 + ee);
-                c[u] = __builtin_nontemporal_load(cs1 + ee);
-                d[u] = ld_stream(dst1 + (ee >> PL));
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int64_t e = base + u * 64 + lane;
-                if (e < e1) {
-                    const double pr = __dmul_rn(v[u], xs[c[u]]);
-                    double *dp = prod + ((int64_t)d[u] << PL) + (e & ((1 << PL) - 1));
-                    if (MODE & 2) {
-                        if (pr == 1.2345e300) *dp = pr;
-                    } else if (MODE & 1) {
-                        __builtin_nontemporal_store(pr, dp);
-                    } else {
-                        *dp = pr;
-                    }
-                }
+        const int64_t first = e0 + (int64_t)w * 64 * U;
+        const int64_t nit = first < e1 ? (e1 - first + STEP - 1) / STEP : 0;
+        MulBatch<U> A, B;
+        if (nit > 0) mul_load<U, PL>(A, first, e0, e1, lane, val1, cs1, dst1);
+        for (int64_t it = 0; it < nit; it += 2) {
+            const int64_t ba = first + it * STEP, bb = ba + STEP;
+            if (it + 1 < nit) mul_load<U, PL>(B, bb, e0, e1, lane, val1, cs1, dst1);
+            mul_store<U, MODE, PL>(A, ba, e1, lane, xs, prod);
+            if (it + 1 < nit) {
+                if (it + 2 < nit) mul_load<U, PL>(A, bb + STEP, e0, e1, lane, val1, cs1, dst1);
+                mul_store<U, MODE, PL>(B, bb, e1, lane, xs, prod);
             }
         }
+    }
+}
+
+template <int U, int MODE>
+struct SumBatch {
+    double v[U];
+    uint32_t s[U];
+};
+
+template <int U, int MODE>
+__device__ __forceinline__ void sum_load(SumBatch<U, MODE> &B, int64_t base, int64_t p0, int64_t p1, int lane,
+                                         int64_t pbase, const uint16_t *__restrict__ slot2,
+                                         const double *__restrict__ prod) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int64_t e = base + u * 64 + lane;
+        const int64_t ee = e < p1 ? e : p0;
+        B.v[u] = (MODE & 1) ? ld_stream(prod + (ee - pbase)) : prod[ee - pbase];
+        B.s[u] = __builtin_nontemporal_load(slot2 + ee);
+    }
+}
+
+template <int U, int MODE, int DUMMY>
+__device__ __forceinline__ void sum_add(const SumBatch<U, MODE> &B, int64_t base, int64_t p1, int lane, double *ys,
+                                        double &sink) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        // masked lanes (past the bin) add +0.0 to the dummy slot
+        const bool ok = base + u * 64 + lane < p1;
+        if (MODE & 2) sink += B.v[u] * (double)B.s[u];
+        else atomicAdd(&ys[ok ? B.s[u] : DUMMY], ok ? B.v[u] : 0.0);
     }
 }
 
@@ -96,6 +159,7 @@ __global__ __launch_bounds__(64 * W2) void bin_sum_kernel(
     int64_t b0, int64_t b1, const int64_t *__restrict__ bin_off, const int32_t *__restrict__ bin_row0,
     int64_t pbase, const uint16_t *__restrict__ slot2, const double *__restrict__ prod, double *__restrict__ y) {
     constexpr int SLICE = kBinLdsDoubles / W2;
+    constexpr int64_t STEP = 64 * U;
     __shared__ double ylds[kBinLdsDoubles];
     const int w = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
@@ -105,23 +169,17 @@ __global__ __launch_bounds__(64 * W2) void bin_sum_kernel(
         const int rows = (int)(bin_row0[b + 1] - r0);
         for (int i = lane; i < rows; i += 64) ys[i] = 0.0;
         const int64_t p0 = bin_off[b], p1 = bin_off[b + 1];
+        const int64_t nit = (p1 - p0 + STEP - 1) / STEP;
         double sink = 0.0;
-        for (int64_t base = p0; base < p1; base += 64 * U) {
-            double v[U];
-            uint32_t s[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int64_t e = base + u * 64 + lane;
-                const int64_t ee = e < p1 ? e : p0;
-                v[u] = (MODE & 1) ? ld_stream(prod + (ee - pbase)) : prod[ee - pbase];
-                s[u] = __builtin_nontemporal_load(slot2 + ee);
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                // masked lanes (past the bin) add +0.0 to the dummy slot
-                const bool ok = base + u * 64 + lane < p1;
-                if (MODE & 2) sink += v[u] * (double)s[u];
-                else atomicAdd(&ys[ok ? s[u] : SLICE - 1], ok ? v[u] : 0.0);
+        SumBatch<U, MODE> A, B;
+        if (nit > 0) sum_load<U, MODE>(A, p0, p0, p1, lane, pbase, slot2, prod);
+        for (int64_t it = 0; it < nit; it += 2) {
+            const int64_t ba = p0 + it * STEP, bb = ba + STEP;
+            if (it + 1 < nit) sum_load<U, MODE>(B, bb, p0, p1, lane, pbase, slot2, prod);
+            sum_add<U, MODE, SLICE - 1>(A, ba, p1, lane, ys, sink);
+            if (it + 1 < nit) {
+                if (it + 2 < nit) sum_load<U, MODE>(A, bb + STEP, p0, p1, lane, pbase, slot2, prod);
+                sum_add<U, MODE, SLICE - 1>(B, bb, p1, lane, ys, sink);
             }
         }
         if ((MODE & 2) && sink == 1.2345e300) ys[0] = sink;
@@ -177,6 +235,26 @@ static void launch_sum_w(const spmv_plan_s *p, int g, double *y) {
     }
 }
 
+int bin_time_mul(const spmv_plan_s *p, const double *x, float *ms) {
+    const BinDev &B = p->bin;
+    hipEvent_t a, b;
+    SPMV_HIP_TRY(hipEventCreate(&a));
+    SPMV_HIP_TRY(hipEventCreate(&b));
+    for (int rep = 0; rep < 2; ++rep) {  // the second pass is timed
+        if (rep == 1) SPMV_HIP_TRY(hipEventRecord(a, p->stream));
+        for (int g = 0; g < B.G; ++g) {
+            if (B.strip_shift == 13) launch_mul<13>(p, g, x);
+            else launch_mul<14>(p, g, x);
+        }
+    }
+    SPMV_HIP_TRY(hipEventRecord(b, p->stream));
+    SPMV_HIP_TRY(hipEventSynchronize(b));
+    SPMV_HIP_TRY(hipEventElapsedTime(ms, a, b));
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    return SPMV_SUCCESS;
+}
+
 int launch_bin(const spmv_plan_s *p, const double *x, double *y) {
     const BinDev &B = p->bin;
     if (p->m == 0) return SPMV_SUCCESS;
@@ -185,9 +263,9 @@ int launch_bin(const spmv_plan_s *p, const double *x, double *y) {
         return SPMV_SUCCESS;
     }
     auto sum = [&](int g) {
-        if (B.sum_waves == 2) launch_sum_w<2, 64>(p, g, y);
-        else if (B.sum_waves == 4) launch_sum_w<4, 32>(p, g, y);
-        else launch_sum_w<8, 16>(p, g, y);
+        if (B.sum_waves == 2) launch_sum_w<2, 32>(p, g, y);
+        else if (B.sum_waves == 4) launch_sum_w<4, 16>(p, g, y);
+        else launch_sum_w<8, 8>(p, g, y);
     };
     // Mul per row group (all groups' writes go to one product buffer unless
     // it is re-used per group), then Sum

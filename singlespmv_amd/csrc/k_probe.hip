@@ -36,6 +36,18 @@ __global__ void gather_idx_kernel(int32_t *__restrict__ idx, int64_t n, int64_t 
         idx[i] = (int32_t)(mix64((uint64_t)i) % (uint64_t)tab_elems);
 }
 
+// the same read, one 16-byte load per thread per step (the faster shape on
+// some boxes: tools/mall_probe.hip e1 read 2 GB at 6.8 TB/s this way)
+__global__ __launch_bounds__(256) void stream_read1_kernel(const f64x2 *__restrict__ a, int64_t n2,
+                                                           double *__restrict__ sink) {
+    double acc = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n2; i += (int64_t)gridDim.x * blockDim.x) {
+        const f64x2 v = __builtin_nontemporal_load(a + i);
+        acc += v.x + v.y;
+    }
+    if (acc == 1.2345) sink[0] = acc;
+}
+
 // streamed 4-byte indices, 8-byte gathers, 8 in flight per lane
 __global__ __launch_bounds__(256) void gather_rate_kernel(const int32_t *__restrict__ idx, const double *__restrict__ tab,
                                                           int64_t n, double *__restrict__ sink) {
@@ -139,13 +151,24 @@ extern "C" int spmv_stream_probe(int32_t device, int64_t bytes, int32_t iters, d
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
     const unsigned blocks = 256 * 16;
-    hipLaunchKernelGGL(stream_read_kernel, dim3(blocks), dim3(256), 0, 0, a, n2, sink);  // warm-up
-    (void)hipEventRecord(e0, 0);
-    for (int i = 0; i < iters; ++i) hipLaunchKernelGGL(stream_read_kernel, dim3(blocks), dim3(256), 0, 0, a, n2, sink);
-    (void)hipEventRecord(e1, 0);
-    hipError_t e = hipEventSynchronize(e1);
+    // the ceiling is the faster of two read shapes (4 strided loads in flight
+    // per thread / one contiguous load per thread)
     float ms = 0;
-    (void)hipEventElapsedTime(&ms, e0, e1);
+    hipError_t e = hipSuccess;
+    for (int shape = 0; shape < 2 && e == hipSuccess; ++shape) {
+        auto launch = [&]() {
+            if (shape == 0) hipLaunchKernelGGL(stream_read_kernel, dim3(blocks), dim3(256), 0, 0, a, n2, sink);
+            else hipLaunchKernelGGL(stream_read1_kernel, dim3(blocks), dim3(256), 0, 0, a, n2, sink);
+        };
+        launch();  // warm-up
+        (void)hipEventRecord(e0, 0);
+        for (int i = 0; i < iters; ++i) launch();
+        (void)hipEventRecord(e1, 0);
+        e = hipEventSynchronize(e1);
+        float t = 0;
+        (void)hipEventElapsedTime(&t, e0, e1);
+        if (shape == 0 || t < ms) ms = t;
+    }
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     (void)hipFree(a);
