@@ -41,6 +41,18 @@ CONFIGS = {
 }
 
 
+def streamed_bytes(info) -> dict:
+    """BIN's own HBM byte model per execute (the format's streams, not the
+    algorithmic 12 B/nnz): Mul reads val 8 + column-in-strip 2 B per stored
+    entry, one int32 destination per padded group, the x strips (each strip
+    once, plus one re-load per workgroup range boundary) and writes 8 B
+    products; Sum reads products 8 + row slot 2 B and writes y."""
+    E = info["stored_slots"]
+    mul = E * (8 + 2 + 8) + E // max(1, info["bin_pad"]) * 4 + 8 * info["n"]
+    summ = E * (8 + 2) + 8 * info["m"]
+    return {"mul": mul, "sum": summ, "total": mul + summ}
+
+
 def cpu_model() -> str:
     try:
         for line in open("/proc/cpuinfo"):
@@ -181,7 +193,8 @@ def main():
             "n_kernels": info["n_kernels"],
         }
         relevant = {"csr": ("csr_lanes",), "ss": ("ss_sigma",), "ell": ("ell_width",),
-                    "hyb": ("ell_width",), "dia": ("n_diags",), "css": ("css_passes", "css_slabs")}
+                    "hyb": ("ell_width",), "dia": ("n_diags",), "css": ("css_passes", "css_slabs"),
+                    "bin": ("bin_bins", "bin_strips", "bin_strip_shift", "bin_pad", "bin_sum_waves")}
         if info["format"] == "bin" and fi != 0:
             r["phases_ms"] = plan.profile(x, y, 10)  # Mul / Sum split (opt_ss MulPerf / SumPerf)
         for k in relevant.get(info["format"], ()):
@@ -273,7 +286,7 @@ def main():
     gather_gps = sp.gather_probe(local, 64 << 20, 1 << 20)
     gathers_gps = nnz_local / (r["event_ms_per_launch"] * 1e-3)
     gather_fields = {}
-    if r["format"] != "dia":  # DIA reads x from an LDS window, not by gathers
+    if r["format"] not in ("dia", "bin"):  # DIA and BIN read x from LDS, not by gathers
         gather_fields = {"x_gathers_per_s": gathers_gps, "gather_ceiling_per_s": gather_gps,
                          "frac_of_gather_ceiling": gathers_gps / gather_gps}
     # the reference's CSR5 byte model (CSR5_cuda/detail/utils.h:10-14), which
@@ -305,6 +318,7 @@ def main():
                      **gather_fields,
                      "csr5_model_gbs": csr5_bytes / (r["event_ms_per_launch"] * 1e-3) / 1e9},
         "cpu_baseline": cpu,
+        "streamed_bytes_model": streamed_bytes(info) if info["format"] == "bin" else None,
         "formats": results,
         "gen_s": round(t_gen, 2),
         "x_broadcast_ms": round(t_bcast * 1e3, 3) if distributed else None,

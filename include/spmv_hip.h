@@ -200,6 +200,12 @@ typedef struct spmv_plan_info {
     int64_t empty_rows;
     int64_t css_split_rows;  /* CSS: rows split into pieces (long rows)       */
     char kernel[64];         /* name of the dominant kernel                    */
+    int64_t bin_bins;        /* BIN: row bins (one Sum wave each), strips      */
+    int64_t bin_strips;
+    int32_t bin_strip_shift; /* BIN: x strip = 2^shift columns                 */
+    int32_t bin_pad;         /* BIN: segment padding (entries)                 */
+    int32_t bin_sum_waves;   /* BIN: Sum waves per workgroup                   */
+    int32_t bin_groups;      /* BIN: row groups (Mul launches)                 */
 } spmv_plan_info_t;
 
 int spmv_plan_info(spmv_plan_t plan, spmv_plan_info_t *info);

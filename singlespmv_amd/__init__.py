@@ -63,7 +63,9 @@ class PlanInfo(C.Structure):
                 ("algo_bytes", C.c_int64), ("row_ptr_bytes", C.c_int32), ("csr_lanes", C.c_int32),
                 ("ell_width", C.c_int32), ("ss_sigma", C.c_int32), ("n_diags", C.c_int32),
                 ("css_passes", C.c_int32), ("css_slabs", C.c_int32), ("n_kernels", C.c_int32), ("overflow_nnz", C.c_int64), ("empty_rows", C.c_int64),
-                ("css_split_rows", C.c_int64), ("kernel", C.c_char * 64)]
+                ("css_split_rows", C.c_int64), ("kernel", C.c_char * 64),
+                ("bin_bins", C.c_int64), ("bin_strips", C.c_int64), ("bin_strip_shift", C.c_int32),
+                ("bin_pad", C.c_int32), ("bin_sum_waves", C.c_int32), ("bin_groups", C.c_int32)]
 
     def as_dict(self):
         d = {k: getattr(self, k) for k, _ in self._fields_}

@@ -168,22 +168,51 @@ int build_bin(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
     std::vector<int> gof((size_t)NB);
     for (int g = 0; g < G; ++g)
         for (int64_t b = B.g_bin[(size_t)g]; b < B.g_bin[(size_t)g + 1]; ++b) gof[(size_t)b] = g;
+    // Within a segment the entries are ordered k-major: the k-th entry (in
+    // column order) of every row of the segment, rows ascending, then the
+    // (k+1)-th ...  A row's products still reach the Sum in column order (the
+    // sequential opt_crs order), but consecutive lanes of one ds_add_f64 hit
+    // different rows instead of all landing on one slot (a banded or long
+    // row otherwise serialises the LDS atomics 64 ways).
 #pragma omp parallel
     {
-        std::vector<int32_t> cur((size_t)S);
+        std::vector<int64_t> segbase((size_t)S + 1);
+        std::vector<int32_t> kpos, rowk((size_t)S, 0);
 #pragma omp for schedule(dynamic, 8)
         for (int64_t b = 0; b < NB; ++b) {
-            std::fill(cur.begin(), cur.end(), 0);
             const int64_t *o1 = off1.data() + b * S, *o2 = off2.data() + b * S;
+            segbase[0] = 0;
+            for (int64_t t = 0; t < S; ++t) segbase[(size_t)t + 1] = segbase[(size_t)t] + cnt[(size_t)(b * S + t)];
+            kpos.assign((size_t)segbase[(size_t)S], 0);
+            // pass 1: per segment, how many rows have a k-th entry
+            for (int64_t r = row0[b]; r < row0[b + 1]; ++r) {
+                for (int64_t j = A.row_ptr[r]; j < A.row_ptr[r + 1]; ++j) {
+                    const int64_t t = A.col[j] >> shift;
+                    ++kpos[(size_t)(segbase[(size_t)t] + rowk[(size_t)t]++)];
+                }
+                for (int64_t j = A.row_ptr[r]; j < A.row_ptr[r + 1]; ++j) rowk[(size_t)(A.col[j] >> shift)] = 0;
+            }
+            // counts -> start of each k-run inside its segment
+            for (int64_t t = 0; t < S; ++t) {
+                int32_t run = 0;
+                for (int64_t q = segbase[(size_t)t]; q < segbase[(size_t)t + 1]; ++q) {
+                    const int32_t c = kpos[(size_t)q];
+                    kpos[(size_t)q] = run;
+                    run += c;
+                }
+            }
+            // pass 2: place every entry
             for (int64_t r = row0[b]; r < row0[b + 1]; ++r) {
                 const uint16_t slot = (uint16_t)(r - row0[b]);
                 for (int64_t j = A.row_ptr[r]; j < A.row_ptr[r + 1]; ++j) {
                     const int32_t c = A.col[j];
-                    const int64_t s = c >> shift, k = cur[(size_t)s]++;
-                    val1[(size_t)(o1[s] + k)] = A.val[j];
-                    cs1[(size_t)(o1[s] + k)] = (uint16_t)(c & (C - 1));
-                    slot2[(size_t)(o2[s] + k)] = slot;
+                    const int64_t t = c >> shift;
+                    const int64_t k = kpos[(size_t)(segbase[(size_t)t] + rowk[(size_t)t]++)]++;
+                    val1[(size_t)(o1[t] + k)] = A.val[j];
+                    cs1[(size_t)(o1[t] + k)] = (uint16_t)(c & (C - 1));
+                    slot2[(size_t)(o2[t] + k)] = slot;
                 }
+                for (int64_t j = A.row_ptr[r]; j < A.row_ptr[r + 1]; ++j) rowk[(size_t)(A.col[j] >> shift)] = 0;
             }
             const int64_t pb = B.reuse ? B.g_prod[(size_t)gof[(size_t)b]] : 0;
             for (int64_t s = 0; s < S; ++s) {

@@ -475,6 +475,14 @@ int spmv_plan_info(spmv_plan_t p, spmv_plan_info_t *info) {
     info->empty_rows = p->empty_rows;
     info->css_split_rows = p->css.split_rows;
     std::strncpy(info->kernel, p->kernel_name.c_str(), sizeof(info->kernel) - 1);
+    if (p->format == SPMV_FORMAT_BIN) {
+        info->bin_bins = p->bin.n_bins;
+        info->bin_strips = p->bin.n_strips;
+        info->bin_strip_shift = p->bin.strip_shift;
+        info->bin_pad = 1 << p->bin.pad_log;
+        info->bin_sum_waves = p->bin.sum_waves;
+        info->bin_groups = p->bin.G;
+    }
     return SPMV_SUCCESS;
 }
 

@@ -68,7 +68,27 @@ def test_invalid_inputs_rejected_before_device():
         sp.Plan.from_csr(1, 1, np.array([0, 3], np.int64), np.array([0], np.int32), np.array([1.0]))
 
 
-def test_options_struct_layout_matches_header():
-    # spmv_options_t: 6 int32 + double + 8 int32 -> 64 bytes
-    assert C.sizeof(sp.Options) == 64
-    assert sp.PlanInfo.kernel.offset + 64 == C.sizeof(sp.PlanInfo)
+def test_options_struct_layout_matches_header(tmp_path):
+    """The ctypes mirrors of spmv_options_t / spmv_plan_info_t match the C
+    header field for field (sizeof and every offsetof, compiled with gcc)."""
+    import subprocess
+    fields = {"spmv_options_t": sp.Options, "spmv_plan_info_t": sp.PlanInfo}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "spmv_hip.h"', "int main(void) {"]
+    for cname, py in fields.items():
+        lines.append(f'printf("{cname} sizeof %zu\\n", sizeof({cname}));')
+        for f, _ in py._fields_:
+            lines.append(f'printf("{cname} {f} %zu\\n", offsetof({cname}, {f}));')
+    lines.append("return 0; }")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    subprocess.check_call(["gcc", "-I", os.path.join(root, "include"), str(src), "-o", str(exe)])
+    got = {}
+    for line in subprocess.check_output([str(exe)], text=True).splitlines():
+        cname, f, v = line.split()
+        got[(cname, f)] = int(v)
+    for cname, py in fields.items():
+        assert got[(cname, "sizeof")] == C.sizeof(py), cname
+        for f, _ in py._fields_:
+            assert got[(cname, f)] == getattr(py, f).offset, (cname, f)

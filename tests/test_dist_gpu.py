@@ -21,7 +21,7 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("config,fmts", [("c2", "css,csr"), ("c3", "auto,ss")])
+@pytest.mark.parametrize("config,fmts", [("c2", "css,csr"), ("c2", "bin,csr"), ("c3", "auto,ss")])
 def test_two_rank_bench_flow(config, fmts):
     env = dict(os.environ, BENCH_DIST_BACKEND="gloo")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
