@@ -49,7 +49,7 @@ struct MulBatch {
     int32_t d[U];
 };
 
-template <int U, int PL>
+template <int U, int PL, int MODE>
 __device__ __forceinline__ void mul_load(MulBatch<U> &B, int64_t base, int64_t e0, int64_t e1, int lane,
                                          const double *__restrict__ val1, const uint16_t *__restrict__ cs1,
                                          const int32_t *__restrict__ dst1) {
@@ -58,7 +58,7 @@ __device__ __forceinline__ void mul_load(MulBatch<U> &B, int64_t base, int64_t e
         const int64_t e = base + u * 64 + lane;
         const int64_t ee = e < e1 ? e : e0;
         B.v[u] = ld_stream(val1 + ee);
-        B.c[u] = __builtin_nontemporal_load(cs1 + ee);
+        B.c[u] = (MODE & 8) ? (uint32_t)((ee * 2654435761u) & 16383) : (uint32_t)__builtin_nontemporal_load(cs1 + ee);
         B.d[u] = ld_stream(dst1 + (ee >> PL));
     }
 }
@@ -71,7 +71,8 @@ __device__ __forceinline__ void mul_store(const MulBatch<U> &B, int64_t base, in
         const int64_t e = base + u * 64 + lane;
         if (e < e1) {
             const double pr = __dmul_rn(B.v[u], xs[B.c[u]]);
-            double *dp = prod + ((int64_t)B.d[u] << PL) + (e & ((1 << PL) - 1));
+            // MODE 4 (ablation): write in Mul order (sequential) instead of Sum order
+            double *dp = (MODE & 4) ? prod + e : prod + ((int64_t)B.d[u] << PL) + (e & ((1 << PL) - 1));
             if (MODE & 2) {
                 if (pr == 1.2345e300) *dp = pr;
             } else if (MODE & 1) {
@@ -84,7 +85,8 @@ __device__ __forceinline__ void mul_store(const MulBatch<U> &B, int64_t base, in
 }
 
 // MODE (SPMV_BIN_DEBUG, internal ablations): 1 nontemporal product stores,
-// 2 no product stores (value kept alive).  PL: segments padded to 2^PL entries.
+// 2 no product stores (value kept alive), 4 products written in Mul order
+// (sequential; wrong results -- measures the cost of the scattered layout).  PL: segments padded to 2^PL entries.
 template <int SHIFT, int U, int MODE, int PL>
 __global__ __launch_bounds__(kBinMulThreads) void bin_mul_kernel(
     const int64_t *__restrict__ piece_off, int64_t q_base, const int32_t *__restrict__ piece_strip,
@@ -108,13 +110,13 @@ __global__ __launch_bounds__(kBinMulThreads) void bin_mul_kernel(
         const int64_t first = e0 + (int64_t)w * 64 * U;
         const int64_t nit = first < e1 ? (e1 - first + STEP - 1) / STEP : 0;
         MulBatch<U> A, B;
-        if (nit > 0) mul_load<U, PL>(A, first, e0, e1, lane, val1, cs1, dst1);
+        if (nit > 0) mul_load<U, PL, MODE>(A, first, e0, e1, lane, val1, cs1, dst1);
         for (int64_t it = 0; it < nit; it += 2) {
             const int64_t ba = first + it * STEP, bb = ba + STEP;
-            if (it + 1 < nit) mul_load<U, PL>(B, bb, e0, e1, lane, val1, cs1, dst1);
+            if (it + 1 < nit) mul_load<U, PL, MODE>(B, bb, e0, e1, lane, val1, cs1, dst1);
             mul_store<U, MODE, PL>(A, ba, e1, lane, xs, prod);
             if (it + 1 < nit) {
-                if (it + 2 < nit) mul_load<U, PL>(A, bb + STEP, e0, e1, lane, val1, cs1, dst1);
+                if (it + 2 < nit) mul_load<U, PL, MODE>(A, bb + STEP, e0, e1, lane, val1, cs1, dst1);
                 mul_store<U, MODE, PL>(B, bb, e1, lane, xs, prod);
             }
         }
@@ -136,7 +138,7 @@ __device__ __forceinline__ void sum_load(SumBatch<U, MODE> &B, int64_t base, int
         const int64_t e = base + u * 64 + lane;
         const int64_t ee = e < p1 ? e : p0;
         B.v[u] = (MODE & 1) ? ld_stream(prod + (ee - pbase)) : prod[ee - pbase];
-        B.s[u] = __builtin_nontemporal_load(slot2 + ee);
+        B.s[u] = (MODE & 4) ? (uint32_t)((ee * 2654435761u) % 4096u) : (uint32_t)__builtin_nontemporal_load(slot2 + ee);
     }
 }
 
@@ -204,6 +206,10 @@ static void launch_mul_p(const spmv_plan_s *p, int g, const double *x) {
     switch (p->bin.dbg & 3) {
         case 1: launch_mul_t<SHIFT, 0, PL>(p, g, x); break;
         case 2: launch_mul_t<SHIFT, 2, PL>(p, g, x); break;
+        case 3:  // ablations: sequential NT writes (+256: no cs1 loads either)
+            if (p->bin.dbg & 256) launch_mul_t<SHIFT, 13, PL>(p, g, x);
+            else launch_mul_t<SHIFT, 5, PL>(p, g, x);
+            break;
         default: launch_mul_t<SHIFT, 1, PL>(p, g, x);
     }
 }
@@ -228,6 +234,10 @@ static void launch_sum_t(const spmv_plan_s *p, int g, double *y) {
 template <int W2, int U>
 static void launch_sum_w(const spmv_plan_s *p, int g, double *y) {
     // SPMV_BIN_DEBUG bits 2-3 -> Sum MODE
+    if (p->bin.dbg & 512) {  // ablation: no slot loads
+        launch_sum_t<W2, U, 4>(p, g, y);
+        return;
+    }
     switch ((p->bin.dbg >> 2) & 3) {
         case 1: launch_sum_t<W2, U, 1>(p, g, y); break;
         case 2: launch_sum_t<W2, U, 2>(p, g, y); break;
