@@ -494,14 +494,18 @@ int build_dia(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
     const int64_t N = A.m + A.n - 1;
     std::vector<int32_t> idx((size_t)std::max<int64_t>(N, 1), -1);
     for (int i = 0; i < d.n_diags; ++i) idx[(size_t)(offs[i] + A.m - 1)] = i;
-    d.mp = round_up(A.m, 2);
+    // row blocks of kDiaBlockRows (one workgroup), each holding its rows of
+    // every diagonal contiguously: val[(blk*nd + d)*B + r%B]
+    d.mp = round_up(A.m, kDiaBlockRows);
     const int64_t slots = (int64_t)d.n_diags * d.mp;
     std::vector<double> val((size_t)std::max<int64_t>(slots, 1), 0.0);
+    const int64_t nd = d.n_diags;
 #pragma omp parallel for schedule(static)
     for (int64_t r = 0; r < A.m; ++r)
         for (int64_t j = A.row_ptr[r]; j < A.row_ptr[r + 1]; ++j) {
             const int di = idx[(size_t)(A.col[j] - r + A.m - 1)];
-            val[(size_t)(di * d.mp + r)] += A.val[j];  // duplicates are summed
+            const int64_t at = ((r / kDiaBlockRows) * nd + di) * kDiaBlockRows + r % kDiaBlockRows;
+            val[(size_t)at] += A.val[j];  // duplicates are summed
         }
     SPMV_RETURN_IF(upload(p, &d.off, offs.data(), d.n_diags));
     if (const char *e = std::getenv("SPMV_DIA_DEBUG")) d.dbg = std::atoi(e);

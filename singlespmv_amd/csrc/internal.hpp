@@ -135,14 +135,17 @@ struct CooDev {
     double *val = nullptr;
 };
 
-// DIA (opt_dia, src/opt_dia.cpp), row-indexed: val[d*mp + r] = A[r, r+off[d]]
-// (0 where absent / outside), offsets ascending.
+// DIA (opt_dia, src/opt_dia.cpp), row-indexed and blocked by workgroup:
+// A[r, r+off[d]] at val[((r/B)*n_diags + d)*B + r%B], B = kDiaBlockRows
+// (0 where absent / outside), offsets ascending -- each workgroup streams one
+// contiguous n_diags*B*8-byte block.
+constexpr int kDiaBlockRows = 512;
 struct DiaDev {
     int n_diags = 0;
     int32_t *off = nullptr;  // device copy of offsets
     std::vector<int32_t> off_host;
     double *val = nullptr;   // [n_diags * mp]
-    int64_t mp = 0;          // diagonal stride: m rounded up to even
+    int64_t mp = 0;          // m rounded up to kDiaBlockRows
     int dbg = 0;             // SPMV_DIA_DEBUG (internal): 1 = x from global memory, no LDS window
 };
 

@@ -2,11 +2,13 @@
 // (src/opt_dia.cpp:65-97, y[col+off-ioff] += diag*x[col], plus a leaked
 // tmp[m+n-1] per call at :80).
 //
-// Row-indexed diagonals: val[d*mp + r] = A[r, r + off[d]].  One lane = two
-// rows; the diagonal loop is wave-uniform and the offsets are loaded as scalars.
-// Each value load is coalesced (consecutive rows), each x load is coalesced
-// and re-used across the diagonals through L1/L2, so HBM sees ~8 B per stored
-// slot + x + y.  Diagonals are summed in ascending offset order, i.e.
+// Row-indexed diagonals, blocked: the 512 rows of workgroup b hold every
+// diagonal contiguously, val[(b*n_diags + d)*512 + r%512] = A[r, r + off[d]],
+// so a workgroup streams ONE contiguous n_diags*4 KB block (the first layout,
+// diagonal-major val[d*mp + r], read 64 streams 160 MB apart at config 4:
+// 1.81 ms vs the blocked layout's, profiles/round1/probe/dia_blocked_ab.jsonl).
+// One lane = two rows; the diagonal loop is wave-uniform and the offsets are
+// loaded as scalars, so HBM sees ~8 B per stored slot + x + y.  Diagonals are summed in ascending offset order, i.e.
 // ascending column order with rounded multiply + add: bit-identical to the
 // sequential opt_crs row sum.  Out-of-range slots hold 0 and read a clamped,
 // in-bounds x entry.
@@ -15,8 +17,8 @@
 
 namespace spmv {
 
-// Two rows per lane: one 16-byte load of val[d*mp + r .. r+1] per diagonal
-// (mp = m rounded up to even), so a wave instruction streams 1 KiB.
+// Two rows per lane: one 16-byte load of the lane's two rows per diagonal, so
+// a wave instruction streams 1 KiB.
 //
 // LDSX: the workgroup's 512 rows need x over ONE contiguous column window
 // [r0 + off_min, r0 + 511 + off_max + 1]; it is staged once into LDS with
@@ -32,6 +34,7 @@ __global__ __launch_bounds__(256) void dia_kernel(int64_t m, int64_t mp, int64_t
     extern __shared__ double xs[];
     const int64_t r0 = 2 * (int64_t)blockIdx.x * blockDim.x;
     const int64_t r = r0 + 2 * threadIdx.x;
+    const double *vb = val + (int64_t)blockIdx.x * n_diags * kDiaBlockRows + 2 * threadIdx.x;
     auto xat = [&](int64_t c) { return x[c < 0 ? 0 : (c >= n ? n - 1 : c)]; };
     if (LDSX) {
         // out-of-range columns only meet zero-filled slots: any finite x works
@@ -47,7 +50,7 @@ __global__ __launch_bounds__(256) void dia_kernel(int64_t m, int64_t mp, int64_t
         f64x2 v[UNROLL];
         double g0[UNROLL], g1[UNROLL];
 #pragma unroll
-        for (int u = 0; u < UNROLL; ++u) v[u] = ld_stream2(val + (int64_t)(d + u) * mp + r);
+        for (int u = 0; u < UNROLL; ++u) v[u] = ld_stream2(vb + (int64_t)(d + u) * kDiaBlockRows);
 #pragma unroll
         for (int u = 0; u < UNROLL; ++u) {
             if (LDSX) {
@@ -67,7 +70,7 @@ __global__ __launch_bounds__(256) void dia_kernel(int64_t m, int64_t mp, int64_t
         }
     }
     for (; d < n_diags; ++d) {
-        const f64x2 v = ld_stream2(val + (int64_t)d * mp + r);
+        const f64x2 v = ld_stream2(vb + (int64_t)d * kDiaBlockRows);
         double a, b;
         if (LDSX) {
             const int li = lbase + off[d];
