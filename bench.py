@@ -194,7 +194,7 @@ def main():
         }
         relevant = {"csr": ("csr_lanes",), "ss": ("ss_sigma",), "ell": ("ell_width",),
                     "hyb": ("ell_width",), "dia": ("n_diags",), "css": ("css_passes", "css_slabs"),
-                    "bin": ("bin_bins", "bin_strips", "bin_strip_shift", "bin_pad", "bin_sum_waves")}
+                    "bin": ("bin_bins", "bin_strips", "bin_strip_cols", "bin_pad", "bin_sum_waves")}
         if info["format"] == "bin" and fi != 0:
             r["phases_ms"] = plan.profile(x, y, 10)  # Mul / Sum split (opt_ss MulPerf / SumPerf)
         for k in relevant.get(info["format"], ()):

@@ -95,7 +95,7 @@ typedef struct spmv_options {
     int32_t css_slab_shift; /* CSS: slab = 2^shift columns (0 = 18, 2 MiB of x) */
     int32_t css_lag;        /* CSS: pacing slack in slabs (0 = 4, -1 = no pacing) */
     int32_t css_pace;       /* CSS: 0/1 pace against every XCD, 2 own XCD only */
-    int32_t bin_strip_shift; /* BIN: x strip = 2^shift columns, 13 or 14 (0 = 14) */
+    int32_t bin_strip_cols;  /* BIN: x strip width, 64..20480 columns (0 = 20480) */
     int32_t bin_groups;      /* BIN: row groups sharing one product buffer (0 = 1) */
     int32_t reserved[3];
 } spmv_options_t;
@@ -202,7 +202,7 @@ typedef struct spmv_plan_info {
     char kernel[64];         /* name of the dominant kernel                    */
     int64_t bin_bins;        /* BIN: row bins (one Sum wave each), strips      */
     int64_t bin_strips;
-    int32_t bin_strip_shift; /* BIN: x strip = 2^shift columns                 */
+    int32_t bin_strip_cols;  /* BIN: x strip width in columns                  */
     int32_t bin_pad;         /* BIN: segment padding (entries)                 */
     int32_t bin_sum_waves;   /* BIN: Sum waves per workgroup                   */
     int32_t bin_groups;      /* BIN: row groups (Mul launches)                 */

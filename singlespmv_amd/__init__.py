@@ -53,7 +53,7 @@ class Options(C.Structure):
     _fields_ = [("format", C.c_int32), ("device", C.c_int32), ("csr_lanes", C.c_int32),
                 ("ell_width", C.c_int32), ("ss_sigma", C.c_int32), ("dia_max_diags", C.c_int32),
                 ("dia_max_fill", C.c_double), ("css_slab_shift", C.c_int32), ("css_lag", C.c_int32),
-                ("css_pace", C.c_int32), ("bin_strip_shift", C.c_int32), ("bin_groups", C.c_int32),
+                ("css_pace", C.c_int32), ("bin_strip_cols", C.c_int32), ("bin_groups", C.c_int32),
                 ("reserved", C.c_int32 * 3)]
 
 
@@ -64,7 +64,7 @@ class PlanInfo(C.Structure):
                 ("ell_width", C.c_int32), ("ss_sigma", C.c_int32), ("n_diags", C.c_int32),
                 ("css_passes", C.c_int32), ("css_slabs", C.c_int32), ("n_kernels", C.c_int32), ("overflow_nnz", C.c_int64), ("empty_rows", C.c_int64),
                 ("css_split_rows", C.c_int64), ("kernel", C.c_char * 64),
-                ("bin_bins", C.c_int64), ("bin_strips", C.c_int64), ("bin_strip_shift", C.c_int32),
+                ("bin_bins", C.c_int64), ("bin_strips", C.c_int64), ("bin_strip_cols", C.c_int32),
                 ("bin_pad", C.c_int32), ("bin_sum_waves", C.c_int32), ("bin_groups", C.c_int32)]
 
     def as_dict(self):
@@ -298,14 +298,14 @@ def coo_to_csr(m: int, row_idx: np.ndarray) -> np.ndarray:
 def make_options(fmt="auto", device: int = -1, csr_lanes: int = 0, ell_width: int = 0,
                  ss_sigma: int = 0, dia_max_diags: int = 0, dia_max_fill: float = 0.0,
                  css_slab_shift: int = 0, css_lag: int = 0, css_pace: int = 0,
-                 bin_strip_shift: int = 0, bin_groups: int = 0) -> Options:
+                 bin_strip_cols: int = 0, bin_groups: int = 0) -> Options:
     o = Options()
     lib().spmv_options_default(C.byref(o))
     o.format = FORMATS[fmt] if isinstance(fmt, str) else int(fmt)
     o.device, o.csr_lanes, o.ell_width, o.ss_sigma = device, csr_lanes, ell_width, ss_sigma
     o.dia_max_diags, o.dia_max_fill = dia_max_diags, dia_max_fill
     o.css_slab_shift, o.css_lag, o.css_pace = css_slab_shift, css_lag, css_pace
-    o.bin_strip_shift, o.bin_groups = bin_strip_shift, bin_groups
+    o.bin_strip_cols, o.bin_groups = bin_strip_cols, bin_groups
     return o
 
 

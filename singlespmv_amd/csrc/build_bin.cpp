@@ -29,16 +29,15 @@ int build_bin(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
     int ncu = 0;
     SPMV_HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, p->device));
     if (ncu <= 0) ncu = 256;
-    B.strip_shift = o.bin_strip_shift ? o.bin_strip_shift : 14;
-    SPMV_CHECK_ARG(B.strip_shift == 13 || B.strip_shift == 14, "bin_strip_shift must be 13 or 14");
-    const int shift = B.strip_shift;
-    const int64_t C = (int64_t)1 << shift;
-    B.nwg1 = ncu * (shift == 13 ? 2 : 1);  // one (two) 1024-thread workgroups per CU
+    B.strip = o.bin_strip_cols ? o.bin_strip_cols : kBinMaxStrip;
+    SPMV_CHECK_ARG(B.strip >= 64 && B.strip <= kBinMaxStrip, "bin_strip_cols must be in [64, 20480]");
+    const int64_t C = B.strip;
+    B.nwg1 = ncu;  // one 1024-thread workgroup per CU (the x strip fills the LDS)
     B.nwg2 = ncu;                           // 160 KB of LDS y slices per workgroup
     if (const char *e = std::getenv("SPMV_BIN_CUS")) {  // experiment: a subset of the CUs
         const int k = std::atoi(e);
         if (k > 0 && k < ncu) {
-            B.nwg1 = k * (shift == 13 ? 2 : 1);
+            B.nwg1 = k;
             B.nwg2 = k;
         }
     }
@@ -104,7 +103,7 @@ int build_bin(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
 #pragma omp parallel for schedule(dynamic, 16)
     for (int64_t b = 0; b < NB; ++b) {
         int32_t *cb = cnt.data() + b * S;
-        for (int64_t j = A.row_ptr[row0[b]]; j < A.row_ptr[row0[b + 1]]; ++j) ++cb[A.col[j] >> shift];
+        for (int64_t j = A.row_ptr[row0[b]]; j < A.row_ptr[row0[b + 1]]; ++j) ++cb[A.col[j] / C];
     }
     std::vector<int64_t> bprod((size_t)NB, 0);
 #pragma omp parallel for schedule(static)
@@ -136,30 +135,45 @@ int build_bin(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
         }
     }
 
-    // ---- offsets: Sum order [b][s] (global), Mul order [g][s][b]
+    // ---- offsets.  Sum (product) order [block][b][s in block]: the strips
+    // may be cut into blocks of SB strips, so a Mul workgroup's product writes
+    // stay inside one block's region instead of spanning the whole buffer,
+    // and a Sum wave reads its bin as one run per block.  Measured
+    // (profiles/round1/probe/bin_strip_blocks.jsonl): the Mul's placement
+    // sensitivity is unchanged by SB and the Sum slows down (0.31 ms at
+    // SB = S, 0.37 at 32, 0.67 at 8), so the default is SB = S: one block,
+    // the plain bin-major layout.  Mul order [g][s][b].
+    int64_t SB = S;
+    if (const char *e = std::getenv("SPMV_BIN_SB")) SB = std::max<int64_t>(1, std::atoll(e));
+    if (B.reuse || SB > S) SB = S;
+    const int64_t NBK = (S + SB - 1) / SB;
+    B.n_blocks = NBK;
     std::vector<int64_t> off2((size_t)(NB * S)), off1((size_t)(NB * S));
+    std::vector<int64_t> run_off((size_t)(NBK * NB + 1));  // run (blk, b) = [run_off[blk*NB+b], +1)
     {
         int64_t cur = 0;
-        for (int64_t i = 0; i < NB * S; ++i) {
-            off2[(size_t)i] = cur;
-            cur += rpad(cnt[(size_t)i]);
-        }
+        for (int64_t k = 0; k < NBK; ++k)
+            for (int64_t b = 0; b < NB; ++b) {
+                run_off[(size_t)(k * NB + b)] = cur;
+                for (int64_t t = k * SB; t < std::min(S, (k + 1) * SB); ++t) {
+                    off2[(size_t)(b * S + t)] = cur;
+                    cur += rpad(cnt[(size_t)(b * S + t)]);
+                }
+            }
+        run_off[(size_t)(NBK * NB)] = cur;
     }
     std::vector<int64_t> strip_start((size_t)G * (S + 1));  // Mul-order start of (g, s)
     for (int g = 0; g < G; ++g) {
         int64_t cur = B.g_prod[(size_t)g];
-        for (int64_t s = 0; s < S; ++s) {
-            strip_start[(size_t)(g * (S + 1) + s)] = cur;
+        for (int64_t t = 0; t < S; ++t) {
+            strip_start[(size_t)(g * (S + 1) + t)] = cur;
             for (int64_t b = B.g_bin[(size_t)g]; b < B.g_bin[(size_t)g + 1]; ++b) {
-                off1[(size_t)(b * S + s)] = cur;
-                cur += rpad(cnt[(size_t)(b * S + s)]);
+                off1[(size_t)(b * S + t)] = cur;
+                cur += rpad(cnt[(size_t)(b * S + t)]);
             }
         }
         strip_start[(size_t)(g * (S + 1) + S)] = cur;
     }
-    std::vector<int64_t> bin_off((size_t)NB + 1);
-    for (int64_t b = 0; b < NB; ++b) bin_off[(size_t)b] = off2[(size_t)(b * S)];
-    bin_off[(size_t)NB] = E;
 
     // ---- fill both orders
     std::vector<double> val1((size_t)E);
@@ -187,10 +201,10 @@ int build_bin(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
             // pass 1: per segment, how many rows have a k-th entry
             for (int64_t r = row0[b]; r < row0[b + 1]; ++r) {
                 for (int64_t j = A.row_ptr[r]; j < A.row_ptr[r + 1]; ++j) {
-                    const int64_t t = A.col[j] >> shift;
+                    const int64_t t = A.col[j] / C;
                     ++kpos[(size_t)(segbase[(size_t)t] + rowk[(size_t)t]++)];
                 }
-                for (int64_t j = A.row_ptr[r]; j < A.row_ptr[r + 1]; ++j) rowk[(size_t)(A.col[j] >> shift)] = 0;
+                for (int64_t j = A.row_ptr[r]; j < A.row_ptr[r + 1]; ++j) rowk[(size_t)(A.col[j] / C)] = 0;
             }
             // counts -> start of each k-run inside its segment
             for (int64_t t = 0; t < S; ++t) {
@@ -206,13 +220,13 @@ int build_bin(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
                 const uint16_t slot = (uint16_t)(r - row0[b]);
                 for (int64_t j = A.row_ptr[r]; j < A.row_ptr[r + 1]; ++j) {
                     const int32_t c = A.col[j];
-                    const int64_t t = c >> shift;
+                    const int64_t t = c / C;
                     const int64_t k = kpos[(size_t)(segbase[(size_t)t] + rowk[(size_t)t]++)]++;
                     val1[(size_t)(o1[t] + k)] = A.val[j];
-                    cs1[(size_t)(o1[t] + k)] = (uint16_t)(c & (C - 1));
+                    cs1[(size_t)(o1[t] + k)] = (uint16_t)(c - t * C);
                     slot2[(size_t)(o2[t] + k)] = slot;
                 }
-                for (int64_t j = A.row_ptr[r]; j < A.row_ptr[r + 1]; ++j) rowk[(size_t)(A.col[j] >> shift)] = 0;
+                for (int64_t j = A.row_ptr[r]; j < A.row_ptr[r + 1]; ++j) rowk[(size_t)(A.col[j] / C)] = 0;
             }
             const int64_t pb = B.reuse ? B.g_prod[(size_t)gof[(size_t)b]] : 0;
             for (int64_t s = 0; s < S; ++s) {
@@ -276,7 +290,7 @@ int build_bin(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
     SPMV_RETURN_IF(upload_vec(p, &B.cs1, cs1));
     SPMV_RETURN_IF(upload_vec(p, &B.dst1, dst1));
     SPMV_RETURN_IF(upload_vec(p, &B.slot2, slot2));
-    SPMV_RETURN_IF(upload_vec(p, &B.bin_off, bin_off));
+    SPMV_RETURN_IF(upload_vec(p, &B.run_off, run_off));
     SPMV_RETURN_IF(upload_vec(p, &B.bin_row0, row0));
     // Product-buffer placement.  The Mul writes 1-KB segments scattered over
     // the whole buffer; with some allocations of the same size it runs ~15 %

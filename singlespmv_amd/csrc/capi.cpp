@@ -478,7 +478,7 @@ int spmv_plan_info(spmv_plan_t p, spmv_plan_info_t *info) {
     if (p->format == SPMV_FORMAT_BIN) {
         info->bin_bins = p->bin.n_bins;
         info->bin_strips = p->bin.n_strips;
-        info->bin_strip_shift = p->bin.strip_shift;
+        info->bin_strip_cols = p->bin.strip;
         info->bin_pad = 1 << p->bin.pad_log;
         info->bin_sum_waves = p->bin.sum_waves;
         info->bin_groups = p->bin.G;

@@ -179,7 +179,7 @@ struct CssDev {
 
 // Binned two-phase Mul/Sum (BIN, k_bin.hip) -- opt_ss's Mul -> val_buf ->
 // Sum split (src/opt_ss.cpp:188-221) crossed with opt_css's column blocks
-// (src/opt_css.cpp:33-45).  Columns are cut into strips of 2^strip_shift
+// (src/opt_css.cpp:33-45).  Columns are cut into strips of `strip` columns
 // (the x strip sits in LDS), rows into bins of <= kBinMaxRows (one wave's
 // LDS y slice).  Entries are grouped into segments (strip s, bin b), each
 // sorted by (row, col) and padded to a multiple of 8:
@@ -193,11 +193,12 @@ struct CssDev {
 // product buffer (re-used by every group: it can stay in the Infinity Cache).
 constexpr int kBinLdsDoubles = 20480;  // Sum: 160 KB of LDS y slices per workgroup
 constexpr int kBinMulThreads = 1024;
+constexpr int kBinMaxStrip = 20480;  // Mul: x strip of 160 KB of LDS
 // Sum waves per workgroup W2 (4 or 8): a wave's slice holds kBinLdsDoubles/W2
 // doubles = bin rows + one dummy slot (padding entries add +0.0 there)
 inline int bin_max_rows(int w2) { return kBinLdsDoubles / w2 - 1; }
 struct BinDev {
-    int strip_shift = 14;  // 13 or 14 (x strip 64 / 128 KB of LDS)
+    int strip = 20480;     // x strip width in columns (<= kBinMaxStrip)
     int pad_log = 3;       // segments padded to 2^pad_log entries (8: 64-B product lines)
     int sum_waves = 8;     // W2
     int max_rows = 0;      // bin_max_rows(W2) = the dummy slot
@@ -214,7 +215,8 @@ struct BinDev {
     uint16_t *cs1 = nullptr;
     int32_t *dst1 = nullptr;       // per 2^pad_log entries
     uint16_t *slot2 = nullptr;
-    int64_t *bin_off = nullptr;   // [n_bins + 1] product offsets (global)
+    int64_t n_blocks = 1;         // strip blocks of the product layout
+    int64_t *run_off = nullptr;   // [n_blocks*n_bins + 1]: run (blk, b) of bin b's products
     int32_t *bin_row0 = nullptr;  // [n_bins + 1]
     double *prod = nullptr;       // product buffer (largest group)
     int64_t prod_cap = 0;

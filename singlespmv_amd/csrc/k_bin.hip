@@ -10,7 +10,7 @@
 //
 //  * Mul (bin_mul_kernel): a workgroup walks its nnz-balanced range of the
 //    Mul-ordered entry stream strip by strip.  Per strip it stages the
-//    2^SHIFT-column x strip in LDS, then every entry gathers x from LDS and
+//    x strip (<= kBinMaxStrip columns) in LDS, then every entry gathers x from LDS and
 //    writes its product to the product buffer at the entry's place in Sum
 //    order.  The entry stream is ordered [strip][bin][row, col] and padded per
 //    (strip, bin) segment to 8 entries, so 8 consecutive lanes write one
@@ -87,13 +87,13 @@ __device__ __forceinline__ void mul_store(const MulBatch<U> &B, int64_t base, in
 // MODE (SPMV_BIN_DEBUG, internal ablations): 1 nontemporal product stores,
 // 2 no product stores (value kept alive), 4 products written in Mul order
 // (sequential; wrong results -- measures the cost of the scattered layout).  PL: segments padded to 2^PL entries.
-template <int SHIFT, int U, int MODE, int PL>
+template <int U, int MODE, int PL>
 __global__ __launch_bounds__(kBinMulThreads) void bin_mul_kernel(
     const int64_t *__restrict__ piece_off, int64_t q_base, const int32_t *__restrict__ piece_strip,
     const int64_t *__restrict__ piece_begin, const int64_t *__restrict__ piece_end,
     const double *__restrict__ val1, const uint16_t *__restrict__ cs1, const int32_t *__restrict__ dst1,
-    const double *__restrict__ x, int64_t n, double *__restrict__ prod) {
-    __shared__ double xs[1 << SHIFT];
+    const double *__restrict__ x, int64_t n, int32_t strip, double *__restrict__ prod) {
+    __shared__ double xs[kBinMaxStrip];
     constexpr int NW = kBinMulThreads / 64;
     constexpr int64_t STEP = (int64_t)NW * 64 * U;
     const int w = threadIdx.x >> 6;
@@ -101,9 +101,9 @@ __global__ __launch_bounds__(kBinMulThreads) void bin_mul_kernel(
     const int64_t q0 = piece_off[q_base + blockIdx.x], q1 = piece_off[q_base + blockIdx.x + 1];
     for (int64_t q = q0; q < q1; ++q) {
         // consecutive pieces of a workgroup are consecutive strips: stage x
-        const int64_t c0 = (int64_t)piece_strip[q] << SHIFT;
+        const int64_t c0 = (int64_t)piece_strip[q] * strip;
         const int64_t e0 = piece_begin[q], e1 = piece_end[q];
-        const int cw = (int)(n - c0 < (1 << SHIFT) ? n - c0 : (1 << SHIFT));
+        const int cw = (int)(n - c0 < strip ? n - c0 : strip);
         __syncthreads();  // the previous strip's readers are done
         for (int i = threadIdx.x; i < cw; i += kBinMulThreads) xs[i] = x[c0 + i];
         __syncthreads();
@@ -154,12 +154,16 @@ __device__ __forceinline__ void sum_add(const SumBatch<U, MODE> &B, int64_t base
     }
 }
 
-// MODE (internal ablations): 1 nontemporal product loads, 2 no LDS atomics.
-// W2 waves per workgroup, each owning a slice of kBinLdsDoubles / W2 doubles.
+// MODE (internal ablations): 1 nontemporal product loads, 2 no LDS atomics,
+// 4 no slot loads.  W2 waves per workgroup, each owning a slice of
+// kBinLdsDoubles / W2 doubles.  A bin's products are NBK runs (one per strip
+// block, run_off[blk*nbins + b]); the batches walk them in order (a batch
+// never crosses a run), ping-ponged so one batch is always in flight.
 template <int W2, int U, int MODE>
 __global__ __launch_bounds__(64 * W2) void bin_sum_kernel(
-    int64_t b0, int64_t b1, const int64_t *__restrict__ bin_off, const int32_t *__restrict__ bin_row0,
-    int64_t pbase, const uint16_t *__restrict__ slot2, const double *__restrict__ prod, double *__restrict__ y) {
+    int64_t b0, int64_t b1, int64_t nbins, int64_t nblk, const int64_t *__restrict__ run_off,
+    const int32_t *__restrict__ bin_row0, int64_t pbase, const uint16_t *__restrict__ slot2,
+    const double *__restrict__ prod, double *__restrict__ y) {
     constexpr int SLICE = kBinLdsDoubles / W2;
     constexpr int64_t STEP = 64 * U;
     __shared__ double ylds[kBinLdsDoubles];
@@ -170,19 +174,32 @@ __global__ __launch_bounds__(64 * W2) void bin_sum_kernel(
         const int64_t r0 = bin_row0[b];
         const int rows = (int)(bin_row0[b + 1] - r0);
         for (int i = lane; i < rows; i += 64) ys[i] = 0.0;
-        const int64_t p0 = bin_off[b], p1 = bin_off[b + 1];
-        const int64_t nit = (p1 - p0 + STEP - 1) / STEP;
         double sink = 0.0;
-        SumBatch<U, MODE> A, B;
-        if (nit > 0) sum_load<U, MODE>(A, p0, p0, p1, lane, pbase, slot2, prod);
-        for (int64_t it = 0; it < nit; it += 2) {
-            const int64_t ba = p0 + it * STEP, bb = ba + STEP;
-            if (it + 1 < nit) sum_load<U, MODE>(B, bb, p0, p1, lane, pbase, slot2, prod);
-            sum_add<U, MODE, SLICE - 1>(A, ba, p1, lane, ys, sink);
-            if (it + 1 < nit) {
-                if (it + 2 < nit) sum_load<U, MODE>(A, bb + STEP, p0, p1, lane, pbase, slot2, prod);
-                sum_add<U, MODE, SLICE - 1>(B, bb, p1, lane, ys, sink);
+        // run cursor: batch = [pos, min(pos + STEP, end)) of run k
+        int64_t k = 0, pos = run_off[b], end = run_off[b + 1];
+        auto next = [&](int64_t &lo, int64_t &hi) -> bool {
+            while (pos >= end) {
+                if (++k >= nblk) return false;
+                pos = run_off[k * nbins + b];
+                end = run_off[k * nbins + b + 1];
             }
+            lo = pos;
+            hi = pos + STEP < end ? pos + STEP : end;
+            pos = hi;
+            return true;
+        };
+        SumBatch<U, MODE> A, B;
+        int64_t alo, ahi, blo, bhi;
+        bool has_a = next(alo, ahi);
+        if (has_a) sum_load<U, MODE>(A, alo, alo, ahi, lane, pbase, slot2, prod);
+        while (has_a) {
+            const bool has_b = next(blo, bhi);
+            if (has_b) sum_load<U, MODE>(B, blo, blo, bhi, lane, pbase, slot2, prod);
+            sum_add<U, MODE, SLICE - 1>(A, alo, ahi, lane, ys, sink);
+            if (!has_b) break;
+            has_a = next(alo, ahi);
+            if (has_a) sum_load<U, MODE>(A, alo, alo, ahi, lane, pbase, slot2, prod);
+            sum_add<U, MODE, SLICE - 1>(B, blo, bhi, lane, ys, sink);
         }
         if ((MODE & 2) && sink == 1.2345e300) ys[0] = sink;
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -191,34 +208,33 @@ __global__ __launch_bounds__(64 * W2) void bin_sum_kernel(
     }
 }
 
-template <int SHIFT, int MODE, int PL>
+template <int MODE, int PL>
 static void launch_mul_t(const spmv_plan_s *p, int g, const double *x) {
     const BinDev &B = p->bin;
-    hipLaunchKernelGGL((bin_mul_kernel<SHIFT, 8, MODE, PL>), dim3((unsigned)B.nwg1), dim3(kBinMulThreads), 0,
+    hipLaunchKernelGGL((bin_mul_kernel<8, MODE, PL>), dim3((unsigned)B.nwg1), dim3(kBinMulThreads), 0,
                        p->stream, B.piece_off, (int64_t)g * B.nwg1, B.piece_strip, B.piece_begin, B.piece_end,
-                       B.val1, B.cs1, B.dst1, x, p->n, B.prod);
+                       B.val1, B.cs1, B.dst1, x, p->n, (int32_t)B.strip, B.prod);
 }
 
-template <int SHIFT, int PL>
+template <int PL>
 static void launch_mul_p(const spmv_plan_s *p, int g, const double *x) {
     // SPMV_BIN_DEBUG bits 0-1 -> Mul MODE; default: nontemporal stores
     // (measured 0.81 -> 0.71 ms at config 2, profiles/round1/probe/bin_probe_c2.jsonl)
     switch (p->bin.dbg & 3) {
-        case 1: launch_mul_t<SHIFT, 0, PL>(p, g, x); break;
-        case 2: launch_mul_t<SHIFT, 2, PL>(p, g, x); break;
+        case 1: launch_mul_t<0, PL>(p, g, x); break;
+        case 2: launch_mul_t<2, PL>(p, g, x); break;
         case 3:  // ablations: sequential NT writes (+256: no cs1 loads either)
-            if (p->bin.dbg & 256) launch_mul_t<SHIFT, 13, PL>(p, g, x);
-            else launch_mul_t<SHIFT, 5, PL>(p, g, x);
+            if (p->bin.dbg & 256) launch_mul_t<13, PL>(p, g, x);
+            else launch_mul_t<5, PL>(p, g, x);
             break;
-        default: launch_mul_t<SHIFT, 1, PL>(p, g, x);
+        default: launch_mul_t<1, PL>(p, g, x);
     }
 }
 
-template <int SHIFT>
 static void launch_mul(const spmv_plan_s *p, int g, const double *x) {
-    if (p->bin.pad_log == 5) launch_mul_p<SHIFT, 5>(p, g, x);
-    else if (p->bin.pad_log == 4) launch_mul_p<SHIFT, 4>(p, g, x);
-    else launch_mul_p<SHIFT, 3>(p, g, x);
+    if (p->bin.pad_log == 5) launch_mul_p<5>(p, g, x);
+    else if (p->bin.pad_log == 4) launch_mul_p<4>(p, g, x);
+    else launch_mul_p<3>(p, g, x);
 }
 
 // Sum over the bins of group g (g < 0: every bin, product buffer = all products)
@@ -227,8 +243,8 @@ static void launch_sum_t(const spmv_plan_s *p, int g, double *y) {
     const BinDev &B = p->bin;
     const int64_t b0 = g < 0 ? 0 : B.g_bin[g], b1 = g < 0 ? B.n_bins : B.g_bin[g + 1];
     const int64_t pbase = g < 0 ? 0 : B.g_prod[g];
-    hipLaunchKernelGGL((bin_sum_kernel<W2, U, MODE>), dim3((unsigned)B.nwg2), dim3(64 * W2), 0, p->stream,
-                       b0, b1, B.bin_off, B.bin_row0, pbase, B.slot2, B.prod, y);
+    hipLaunchKernelGGL((bin_sum_kernel<W2, U, MODE>), dim3((unsigned)B.nwg2), dim3(64 * W2), 0, p->stream, b0, b1,
+                       B.n_bins, B.n_blocks, B.run_off, B.bin_row0, pbase, B.slot2, B.prod, y);
 }
 
 template <int W2, int U>
@@ -253,8 +269,7 @@ int bin_time_mul(const spmv_plan_s *p, const double *x, float *ms) {
     for (int rep = 0; rep < 2; ++rep) {  // the second pass is timed
         if (rep == 1) SPMV_HIP_TRY(hipEventRecord(a, p->stream));
         for (int g = 0; g < B.G; ++g) {
-            if (B.strip_shift == 13) launch_mul<13>(p, g, x);
-            else launch_mul<14>(p, g, x);
+            launch_mul(p, g, x);
         }
     }
     SPMV_HIP_TRY(hipEventRecord(b, p->stream));
@@ -280,8 +295,7 @@ int launch_bin(const spmv_plan_s *p, const double *x, double *y) {
     // Mul per row group (all groups' writes go to one product buffer unless
     // it is re-used per group), then Sum
     for (int g = 0; g < B.G; ++g) {
-        if (B.strip_shift == 13) launch_mul<13>(p, g, x);
-        else launch_mul<14>(p, g, x);
+        launch_mul(p, g, x);
         SPMV_HIP_TRY(hipGetLastError());
         if (B.reuse) {
             phase_mark(p);  // mul | sum

@@ -505,7 +505,7 @@ def _bin_matrix(kind, m, n, seed):
 
 @pytest.mark.parametrize("shape", [(40_000, 40_000), (30_011, 100_003), (70_001, 9_000), (5, 3), (1, 70_000)])
 @pytest.mark.parametrize("kind", ["uniform", "powerlaw", "empty_rows"])
-@pytest.mark.parametrize("opts", [{}, {"bin_strip_shift": 13}, {"bin_groups": 3}])
+@pytest.mark.parametrize("opts", [{}, {"bin_strip_cols": 16384}, {"bin_strip_cols": 3001}, {"bin_groups": 3}])
 def test_bin_bit_exact(shape, kind, opts):
     """BIN (binned Mul/Sum): every row is the sequential opt_crs sum bit for
     bit (one wave per bin adds its products in column order), for partial
@@ -560,4 +560,4 @@ def test_bin_edge_cases():
     ph = plan.profile(xd, yd, 3)
     assert list(ph) == ["mul", "sum"], ph
     with pytest.raises(sp.SpmvError):
-        sp.Plan.from_csr(50_000, 50_000, rp, col, val, "bin", bin_strip_shift=12)
+        sp.Plan.from_csr(50_000, 50_000, rp, col, val, "bin", bin_strip_cols=20481)

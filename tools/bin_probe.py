@@ -2,7 +2,7 @@
 """Per-phase times (Mul / Sum) of BIN plans on one workload, with the
 streamed bytes of each phase -> effective GB/s.  One process, interleaved.
 
-  python tools/bin_probe.py --rows 10000000 --grid 'bin_groups=1,2;bin_strip_shift=14' [--dbg 0,1,2]
+  python tools/bin_probe.py --rows 10000000 --grid 'bin_groups=1,2;bin_strip_cols=16384' [--dbg 0,1,2]
 """
 import argparse
 import itertools
