@@ -298,7 +298,7 @@ int build_bin(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
     // re-allocated between timings, profiles/round1/probe/bin_realloc.jsonl).
     // For large buffers keep the fastest of K candidates, each timed with a
     // Mul pass over a zero x at build time (results never depend on it).
-    int K = prod_bytes >= ((size_t)256 << 20) ? 3 : 1;
+    int K = prod_bytes >= ((size_t)256 << 20) ? 4 : 1;
     if (const char *e = std::getenv("SPMV_BIN_PLACEMENT")) K = std::max(1, std::min(8, std::atoi(e)));
     if (K == 1) {
         SPMV_RETURN_IF(alloc_prod());
@@ -309,7 +309,29 @@ int build_bin(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
         std::vector<double *> cand;
         std::vector<float> t;
         int st = SPMV_SUCCESS;
+        // Consecutive allocations tend to share the fast or the slow mode;
+        // candidates spaced by 16 GB spacer allocations land in different
+        // regions of device memory (all 6 unspaced candidates slow, 3 of 6
+        // spaced ones fast, profiles/round1/probe/bin_placement_spacers.jsonl).
+        // Spacers only when the device has room for them with 8 GB to spare.
+        int64_t gap_mb = 16384;
+        if (const char *e = std::getenv("SPMV_BIN_PLACEMENT_GAP_MB")) gap_mb = std::atoll(e);
+        {
+            size_t free_b = 0, total_b = 0;
+            if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) {
+                (void)hipGetLastError();
+                free_b = 0;
+            }
+            const size_t need = (size_t)(K - 1) * ((size_t)gap_mb << 20) + (size_t)K * prod_bytes + ((size_t)8 << 30);
+            if (free_b < need) gap_mb = 0;
+        }
+        std::vector<void *> spacers;
         for (int k = 0; k < K && st == SPMV_SUCCESS; ++k) {
+            if (k > 0 && gap_mb > 0) {
+                void *g = nullptr;
+                if (hipMalloc(&g, (size_t)gap_mb << 20) == hipSuccess) spacers.push_back(g);
+                else (void)hipGetLastError();
+            }
             st = alloc_prod();
             if (st != SPMV_SUCCESS) break;
             float ms = 0;
@@ -317,6 +339,7 @@ int build_bin(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
             cand.push_back(B.prod);
             t.push_back(ms);
         }
+        for (void *g : spacers) (void)hipFree(g);
         (void)hipFree(xz);
         if (cand.empty()) return st;
         (void)hipGetLastError();
