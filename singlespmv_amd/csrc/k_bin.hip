@@ -289,7 +289,9 @@ int launch_bin(const spmv_plan_s *p, const double *x, double *y) {
     }
     auto sum = [&](int g) {
         if (B.sum_waves == 2) launch_sum_w<2, 32>(p, g, y);
-        else if (B.sum_waves == 4) launch_sum_w<4, 16>(p, g, y);
+        // 4 waves: 32-entry batches per lane (0.313 -> 0.295 ms against 16,
+        // profiles/round1/probe/bin_sum_depth.jsonl; 231 VGPRs, 1 wave/SIMD)
+        else if (B.sum_waves == 4) launch_sum_w<4, 32>(p, g, y);
         else launch_sum_w<8, 8>(p, g, y);
     };
     // Mul per row group (all groups' writes go to one product buffer unless
