@@ -287,8 +287,12 @@ def test_device_pointers_and_streams():
         assert ms > 0
 
 
-def test_dropin_optimizeproblem_spmv():
-    """The reference-signature drop-in (include/opt_hip.h) via libopt_hip.so."""
+@pytest.mark.parametrize("fmt", ["", "bin", "css"])
+def test_dropin_optimizeproblem_spmv(fmt, monkeypatch):
+    """The reference-signature drop-in (include/opt_hip.h) via libopt_hip.so
+    (format from SPMV_HIP_FORMAT, as the -DOPT_HIP_<FMT> build would fix it)."""
+    if fmt:
+        monkeypatch.setenv("SPMV_HIP_FORMAT", fmt)
     class SpMatC(C.Structure):
         _fields_ = [("nRow", C.c_int), ("nCol", C.c_int), ("nNnz", C.c_int),
                     ("row_idx", C.c_void_p), ("col_idx", C.c_void_p), ("val", C.c_void_p)]
@@ -320,7 +324,7 @@ def test_dropin_optimizeproblem_spmv():
     L.SpMVRelease(C.byref(Ao))
 
 
-@pytest.mark.parametrize("fmt,name", [("ss", "SS"), ("css", "CSS"), ("jds", "JDS"), ("coo", "COO")])
+@pytest.mark.parametrize("fmt,name", [("ss", "SS"), ("css", "CSS"), ("jds", "JDS"), ("coo", "COO"), ("bin", "BIN")])
 def test_driver_binary_reports_block(fmt, name):
     import subprocess
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
