@@ -228,6 +228,33 @@ def main():
         torch.cuda.synchronize()
         coll_ms = (time.perf_counter() - tc) / reps * 1e3
 
+    # iterative use (power-iteration shape): every step is the
+    # local SpMV followed by ONE all_gather of the y slices into the next x
+    # (RCCL over xGMI), both on the current stream; reported beside `value`,
+    # never as it.  Runs on a copy of x.
+    iterative = None
+    if distributed and n_glob == rows * world:
+        x_it = x.clone()
+        cur = torch.cuda.current_stream(dev)
+        plan.set_stream(cur)
+        for _ in range(2):
+            plan.execute(x_it, y_head, async_=True)
+            sdist.allgather_into(x_it, y_head)
+        torch.cuda.synchronize()
+        dist.barrier()
+        ti = time.perf_counter()
+        for _ in range(args.steps):
+            plan.execute(x_it, y_head, async_=True)
+            sdist.allgather_into(x_it, y_head)
+        torch.cuda.synchronize()
+        dist.barrier()
+        t_it = sdist.max_over_ranks([time.perf_counter() - ti], dev)[0] / args.steps
+        iterative = {"ms_per_iter": t_it * 1e3, "gflops": 2.0 * nnz_local * world / t_it / 1e9,
+                     "step": "local SpMV + all_gather(y slices -> next x)"}
+        del x_it
+        plan.set_stream(stream)
+        plan.execute(x, y_head)  # y_head back to A x for the checks below
+
     verify_rel = None
     if args.verify:
         # the whole y (all ranks' slices, RCCL/gloo all_gather) vs the oracle's
@@ -323,6 +350,7 @@ def main():
         "gen_s": round(t_gen, 2),
         "x_broadcast_ms": round(t_bcast * 1e3, 3) if distributed else None,
         "collective_ms": coll_ms,
+        "iterative": iterative,
         "max_rel_err_vs_cpu": max_rel,
         "verify_max_rel": verify_rel,
     }

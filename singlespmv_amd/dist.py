@@ -99,3 +99,20 @@ def gather_y(y_local, rows_per_rank: int):
     out = torch.empty(world * rows_per_rank, dtype=y_local.dtype, device=y_local.device)
     dist.all_gather_into_tensor(out, y_local.contiguous())
     return out
+
+
+def allgather_into(x, y_local):
+    """Iterative use (y -> next x): all-gather every rank's
+    equal y slice straight into the replicated x (length world * slice)."""
+    import torch
+    import torch.distributed as dist
+    if not _dist_on():
+        x[: y_local.numel()].copy_(y_local)
+        return x
+    if _CPU_COLLECTIVES and y_local.is_cuda:
+        parts = [torch.empty(y_local.numel(), dtype=y_local.dtype) for _ in range(dist.get_world_size())]
+        dist.all_gather(parts, y_local.cpu())
+        x.copy_(torch.cat(parts).to(x.device))
+        return x
+    dist.all_gather_into_tensor(x, y_local.contiguous())
+    return x

@@ -86,3 +86,43 @@ def test_partition_is_nnz_balanced():
         loads.append(len(c))
     assert sum(loads) == nnz
     assert max(loads) - min(loads) <= 5000 + 1  # within one row of perfect
+
+
+def _iter_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        m = 4000  # divisible by world: equal slices, as bench.py's weak-scaled configs
+        spec = sp.gen_spec("uniform", m, per_row=7, seed=21)
+        (r0, r1), rp, col, val = sdist.shard_generated(spec, rank, world)
+        x = torch.zeros(m, dtype=torch.float64)
+        if rank == 0:
+            x.copy_(torch.from_numpy(sp.generate_vector(m, seed=22)))
+        sdist.replicate_x(x, 0)
+        for _ in range(3):  # y = A x; x <- all_gather(y slices)
+            y_local = torch.from_numpy(oracle.csr_spmv(rp, col, val, x.numpy()))
+            sdist.allgather_into(x, y_local)
+        if rank == 0:
+            grp, gcol, gval = sp.generate_csr(spec)
+            xr = sp.generate_vector(m, seed=22)
+            for _ in range(3):
+                xr = oracle.csr_spmv(grp, gcol, gval, xr)
+            q.put(bool(np.array_equal(x.numpy(), xr)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_iterative_allgather_step_matches_single_process():
+    """bench.py's iterative measurement: local SpMV + one all_gather of the
+    y slices into the next x, three steps, equals three global SpMVs."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_iter_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    assert q.get(timeout=10), "iterated sharded x differs from the single-process iteration"

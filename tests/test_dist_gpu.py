@@ -36,3 +36,4 @@ def test_two_rank_bench_flow(config, fmts):
     assert d["n_gpus"] == 2 and d["scaling"] == "weak" and d["value"] > 0
     assert d["config"]["m"] == 300000 and d["collective_ms"] is not None
     assert d["verify_max_rel"] is not None and d["verify_max_rel"] <= 1e-12, d["verify_max_rel"]
+    assert d["iterative"] is not None and d["iterative"]["ms_per_iter"] > 0
