@@ -565,3 +565,31 @@ def test_bin_edge_cases():
     assert list(ph) == ["mul", "sum"], ph
     with pytest.raises(sp.SpmvError):
         sp.Plan.from_csr(50_000, 50_000, rp, col, val, "bin", bin_strip_cols=20481)
+
+
+# ---------------------------------------------------------------- full size
+@pytest.mark.parametrize("config", ["c2", "c3"])
+def test_full_size_headline_bit_exact(config):
+    """BASELINE configs 2 and 3 at their full size (160 M / 29.6 M entries):
+    the AUTO plan (BIN) against the oracle's opt_crs restatement -- bit for
+    bit -- plus linearity A(x1 + x2) = A x1 + A x2 to fp64 rounding."""
+    import torch
+    if config == "c2":
+        spec = sp.gen_spec("uniform", 10_000_000, per_row=16, seed=42)
+    else:
+        spec = sp.gen_spec("powerlaw", 5_000_000, max_len=10000, alpha=2.0, seed=42)
+    rp, col, val = sp.generate_csr(spec)
+    m = len(rp) - 1
+    plan = sp.Plan.from_csr(m, m, rp, col, val, "auto")
+    assert plan.info()["format"] == "bin"
+    x1 = sp.generate_vector(m, seed=43)
+    x2 = sp.generate_vector(m, seed=44)
+    y = torch.empty(m, dtype=torch.float64, device="cuda")
+    outs = []
+    for xv in (x1, x2, x1 + x2):
+        plan.execute(torch.from_numpy(xv).cuda(), y)
+        outs.append(y.cpu().numpy().copy())
+    assert np.array_equal(outs[0], oracle_y(rp, col, val, x1))
+    lin = np.abs(outs[2] - (outs[0] + outs[1]))
+    assert np.all(lin <= 1e-12 * np.abs(outs[2]) + 1e-300)
+    plan.destroy()
