@@ -255,6 +255,23 @@ def main():
         plan.set_stream(stream)
         plan.execute(x, y_head)  # y_head back to A x for the checks below
 
+    # the drop-in's host-buffer mode (opt_cusparse's per-call H2D x / D2H y,
+    # src/opt_cusparse.cpp:72,82): PCIe-inclusive, reported beside `value`
+    host_mode = None
+    if rank == 0 and world == 1:
+        xh = np.ascontiguousarray(x.cpu().numpy())
+        yh = np.empty(rows, np.float64)
+        reps = 5
+        plan.execute(xh, yh)
+        th = time.perf_counter()
+        for _ in range(reps):
+            plan.execute(xh, yh)
+        t_h = (time.perf_counter() - th) / reps
+        host_mode = {"ms_per_call": t_h * 1e3, "gflops": 2.0 * nnz_local / t_h / 1e9,
+                     "pcie_bytes": 8 * (n_glob + rows),
+                     "note": "host x and y (numpy): H2D x + SpMV + D2H y per call, like opt_cusparse"}
+        del xh, yh
+
     verify_rel = None
     if args.verify:
         # the whole y (all ranks' slices, RCCL/gloo all_gather) vs the oracle's
@@ -351,6 +368,7 @@ def main():
         "x_broadcast_ms": round(t_bcast * 1e3, 3) if distributed else None,
         "collective_ms": coll_ms,
         "iterative": iterative,
+        "host_buffers": host_mode,
         "max_rel_err_vs_cpu": max_rel,
         "verify_max_rel": verify_rel,
     }
