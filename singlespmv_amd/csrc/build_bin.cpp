@@ -97,6 +97,14 @@ int build_bin(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
     }
     const int64_t NB = (int64_t)row0.size() - 1;
     B.n_bins = NB;
+    // the (bin, strip) tables are dense: refuse shapes whose segment grid
+    // would not fit (a huge, very sparse matrix -- BIN's padding would be
+    // most of its traffic there anyway)
+    if ((__int128)NB * S > ((__int128)1 << 28)) {
+        set_error("BIN: " + std::to_string(NB) + " row bins x " + std::to_string(S) +
+                  " column strips exceed the segment table limit (2^28); use CSS or CSR");
+        return SPMV_ERROR_NOT_SUPPORTED;
+    }
 
     // ---- segment sizes (bin b, strip s)
     std::vector<int32_t> cnt((size_t)(NB * S), 0);

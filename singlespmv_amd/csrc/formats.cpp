@@ -806,7 +806,13 @@ int choose_format(const HostCsr &A, const spmv_options_t &o) {
     // (profiles/round1/probe/bin_vs_css_sizes.jsonl: 0.50 vs 0.58 ms at
     // 5 M x 5 M uniform, 0.25 vs 0.28 ms at config 3; CSS wins at 1-2 M), and
     // its advantage grows with n (1.2 vs 2.6 ms at 10 M x 80 M)
-    if (A.n >= 3500000 && A.nnz >= 20000000 && mean >= 2.0) return SPMV_FORMAT_BIN;
+    // ... as long as its (bin, strip) segments stay long enough for the
+    // 8/16-entry padding (expected segment >= 12 entries: 20 at the N = 8
+    // rank shape, 128 at config 2)
+    if (A.n >= 3500000 && A.nnz >= 20000000 && mean >= 2.0) {
+        const double bins = std::ceil((double)A.m / 5119.0), strips = std::ceil((double)A.n / 20480.0);
+        if ((double)A.nnz / (bins * strips) >= 12.0 && bins * strips <= (double)(1 << 28)) return SPMV_FORMAT_BIN;
+    }
     if (A.n * 8 > ((int64_t)6 << 20) && A.m >= 256 * 1024 && mean >= 2.0) return SPMV_FORMAT_CSS;
     // near-uniform rows -> CSR (one lane count fits every row; it matched or
     // beat sliced ELL at every measured size); skewed -> segmented sum

@@ -593,3 +593,22 @@ def test_full_size_headline_bit_exact(config):
     lin = np.abs(outs[2] - (outs[0] + outs[1]))
     assert np.all(lin <= 1e-12 * np.abs(outs[2]) + 1e-300)
     plan.destroy()
+
+
+
+def test_bin_refuses_huge_sparse_grid_and_auto_avoids_it():
+    """A very sparse, very wide matrix: BIN's (bin, strip) segments would be
+    nearly empty (all padding) -- AUTO does not pick BIN; a segment grid
+    beyond 2^28 is refused with NOT_SUPPORTED."""
+    m, n = 4_000_000, 2_000_000_000
+    rng = np.random.default_rng(3)
+    per = 6
+    rp = np.arange(0, per * m + 1, per, dtype=np.int64)
+    col = np.sort(rng.integers(0, n, size=(m, per)), axis=1).astype(np.int32).ravel()
+    val = rng.random(per * m)
+    with pytest.raises(sp.SpmvError, match="not supported"):
+        sp.Plan.from_csr(m, n, rp, col, val, "bin")
+    m2, n2 = 4_000_000, 400_000_000  # 782 bins x 19532 strips: 1.5 entries per segment
+    col2 = np.sort(rng.integers(0, n2, size=(m2, per)), axis=1).astype(np.int32).ravel()
+    plan = sp.Plan.from_csr(m2, n2, rp, col2, val, "auto")
+    assert plan.info()["format"] != "bin"
