@@ -600,15 +600,15 @@ def test_bin_refuses_huge_sparse_grid_and_auto_avoids_it():
     """A very sparse, very wide matrix: BIN's (bin, strip) segments would be
     nearly empty (all padding) -- AUTO does not pick BIN; a segment grid
     beyond 2^28 is refused with NOT_SUPPORTED."""
-    m, n = 4_000_000, 2_000_000_000
     rng = np.random.default_rng(3)
-    per = 6
+    m, n, per = 16_000_000, 2_000_000_000, 2  # 4096 bins x 97657 strips > 2^28
     rp = np.arange(0, per * m + 1, per, dtype=np.int64)
     col = np.sort(rng.integers(0, n, size=(m, per)), axis=1).astype(np.int32).ravel()
     val = rng.random(per * m)
     with pytest.raises(sp.SpmvError, match="not supported"):
         sp.Plan.from_csr(m, n, rp, col, val, "bin")
-    m2, n2 = 4_000_000, 400_000_000  # 782 bins x 19532 strips: 1.5 entries per segment
-    col2 = np.sort(rng.integers(0, n2, size=(m2, per)), axis=1).astype(np.int32).ravel()
-    plan = sp.Plan.from_csr(m2, n2, rp, col2, val, "auto")
+    m2, n2, per2 = 4_000_000, 400_000_000, 6  # 782 bins x 19532 strips: 1.6 entries per segment
+    rp2 = np.arange(0, per2 * m2 + 1, per2, dtype=np.int64)
+    col2 = np.sort(rng.integers(0, n2, size=(m2, per2)), axis=1).astype(np.int32).ravel()
+    plan = sp.Plan.from_csr(m2, n2, rp2, col2, rng.random(per2 * m2), "auto")
     assert plan.info()["format"] != "bin"
