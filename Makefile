@@ -21,7 +21,7 @@ LIB       = singlespmv_amd/libspmv_hip.so
 OPTLIB    = singlespmv_amd/libopt_hip.so
 OBJDIR    = build/obj
 HOST_SRC  = $(CSRC)/capi.cpp $(CSRC)/formats.cpp $(CSRC)/build_bin.cpp $(CSRC)/hostutil.cpp $(CSRC)/mmio.cpp
-KERN_SRC  = $(CSRC)/k_csr.hip $(CSRC)/k_ell.hip $(CSRC)/k_ss.hip $(CSRC)/k_dia.hip $(CSRC)/k_css.hip $(CSRC)/k_coo.hip $(CSRC)/k_convert.hip $(CSRC)/k_probe.hip $(CSRC)/k_bin.hip
+KERN_SRC  = $(CSRC)/k_csr.hip $(CSRC)/k_ell.hip $(CSRC)/k_ss.hip $(CSRC)/k_dia.hip $(CSRC)/k_css.hip $(CSRC)/k_coo.hip $(CSRC)/k_convert.hip $(CSRC)/k_probe.hip $(CSRC)/k_bin.hip $(CSRC)/k_bin_build.hip
 HOST_OBJ  = $(patsubst $(CSRC)/%.cpp,$(OBJDIR)/%.o,$(HOST_SRC))
 KERN_OBJ  = $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(KERN_SRC))
 HDRS      = include/spmv_hip.h include/opt_hip.h include/spmv_util.h \

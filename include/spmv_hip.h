@@ -123,7 +123,9 @@ int spmv_plan_create_csr32(int32_t m, int32_t n, int32_t nnz, const int32_t *row
 /* Plan from a CSR that already lives in device memory (64-bit row pointers;
  * all three arrays on the plan's device, only read).  CSR and SS are
  * converted on the device (the CSR5 conversion pipeline,
- * CSR5_cuda/detail/cuda/format_cuda.h:21-718); every other format, and
+ * CSR5_cuda/detail/cuda/format_cuda.h:21-718), and so is BIN when every
+ * row's columns are ascending by 20480-column strip (only the row pointers
+ * and the (bin, strip) counts visit the host); every other format, and
  * AUTO, copies the CSR to the host and takes the host builder.  The input is
  * validated on the device like spmv_plan_create_csr's host check. */
 int spmv_plan_create_csr_device(int64_t m, int64_t n, int64_t nnz, const int64_t *d_row_ptr,

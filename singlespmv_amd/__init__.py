@@ -332,8 +332,8 @@ class Plan:
     @classmethod
     def from_device_csr(cls, m: int, n: int, row_ptr, col, val, fmt="auto", **opts) -> "Plan":
         """Plan from torch CUDA tensors (int64 row_ptr, int32 col, float64
-        val): CSR and SS are converted on the device, other formats stage
-        through the host (spmv_plan_create_csr_device)."""
+        val): CSR, SS and BIN are converted on the device, other formats
+        stage through the host (spmv_plan_create_csr_device)."""
         for name, t, dt in (("row_ptr", row_ptr, torch.int64), ("col", col, torch.int32),
                             ("val", val, torch.float64)):
             if not _is_device(t) or t.dtype != dt or not t.is_contiguous():

@@ -1,7 +1,15 @@
-// build_bin.cpp -- host builder of the binned two-phase Mul/Sum format (BIN,
-// see internal.hpp BinDev and k_bin.hip).  The OptimizeProblem counterpart
-// (src/opt_ss.cpp:52-142 builds opt_ss's segments and val_buf, untimed, once);
-// OpenMP-parallel over bins, 64-bit offsets.
+// build_bin.cpp -- builders of the binned two-phase Mul/Sum format (BIN, see
+// internal.hpp BinDev and k_bin.hip).  The OptimizeProblem counterpart
+// (src/opt_ss.cpp:52-142 builds opt_ss's segments and val_buf, untimed, once).
+//
+//   build_bin        host CSR: OpenMP-parallel over bins, then one upload
+//   build_bin_device device CSR (k_bin_build.hip): only the row pointers and
+//                    the (bin, strip) counts visit the host; the entry arrays
+//                    are filled in HBM
+//
+// Both share the phases: parameters -> row bins -> segment counts -> offsets
+// (row groups, Mul / Sum orders) -> fill -> Mul pieces -> uploads and the
+// product-buffer placement search.
 #include <omp.h>
 
 #include <algorithm>
@@ -22,8 +30,19 @@ static int upload_vec(spmv_plan_s *p, T **dst, const std::vector<T> &src) {
     return SPMV_SUCCESS;
 }
 
+// Host-side layout shared by the two builders.
+struct BinLayout {
+    int64_t S = 0, NB = 0, E = 0, PAD = 16;
+    std::vector<int32_t> row0;          // [NB + 1]
+    std::vector<int32_t> cnt;           // [NB * S] entries per (bin, strip)
+    std::vector<int64_t> off1, off2;    // [NB * S] segment start, Mul / Sum order
+    std::vector<int64_t> run_off;       // [NBK * NB + 1]
+    std::vector<int64_t> strip_start;   // [G * (S + 1)] Mul-order start of (group, strip)
+    int64_t rpad(int64_t v) const { return (v + PAD - 1) & ~(PAD - 1); }
+};
 
-int build_bin(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
+// ---- parameters (strip width, workgroups, padding, Sum waves) -----------
+static int bin_params(spmv_plan_s *p, const spmv_options_t &o, int64_t m, int64_t n, int64_t nnz) {
     BinDev &B = p->bin;
     if (const char *d = std::getenv("SPMV_BIN_DEBUG")) B.dbg = std::atoi(d);
     int ncu = 0;
@@ -33,7 +52,7 @@ int build_bin(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
     SPMV_CHECK_ARG(B.strip >= 64 && B.strip <= kBinMaxStrip, "bin_strip_cols must be in [64, 20480]");
     const int64_t C = B.strip;
     B.nwg1 = ncu;  // one 1024-thread workgroup per CU (the x strip fills the LDS)
-    B.nwg2 = ncu;                           // 160 KB of LDS y slices per workgroup
+    B.nwg2 = ncu;  // 160 KB of LDS y slices per workgroup
     if (const char *e = std::getenv("SPMV_BIN_CUS")) {  // experiment: a subset of the CUs
         const int k = std::atoi(e);
         if (k > 0 && k < ncu) {
@@ -52,9 +71,9 @@ int build_bin(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
     // 16-64 on the N = 2..8 weak-scaling shapes (pad 8 best: 22 % padding
     // instead of 43 % at N = 8, profiles/round1/probe/bin_wide.jsonl)
     {
-        const int64_t S0 = std::max<int64_t>(1, (A.n + C - 1) / C);
-        const int64_t NB0 = std::max<int64_t>(1, (A.m + bin_max_rows(B.sum_waves) - 1) / bin_max_rows(B.sum_waves));
-        const double seg = (double)A.nnz / ((double)S0 * (double)NB0);
+        const int64_t S0 = std::max<int64_t>(1, (n + C - 1) / C);
+        const int64_t NB0 = std::max<int64_t>(1, (m + bin_max_rows(B.sum_waves) - 1) / bin_max_rows(B.sum_waves));
+        const double seg = (double)nnz / ((double)S0 * (double)NB0);
         B.pad_log = seg >= 96.0 ? 4 : 3;
     }
     if (const char *e = std::getenv("SPMV_BIN_PADLOG")) B.pad_log = std::min(5, std::max(3, std::atoi(e)));
@@ -63,68 +82,68 @@ int build_bin(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
         B.sum_waves = w == 2 || w == 4 ? w : 8;
     }
     B.max_rows = bin_max_rows(B.sum_waves);
-    const int max_rows = B.max_rows;
-    const int64_t PAD = (int64_t)1 << B.pad_log;
-    p->algo_bytes = 12 * A.nnz + 8 * A.n + 8 * A.m;
+    p->algo_bytes = 12 * nnz + 8 * n + 8 * m;
     p->n_kernels = 2;
     p->kernel_name = "bin_mul_kernel+bin_sum_kernel";
-    if (A.m == 0 || A.nnz == 0) {  // launch_bin only clears y
-        B.G = 0;
-        return SPMV_SUCCESS;
-    }
-    const int64_t S = std::max<int64_t>(1, (A.n + C - 1) / C);
-    B.n_strips = S;
-    auto rpad = [PAD](int64_t v) { return (v + PAD - 1) & ~(PAD - 1); };
+    return SPMV_SUCCESS;
+}
 
-    // ---- bins: <= max_rows rows, cut at cumulative nnz targets; a
-    // multiple of the Sum kernel's wave count when there are enough rows
+// ---- row bins: <= max_rows rows, cut at cumulative nnz targets; a multiple
+// of the Sum kernel's wave count when there are enough rows
+static int bin_rows(spmv_plan_s *p, const int64_t *row_ptr, int64_t m, int64_t n, int64_t nnz, BinLayout &L) {
+    BinDev &B = p->bin;
+    const int max_rows = B.max_rows;
+    L.S = std::max<int64_t>(1, (n + B.strip - 1) / B.strip);
+    L.PAD = (int64_t)1 << B.pad_log;
+    B.n_strips = L.S;
     const int64_t waves = (int64_t)B.nwg2 * B.sum_waves;
-    int64_t nb = std::max<int64_t>(1, (A.m + max_rows - 1) / max_rows);
+    int64_t nb = std::max<int64_t>(1, (m + max_rows - 1) / max_rows);
     if (nb * 2 >= waves) nb = (nb + waves - 1) / waves * waves;
-    std::vector<int32_t> row0{0};
-    for (int64_t r = 0; r < A.m;) {
-        const int64_t b = (int64_t)row0.size() - 1;
+    L.row0.assign(1, 0);
+    for (int64_t r = 0; r < m;) {
+        const int64_t b = (int64_t)L.row0.size() - 1;
         int64_t r1;
         if (b >= nb - 1) {
-            r1 = std::min<int64_t>(A.m, r + max_rows);
+            r1 = std::min<int64_t>(m, r + max_rows);
         } else {
-            const int64_t tgt = (int64_t)((__int128)A.nnz * (b + 1) / nb);
-            r1 = std::lower_bound(A.row_ptr + r + 1, A.row_ptr + A.m + 1, tgt) - A.row_ptr;
+            const int64_t tgt = (int64_t)((__int128)nnz * (b + 1) / nb);
+            r1 = std::lower_bound(row_ptr + r + 1, row_ptr + m + 1, tgt) - row_ptr;
             r1 = std::max<int64_t>(r + 1, std::min<int64_t>(r1, r + max_rows));
         }
-        row0.push_back((int32_t)r1);
+        L.row0.push_back((int32_t)r1);
         r = r1;
     }
-    const int64_t NB = (int64_t)row0.size() - 1;
-    B.n_bins = NB;
+    L.NB = (int64_t)L.row0.size() - 1;
+    B.n_bins = L.NB;
     // the (bin, strip) tables are dense: refuse shapes whose segment grid
     // would not fit (a huge, very sparse matrix -- BIN's padding would be
     // most of its traffic there anyway)
-    if ((__int128)NB * S > ((__int128)1 << 28)) {
-        set_error("BIN: " + std::to_string(NB) + " row bins x " + std::to_string(S) +
+    if ((__int128)L.NB * L.S > ((__int128)1 << 28)) {
+        set_error("BIN: " + std::to_string(L.NB) + " row bins x " + std::to_string(L.S) +
                   " column strips exceed the segment table limit (2^28); use CSS or CSR");
         return SPMV_ERROR_NOT_SUPPORTED;
     }
+    return SPMV_SUCCESS;
+}
 
-    // ---- segment sizes (bin b, strip s)
-    std::vector<int32_t> cnt((size_t)(NB * S), 0);
-#pragma omp parallel for schedule(dynamic, 16)
-    for (int64_t b = 0; b < NB; ++b) {
-        int32_t *cb = cnt.data() + b * S;
-        for (int64_t j = A.row_ptr[row0[b]]; j < A.row_ptr[row0[b + 1]]; ++j) ++cb[A.col[j] / C];
-    }
+// ---- offsets from the counts: row groups, Sum (product) order
+// [block][b][s in block], Mul order [g][s][b]
+static void bin_offsets(spmv_plan_s *p, const spmv_options_t &o, BinLayout &L) {
+    BinDev &B = p->bin;
+    const int64_t S = L.S, NB = L.NB;
     std::vector<int64_t> bprod((size_t)NB, 0);
 #pragma omp parallel for schedule(static)
     for (int64_t b = 0; b < NB; ++b) {
         int64_t t = 0;
-        for (int64_t s = 0; s < S; ++s) t += rpad(cnt[(size_t)(b * S + s)]);
+        for (int64_t s = 0; s < S; ++s) t += L.rpad(L.cnt[(size_t)(b * S + s)]);
         bprod[(size_t)b] = t;
     }
     int64_t E = 0;
     for (int64_t b = 0; b < NB; ++b) E += bprod[(size_t)b];
+    L.E = E;
     B.n_entries = E;
 
-    // ---- row groups: contiguous bins, balanced by products
+    // row groups: contiguous bins, balanced by products
     int G = o.bin_groups > 0 ? o.bin_groups : 1;
     if (G > NB) G = (int)NB;
     B.G = G;
@@ -143,68 +162,73 @@ int build_bin(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
         }
     }
 
-    // ---- offsets.  Sum (product) order [block][b][s in block]: the strips
-    // may be cut into blocks of SB strips, so a Mul workgroup's product writes
-    // stay inside one block's region instead of spanning the whole buffer,
-    // and a Sum wave reads its bin as one run per block.  Measured
-    // (profiles/round1/probe/bin_strip_blocks.jsonl): the Mul's placement
-    // sensitivity is unchanged by SB and the Sum slows down (0.31 ms at
-    // SB = S, 0.37 at 32, 0.67 at 8), so the default is SB = S: one block,
-    // the plain bin-major layout.  Mul order [g][s][b].
+    // The strips may be cut into blocks of SB strips, so a Mul workgroup's
+    // product writes stay inside one block's region instead of spanning the
+    // whole buffer, and a Sum wave reads its bin as one run per block.
+    // Measured (profiles/round1/probe/bin_strip_blocks.jsonl): the Mul's
+    // placement sensitivity is unchanged by SB and the Sum slows down (0.31
+    // ms at SB = S, 0.37 at 32, 0.67 at 8), so the default is SB = S: one
+    // block, the plain bin-major layout.
     int64_t SB = S;
     if (const char *e = std::getenv("SPMV_BIN_SB")) SB = std::max<int64_t>(1, std::atoll(e));
     if (B.reuse || SB > S) SB = S;
     const int64_t NBK = (S + SB - 1) / SB;
     B.n_blocks = NBK;
-    std::vector<int64_t> off2((size_t)(NB * S)), off1((size_t)(NB * S));
-    std::vector<int64_t> run_off((size_t)(NBK * NB + 1));  // run (blk, b) = [run_off[blk*NB+b], +1)
+    L.off2.assign((size_t)(NB * S), 0);
+    L.off1.assign((size_t)(NB * S), 0);
+    L.run_off.assign((size_t)(NBK * NB + 1), 0);
     {
         int64_t cur = 0;
         for (int64_t k = 0; k < NBK; ++k)
             for (int64_t b = 0; b < NB; ++b) {
-                run_off[(size_t)(k * NB + b)] = cur;
+                L.run_off[(size_t)(k * NB + b)] = cur;
                 for (int64_t t = k * SB; t < std::min(S, (k + 1) * SB); ++t) {
-                    off2[(size_t)(b * S + t)] = cur;
-                    cur += rpad(cnt[(size_t)(b * S + t)]);
+                    L.off2[(size_t)(b * S + t)] = cur;
+                    cur += L.rpad(L.cnt[(size_t)(b * S + t)]);
                 }
             }
-        run_off[(size_t)(NBK * NB)] = cur;
+        L.run_off[(size_t)(NBK * NB)] = cur;
     }
-    std::vector<int64_t> strip_start((size_t)G * (S + 1));  // Mul-order start of (g, s)
+    L.strip_start.assign((size_t)G * (S + 1), 0);
     for (int g = 0; g < G; ++g) {
         int64_t cur = B.g_prod[(size_t)g];
         for (int64_t t = 0; t < S; ++t) {
-            strip_start[(size_t)(g * (S + 1) + t)] = cur;
+            L.strip_start[(size_t)(g * (S + 1) + t)] = cur;
             for (int64_t b = B.g_bin[(size_t)g]; b < B.g_bin[(size_t)g + 1]; ++b) {
-                off1[(size_t)(b * S + t)] = cur;
-                cur += rpad(cnt[(size_t)(b * S + t)]);
+                L.off1[(size_t)(b * S + t)] = cur;
+                cur += L.rpad(L.cnt[(size_t)(b * S + t)]);
             }
         }
-        strip_start[(size_t)(g * (S + 1) + S)] = cur;
+        L.strip_start[(size_t)(g * (S + 1) + S)] = cur;
     }
+}
 
-    // ---- fill both orders
+// ---- host fill.  Within a segment the entries are ordered k-major: the
+// k-th entry (in column order) of every row of the segment, rows ascending,
+// then the (k+1)-th ...  A row's products still reach the Sum in column order
+// (the sequential opt_crs order), but consecutive lanes of one ds_add_f64 hit
+// different rows instead of all landing on one slot (a banded or long row
+// otherwise serialises the LDS atomics 64 ways).
+static int bin_fill_host(spmv_plan_s *p, const HostCsr &A, const BinLayout &L) {
+    BinDev &B = p->bin;
+    const int64_t S = L.S, NB = L.NB, E = L.E, C = B.strip, PAD = L.PAD;
+    const int max_rows = B.max_rows;
     std::vector<double> val1((size_t)E);
     std::vector<uint16_t> cs1((size_t)E), slot2((size_t)E);
     std::vector<int32_t> dst1((size_t)(E >> B.pad_log));
     std::vector<int> gof((size_t)NB);
-    for (int g = 0; g < G; ++g)
+    for (int g = 0; g < B.G; ++g)
         for (int64_t b = B.g_bin[(size_t)g]; b < B.g_bin[(size_t)g + 1]; ++b) gof[(size_t)b] = g;
-    // Within a segment the entries are ordered k-major: the k-th entry (in
-    // column order) of every row of the segment, rows ascending, then the
-    // (k+1)-th ...  A row's products still reach the Sum in column order (the
-    // sequential opt_crs order), but consecutive lanes of one ds_add_f64 hit
-    // different rows instead of all landing on one slot (a banded or long
-    // row otherwise serialises the LDS atomics 64 ways).
 #pragma omp parallel
     {
         std::vector<int64_t> segbase((size_t)S + 1);
         std::vector<int32_t> kpos, rowk((size_t)S, 0);
 #pragma omp for schedule(dynamic, 8)
         for (int64_t b = 0; b < NB; ++b) {
-            const int64_t *o1 = off1.data() + b * S, *o2 = off2.data() + b * S;
+            const int64_t *o1 = L.off1.data() + b * S, *o2 = L.off2.data() + b * S;
+            const int32_t *row0 = L.row0.data();
             segbase[0] = 0;
-            for (int64_t t = 0; t < S; ++t) segbase[(size_t)t + 1] = segbase[(size_t)t] + cnt[(size_t)(b * S + t)];
+            for (int64_t t = 0; t < S; ++t) segbase[(size_t)t + 1] = segbase[(size_t)t] + L.cnt[(size_t)(b * S + t)];
             kpos.assign((size_t)segbase[(size_t)S], 0);
             // pass 1: per segment, how many rows have a k-th entry
             for (int64_t r = row0[b]; r < row0[b + 1]; ++r) {
@@ -238,7 +262,7 @@ int build_bin(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
             }
             const int64_t pb = B.reuse ? B.g_prod[(size_t)gof[(size_t)b]] : 0;
             for (int64_t s = 0; s < S; ++s) {
-                const int64_t n0 = cnt[(size_t)(b * S + s)], n8 = rpad(n0);
+                const int64_t n0 = L.cnt[(size_t)(b * S + s)], n8 = L.rpad(n0);
                 for (int64_t k = n0; k < n8; ++k) {
                     val1[(size_t)(o1[s] + k)] = 0.0;
                     cs1[(size_t)(o1[s] + k)] = 0;
@@ -249,16 +273,24 @@ int build_bin(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
             }
         }
     }
-    std::vector<int64_t>().swap(off1);
-    std::vector<int64_t>().swap(off2);
+    SPMV_RETURN_IF(upload_vec(p, &B.val1, val1));
+    SPMV_RETURN_IF(upload_vec(p, &B.cs1, cs1));
+    SPMV_RETURN_IF(upload_vec(p, &B.dst1, dst1));
+    SPMV_RETURN_IF(upload_vec(p, &B.slot2, slot2));
+    return SPMV_SUCCESS;
+}
 
-    // ---- Mul pieces: each workgroup takes an nnz-balanced range of its
-    // group's Mul-ordered entries (cut at 64-entry multiples), split at strips
+// ---- Mul pieces, small tables, product buffer (placement search) -----------
+static int bin_finish(spmv_plan_s *p, int64_t n, const BinLayout &L) {
+    BinDev &B = p->bin;
+    const int64_t S = L.S, E = L.E;
+    // Mul pieces: each workgroup takes an nnz-balanced range of its group's
+    // Mul-ordered entries (cut at 64-entry multiples), split at strips
     std::vector<int64_t> piece_off{0}, pbeg, pend;
     std::vector<int32_t> pstrip;
-    for (int g = 0; g < G; ++g) {
+    for (int g = 0; g < B.G; ++g) {
         const int64_t g0 = B.g_prod[(size_t)g], g1 = B.g_prod[(size_t)g + 1];
-        const int64_t *ss = strip_start.data() + (size_t)g * (S + 1);
+        const int64_t *ss = L.strip_start.data() + (size_t)g * (S + 1);
         int64_t s = 0;
         for (int k = 0; k < B.nwg1; ++k) {
             const int64_t a = g0 + (int64_t)(((__int128)(g1 - g0) * k / B.nwg1) & ~(__int128)63);
@@ -275,10 +307,9 @@ int build_bin(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
             piece_off.push_back((int64_t)pstrip.size());
         }
     }
-
     B.prod_cap = B.reuse ? 0 : E;
     if (B.reuse)
-        for (int g = 0; g < G; ++g) B.prod_cap = std::max(B.prod_cap, B.g_prod[(size_t)g + 1] - B.g_prod[(size_t)g]);
+        for (int g = 0; g < B.G; ++g) B.prod_cap = std::max(B.prod_cap, B.g_prod[(size_t)g + 1] - B.g_prod[(size_t)g]);
     const size_t prod_bytes = sizeof(double) * (size_t)std::max<int64_t>(B.prod_cap, 1);
     auto alloc_prod = [&]() -> int {
         // plain hipMalloc.  (hipDeviceMallocContiguous was tried for the
@@ -294,12 +325,8 @@ int build_bin(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
     SPMV_RETURN_IF(upload_vec(p, &B.piece_strip, pstrip));
     SPMV_RETURN_IF(upload_vec(p, &B.piece_begin, pbeg));
     SPMV_RETURN_IF(upload_vec(p, &B.piece_end, pend));
-    SPMV_RETURN_IF(upload_vec(p, &B.val1, val1));
-    SPMV_RETURN_IF(upload_vec(p, &B.cs1, cs1));
-    SPMV_RETURN_IF(upload_vec(p, &B.dst1, dst1));
-    SPMV_RETURN_IF(upload_vec(p, &B.slot2, slot2));
-    SPMV_RETURN_IF(upload_vec(p, &B.run_off, run_off));
-    SPMV_RETURN_IF(upload_vec(p, &B.bin_row0, row0));
+    SPMV_RETURN_IF(upload_vec(p, &B.run_off, L.run_off));
+    SPMV_RETURN_IF(upload_vec(p, &B.bin_row0, L.row0));
     // Product-buffer placement.  The Mul writes 1-KB segments scattered over
     // the whole buffer; with some allocations of the same size it runs ~15 %
     // slower (config 2: 0.66 vs 0.56 ms for ONE plan whose buffer was
@@ -312,8 +339,8 @@ int build_bin(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
         SPMV_RETURN_IF(alloc_prod());
     } else {
         double *xz = nullptr;
-        SPMV_HIP_TRY(hipMalloc(&xz, sizeof(double) * (size_t)std::max<int64_t>(A.n, 1)));
-        SPMV_HIP_TRY(hipMemset(xz, 0, sizeof(double) * (size_t)std::max<int64_t>(A.n, 1)));
+        SPMV_HIP_TRY(hipMalloc(&xz, sizeof(double) * (size_t)std::max<int64_t>(n, 1)));
+        SPMV_HIP_TRY(hipMemset(xz, 0, sizeof(double) * (size_t)std::max<int64_t>(n, 1)));
         std::vector<double *> cand;
         std::vector<float> t;
         int st = SPMV_SUCCESS;
@@ -360,12 +387,56 @@ int build_bin(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
     if (B.dbg & 16) {
         std::fprintf(stderr, "[bin] val1 %p cs1 %p dst1 %p slot2 %p prod %p (E %lld) placement ms:", (void *)B.val1,
                      (void *)B.cs1, (void *)B.dst1, (void *)B.slot2, (void *)B.prod, (long long)E);
-        for (float t : B.placement_ms) std::fprintf(stderr, " %.4f", t);
+        for (float tt : B.placement_ms) std::fprintf(stderr, " %.4f", tt);
         std::fprintf(stderr, "\n");
     }
     p->stored_slots = E;
-    p->n_kernels = B.reuse ? 2 * G : G + 1;
+    p->n_kernels = B.reuse ? 2 * B.G : B.G + 1;
     return SPMV_SUCCESS;
+}
+
+int build_bin(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
+    BinDev &B = p->bin;
+    SPMV_RETURN_IF(bin_params(p, o, A.m, A.n, A.nnz));
+    if (A.m == 0 || A.nnz == 0) {  // launch_bin only clears y
+        B.G = 0;
+        return SPMV_SUCCESS;
+    }
+    BinLayout L;
+    SPMV_RETURN_IF(bin_rows(p, A.row_ptr, A.m, A.n, A.nnz, L));
+    // segment sizes (bin b, strip s)
+    const int64_t S = L.S, NB = L.NB, C = B.strip;
+    L.cnt.assign((size_t)(NB * S), 0);
+#pragma omp parallel for schedule(dynamic, 16)
+    for (int64_t b = 0; b < NB; ++b) {
+        int32_t *cb = L.cnt.data() + b * S;
+        for (int64_t j = A.row_ptr[L.row0[(size_t)b]]; j < A.row_ptr[L.row0[(size_t)b + 1]]; ++j) ++cb[A.col[j] / C];
+    }
+    bin_offsets(p, o, L);
+    SPMV_RETURN_IF(bin_fill_host(p, A, L));
+    return bin_finish(p, A.n, L);
+}
+
+int build_bin_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, const double *d_val,
+                     const spmv_options_t &o) {
+    BinDev &B = p->bin;
+    SPMV_RETURN_IF(bin_params(p, o, p->m, p->n, p->nnz));
+    if (p->m == 0 || p->nnz == 0) {
+        B.G = 0;
+        return SPMV_SUCCESS;
+    }
+    std::vector<int64_t> rp((size_t)p->m + 1);
+    SPMV_HIP_TRY(hipMemcpy(rp.data(), d_rp, 8 * (size_t)(p->m + 1), hipMemcpyDeviceToHost));
+    BinLayout L;
+    SPMV_RETURN_IF(bin_rows(p, rp.data(), p->m, p->n, p->nnz, L));
+    std::vector<int64_t> bstart((size_t)L.NB + 1);
+    for (int64_t b = 0; b <= L.NB; ++b) bstart[(size_t)b] = rp[(size_t)L.row0[(size_t)b]];
+    std::vector<int64_t>().swap(rp);
+    const int st = bin_count_device(p, d_rp, d_col, L.row0, bstart, L.S, L.cnt);
+    if (st != SPMV_SUCCESS) return st;  // kBinNeedHostBuild: unsorted rows
+    bin_offsets(p, o, L);
+    SPMV_RETURN_IF(bin_fill_device(p, d_rp, d_col, d_val, L.row0, bstart, L.cnt, L.off1, L.off2, L.S, L.E));
+    return bin_finish(p, p->n, L);
 }
 
 }  // namespace spmv

@@ -3,6 +3,7 @@
 #include <omp.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -200,7 +201,37 @@ int spmv_plan_create_csr_device(int64_t m, int64_t n, int64_t nnz, const int64_t
         }
     }
     SPMV_RETURN_IF(validate_csr_device(d_row_ptr, m, d_col_idx, nnz, n));
-    if (o.format != SPMV_FORMAT_CSR && o.format != SPMV_FORMAT_SS) {
+    const bool on_device = o.format == SPMV_FORMAT_CSR || o.format == SPMV_FORMAT_SS ||
+                           (o.format == SPMV_FORMAT_BIN && !std::getenv("SPMV_BIN_HOST_BUILD"));
+    if (on_device) {
+        spmv_plan_s *p = new (std::nothrow) spmv_plan_s;
+        if (!p) {
+            set_error("host allocation of the plan failed");
+            return SPMV_ERROR_OUT_OF_MEMORY;
+        }
+        p->device = dev;
+        p->m = m;
+        p->n = n;
+        p->nnz = nnz;
+        const double mean = m ? (double)nnz / (double)m : 0.0;
+        int st;
+        switch (o.format) {
+            case SPMV_FORMAT_CSR: st = build_csr_device(p, d_row_ptr, d_col_idx, d_val, o, mean); break;
+            case SPMV_FORMAT_SS: st = build_ss_device(p, d_row_ptr, d_col_idx, d_val, o, mean); break;
+            default: st = build_bin_device(p, d_row_ptr, d_col_idx, d_val, o); break;
+        }
+        if (st == SPMV_SUCCESS) {
+            p->format = o.format;
+            *out = p;
+            return SPMV_SUCCESS;
+        }
+        p->arena.release();
+        delete p;
+        // BIN's device fill needs every row's column strips non-decreasing;
+        // other CSRs take the host builder below
+        if (st != kBinNeedHostBuild) return st;
+    }
+    {
         // host builders: stage the CSR through host memory
         std::vector<int64_t> rp((size_t)m + 1);
         std::vector<int32_t> col((size_t)nnz);
@@ -214,26 +245,6 @@ int spmv_plan_create_csr_device(int64_t m, int64_t n, int64_t nnz, const int64_t
         HostCsr A{m, n, nnz, rp.data(), col.data(), val.data()};
         return create_from_csr(A, &o, out);
     }
-    spmv_plan_s *p = new (std::nothrow) spmv_plan_s;
-    if (!p) {
-        set_error("host allocation of the plan failed");
-        return SPMV_ERROR_OUT_OF_MEMORY;
-    }
-    p->device = dev;
-    p->m = m;
-    p->n = n;
-    p->nnz = nnz;
-    const double mean = m ? (double)nnz / (double)m : 0.0;
-    const int st = o.format == SPMV_FORMAT_CSR ? build_csr_device(p, d_row_ptr, d_col_idx, d_val, o, mean)
-                                               : build_ss_device(p, d_row_ptr, d_col_idx, d_val, o, mean);
-    if (st != SPMV_SUCCESS) {
-        p->arena.release();
-        delete p;
-        return st;
-    }
-    p->format = o.format;
-    *out = p;
-    return SPMV_SUCCESS;
 }
 
 int spmv_plan_create_csr32_device(int32_t m, int32_t n, int32_t nnz, const int32_t *d_row_ptr,

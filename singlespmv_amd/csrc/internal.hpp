@@ -274,10 +274,24 @@ int build_css(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o);
 int build_coo(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o);
 int build_jds(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o);
 int build_bin(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o);  // build_bin.cpp
+// BIN from a device CSR (build_bin.cpp + k_bin_build.hip).  Returns
+// kBinNeedHostBuild when a row's column strips are not non-decreasing (the
+// caller then stages the CSR through the host builder).
+constexpr int kBinNeedHostBuild = -1000;
+int build_bin_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, const double *d_val,
+                     const spmv_options_t &o);
+// k_bin_build.hip: bstart[b] = row_ptr[row0[b]] (first entry of each bin)
+int bin_count_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, const std::vector<int32_t> &row0,
+                     const std::vector<int64_t> &bstart, int64_t S, std::vector<int32_t> &cnt);
+int bin_fill_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, const double *d_val,
+                    const std::vector<int32_t> &row0, const std::vector<int64_t> &bstart,
+                    const std::vector<int32_t> &cnt, const std::vector<int64_t> &off1,
+                    const std::vector<int64_t> &off2, int64_t S, int64_t E);
 // k_convert.hip -- device-input builders (the CSR already lives in HBM).
 int validate_csr_device(const int64_t *d_rp, int64_t m, const int32_t *d_col, int64_t nnz, int64_t n);
 int widen_row_ptr_device(const int32_t *d_rp32, int64_t m, int64_t **d_rp64);  // hipMalloc'd; caller frees
 int launch_scale(const spmv_plan_s *p, double *y, double alpha);              // y *= alpha on p->stream
+int exclusive_scan_i64(const int64_t *in, int64_t *out, int64_t n, hipStream_t st, std::vector<void *> &tmp);
 int build_csr_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, const double *d_val,
                      const spmv_options_t &o, double mean_row);
 int build_ss_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, const double *d_val,

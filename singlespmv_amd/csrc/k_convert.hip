@@ -167,6 +167,10 @@ inline unsigned grid_for(int64_t n) { return (unsigned)std::max<int64_t>(1, std:
 
 }  // namespace
 
+int exclusive_scan_i64(const int64_t *in, int64_t *out, int64_t n, hipStream_t st, std::vector<void *> &tmp) {
+    return exclusive_scan(nullptr, in, out, n, st, tmp);
+}
+
 int widen_row_ptr_device(const int32_t *d_rp32, int64_t m, int64_t **d_rp64) {
     *d_rp64 = nullptr;
     SPMV_HIP_TRY(hipMalloc(d_rp64, 8 * (size_t)(m + 1)));

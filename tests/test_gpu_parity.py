@@ -567,6 +567,49 @@ def test_bin_edge_cases():
         sp.Plan.from_csr(50_000, 50_000, rp, col, val, "bin", bin_strip_cols=20481)
 
 
+@pytest.mark.parametrize("opts", [{}, {"bin_strip_cols": 3001}, {"bin_groups": 3}])
+def test_bin_device_build(opts, monkeypatch):
+    """spmv_plan_create_csr_device with BIN: the segments are counted, laid
+    out and filled on the GPU (k_bin_build.hip).  Same bins / strips / slots
+    as the host builder and y bit-identical to it and to the oracle; rows
+    whose column strips are not ascending stage through the host builder."""
+    import torch
+    cases = [("uniform", 40_000, 40_000), ("powerlaw", 30_011, 100_003), ("empty_rows", 70_001, 9_000),
+             ("uniform", 5, 3), ("powerlaw", 1, 70_000)]
+    for kind, m, n in cases:
+        rp, col, val = _bin_matrix(kind, m, n, seed=m % 89)
+        x = sp.generate_vector(n, seed=17)
+        yo = oracle_y(rp, col, val, x)
+        ph = sp.Plan.from_csr(m, n, rp, col, val, "bin", **opts)
+        pd = sp.Plan.from_device_csr(m, n, torch.from_numpy(rp).cuda(), torch.from_numpy(col).cuda(),
+                                     torch.from_numpy(val).cuda(), "bin", **opts)
+        ih, idv = ph.info(), pd.info()
+        for k in ("format", "stored_slots", "bin_bins", "bin_strips", "bin_pad", "bin_groups"):
+            assert ih[k] == idv[k], (kind, m, n, k, ih[k], idv[k])
+        yd = run_plan(pd, x, m)
+        assert np.array_equal(yd, run_plan(ph, x, m)), f"{kind} {m}x{n} {opts}"
+        assert np.array_equal(yd, yo), f"{kind} {m}x{n} {opts}"
+    # unsorted rows (strips descending inside some rows) -> host builder
+    rp, col, val = _bin_matrix("powerlaw", 50_000, 50_000, seed=3)
+    col = col.copy()
+    for r in range(0, 50_000, 7):
+        col[rp[r]:rp[r + 1]] = col[rp[r]:rp[r + 1]][::-1]
+    x = sp.generate_vector(50_000, seed=5)
+    pd = sp.Plan.from_device_csr(50_000, 50_000, torch.from_numpy(rp).cuda(), torch.from_numpy(col).cuda(),
+                                 torch.from_numpy(val).cuda(), "bin", **opts)
+    ph = sp.Plan.from_csr(50_000, 50_000, rp, col, val, "bin", **opts)
+    yd = run_plan(pd, x, 50_000)
+    assert np.array_equal(yd, run_plan(ph, x, 50_000))
+    # BIN adds a row's strips in strip order: with unsorted columns that is
+    # not the CSR order the oracle follows, so rounding may differ
+    check_close(yd, oracle_y(rp, col, val, x), what="unsorted rows")
+    # all-empty
+    pd = sp.Plan.from_device_csr(6, 6, torch.zeros(7, dtype=torch.int64, device="cuda"),
+                                 torch.zeros(0, dtype=torch.int32, device="cuda"),
+                                 torch.zeros(0, dtype=torch.float64, device="cuda"), "bin")
+    assert not run_plan(pd, np.ones(6), 6).any()
+
+
 # ---------------------------------------------------------------- full size
 @pytest.mark.parametrize("config", ["c2", "c3"])
 def test_full_size_headline_bit_exact(config):
