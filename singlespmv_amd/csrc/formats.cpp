@@ -541,6 +541,10 @@ int build_css(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
     int ncu = 0;
     SPMV_HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, p->device));
     c.nwg = ncu > 0 ? ncu : 256;
+    if (const char *e = std::getenv("SPMV_CSS_WGS")) {  // experiment: a subset of the CUs
+        const int k = std::atoi(e);
+        if (k >= 8 && k < c.nwg) c.nwg = k;
+    }
     constexpr int W = kCssWorkers;
     const int64_t per_pass = (int64_t)c.nwg * kCssMaxRows;
     const int P_min = (int)std::max<int64_t>(1, (A.m + per_pass - 1) / per_pass);

@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--repeat", type=int, default=1, help="identical plans per variant (placement effects)")
     ap.add_argument("--prealloc-gb", type=float, default=0, help="allocate and free this much device memory first")
+    ap.add_argument("--hold-gb", type=float, default=0, help="allocate this much device memory first and keep it")
+    ap.add_argument("--throwaway", action="store_true", help="build and destroy one plan before the measured ones")
     a = ap.parse_args()
     import torch
     import singlespmv_amd as sp
@@ -42,6 +44,11 @@ def main():
         torch.cuda.synchronize()
         del t
         torch.cuda.empty_cache()
+    if a.hold_gb:
+        hold = torch.empty(int(a.hold_gb * (1 << 30)), dtype=torch.uint8, device="cuda")  # noqa: F841
+        hold.fill_(1)
+    if a.throwaway:
+        sp.Plan.from_csr(m, n, rp, col, val, "bin").destroy()
     keys, vals = [], []
     for part in filter(None, a.grid.split(";")):
         k, v = part.split("=")
