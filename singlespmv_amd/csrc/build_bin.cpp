@@ -333,8 +333,10 @@ static int bin_finish(spmv_plan_s *p, int64_t n, const BinLayout &L) {
     // re-allocated between timings, profiles/round1/probe/bin_realloc.jsonl).
     // For large buffers keep the fastest of K candidates, each timed with a
     // Mul pass over a zero x at build time (results never depend on it).
-    int K = prod_bytes >= ((size_t)256 << 20) ? 4 : 1;
-    if (const char *e = std::getenv("SPMV_BIN_PLACEMENT")) K = std::max(1, std::min(8, std::atoi(e)));
+    // Up to 8 candidates: best-of-4 still left 5 of 9 config-2 plans in the
+    // slow mode, best-of-8 1 of 9 (profiles/round1/probe/bin_placement_k8.txt).
+    int K = prod_bytes >= ((size_t)256 << 20) ? 8 : 1;
+    if (const char *e = std::getenv("SPMV_BIN_PLACEMENT")) K = std::max(1, std::min(12, std::atoi(e)));
     if (K == 1) {
         SPMV_RETURN_IF(alloc_prod());
     } else {
@@ -357,8 +359,15 @@ static int bin_finish(spmv_plan_s *p, int64_t n, const BinLayout &L) {
                 (void)hipGetLastError();
                 free_b = 0;
             }
-            const size_t need = (size_t)(K - 1) * ((size_t)gap_mb << 20) + (size_t)K * prod_bytes + ((size_t)8 << 30);
-            if (free_b < need) gap_mb = 0;
+            // as many spaced candidates as fit (at least 2), else 4 unspaced
+            auto need = [&](int k) {
+                return (size_t)(k - 1) * ((size_t)gap_mb << 20) + (size_t)k * prod_bytes + ((size_t)8 << 30);
+            };
+            while (K > 2 && free_b < need(K)) --K;
+            if (free_b < need(K)) {
+                gap_mb = 0;
+                K = std::min(K, 4);
+            }
         }
         std::vector<void *> spacers;
         for (int k = 0; k < K && st == SPMV_SUCCESS; ++k) {
@@ -373,6 +382,9 @@ static int bin_finish(spmv_plan_s *p, int64_t n, const BinLayout &L) {
             st = bin_time_mul(p, xz, &ms);
             cand.push_back(B.prod);
             t.push_back(ms);
+            // the modes differ by ~15 %: once both have been seen, stop
+            if (k >= 3 && *std::min_element(t.begin(), t.end()) < 0.93f * *std::max_element(t.begin(), t.end()))
+                break;
         }
         for (void *g : spacers) (void)hipFree(g);
         (void)hipFree(xz);
