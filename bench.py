@@ -94,6 +94,13 @@ def main():
         # any OpenMP runtime is loaded.  Not for N>1: ranks share the host.
         os.environ.setdefault("OMP_PROC_BIND", "close")
         os.environ.setdefault("OMP_PLACES", "cores")
+    elif os.environ.get("OMP_NUM_THREADS", "1") == "1":
+        # torchrun's default of one OpenMP thread per rank would serialise the
+        # host generator and format builders (untimed, but minutes at the
+        # 8-GPU shape): share the host cores between the node's ranks instead
+        # (read by the library's OpenMP runtime when it loads, below)
+        local_world = max(1, int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "1"))))
+        os.environ["OMP_NUM_THREADS"] = str(max(1, host_cores // local_world))
     import torch
     import torch.distributed as dist
 
