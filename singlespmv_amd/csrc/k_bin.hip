@@ -154,7 +154,7 @@ __device__ __forceinline__ void sum_add(const SumBatch<U, MODE> &B, int64_t base
     }
 }
 
-// MODE (internal ablations): 1 nontemporal product loads, 2 no LDS atomics,
+// MODE (internal ablations): 1 nontemporal product loads (the default), 2 no LDS atomics,
 // 4 no slot loads.  W2 waves per workgroup, each owning a slice of
 // kBinLdsDoubles / W2 doubles.  A bin's products are NBK runs (one per strip
 // block, run_off[blk*nbins + b]); the batches walk them in order (a batch
@@ -254,10 +254,13 @@ static void launch_sum_w(const spmv_plan_s *p, int g, double *y) {
         launch_sum_t<W2, U, 4>(p, g, y);
         return;
     }
+    // default: nontemporal product loads (config 2 Sum 0.308 -> 0.298 ms,
+    // neutral at config 3 and the N = 8 shape, profiles/round1/probe/bin_sum_nt_loads.jsonl);
+    // bits 2-3 = 1: ordinary loads (ablation)
     switch ((p->bin.dbg >> 2) & 3) {
-        case 1: launch_sum_t<W2, U, 1>(p, g, y); break;
+        case 1: launch_sum_t<W2, U, 0>(p, g, y); break;
         case 2: launch_sum_t<W2, U, 2>(p, g, y); break;
-        default: launch_sum_t<W2, U, 0>(p, g, y);
+        default: launch_sum_t<W2, U, 1>(p, g, y);
     }
 }
 
