@@ -37,6 +37,8 @@ struct BinLayout {
     std::vector<int32_t> cnt;           // [NB * S] entries per (bin, strip)
     std::vector<int64_t> off1, off2;    // [NB * S] segment start, Mul / Sum order
     std::vector<int64_t> run_off;       // [NBK * NB + 1]
+    std::vector<int64_t> srun_off;      // [NBK * NB + 1] slot runs, each padded to 64*sum_u
+    int64_t ES = 0, SB = 1;             // slot entries; strips per block
     std::vector<int64_t> strip_start;   // [G * (S + 1)] Mul-order start of (group, strip)
     int64_t rpad(int64_t v) const { return (v + PAD - 1) & ~(PAD - 1); }
 };
@@ -82,6 +84,9 @@ static int bin_params(spmv_plan_s *p, const spmv_options_t &o, int64_t m, int64_
         B.sum_waves = w == 2 || w == 4 ? w : 8;
     }
     B.max_rows = bin_max_rows(B.sum_waves);
+    B.sum_u = B.sum_waves == 8 ? 8 : 32;  // must match launch_sum's <W2, U> pairs
+    B.slot_linear = false;
+    if (const char *e = std::getenv("SPMV_BIN_SLOT_LINEAR")) B.slot_linear = std::atoi(e) != 0;
     p->algo_bytes = 12 * nnz + 8 * n + 8 * m;
     p->n_kernels = 2;
     p->kernel_name = "bin_mul_kernel+bin_sum_kernel";
@@ -189,6 +194,20 @@ static void bin_offsets(spmv_plan_s *p, const spmv_options_t &o, BinLayout &L) {
             }
         L.run_off[(size_t)(NBK * NB)] = cur;
     }
+    // slot runs: the same runs, each padded to whole Sum batches
+    {
+        const int64_t step = B.slot_linear ? 1 : 64 * (int64_t)B.sum_u;
+        L.srun_off.assign(L.run_off.size(), 0);
+        int64_t sc = 0;
+        for (size_t r = 0; r + 1 < L.run_off.size(); ++r) {
+            L.srun_off[r] = sc;
+            sc += (L.run_off[r + 1] - L.run_off[r] + step - 1) / step * step;
+        }
+        L.srun_off.back() = sc;
+        L.ES = sc;
+        L.SB = SB;
+        B.strip_block = SB;
+    }
     L.strip_start.assign((size_t)G * (S + 1), 0);
     for (int g = 0; g < G; ++g) {
         int64_t cur = B.g_prod[(size_t)g];
@@ -214,7 +233,7 @@ static int bin_fill_host(spmv_plan_s *p, const HostCsr &A, const BinLayout &L) {
     const int64_t S = L.S, NB = L.NB, E = L.E, C = B.strip, PAD = L.PAD;
     const int max_rows = B.max_rows;
     std::vector<double> val1((size_t)E);
-    std::vector<uint16_t> cs1((size_t)E), slot2((size_t)E);
+    std::vector<uint16_t> cs1((size_t)E), slot2((size_t)L.ES, (uint16_t)max_rows);
     std::vector<int32_t> dst1((size_t)(E >> B.pad_log));
     std::vector<int> gof((size_t)NB);
     for (int g = 0; g < B.G; ++g)
@@ -226,6 +245,11 @@ static int bin_fill_host(spmv_plan_s *p, const HostCsr &A, const BinLayout &L) {
 #pragma omp for schedule(dynamic, 8)
         for (int64_t b = 0; b < NB; ++b) {
             const int64_t *o1 = L.off1.data() + b * S, *o2 = L.off2.data() + b * S;
+            // slot index of product position q of strip t's segment (its run: block t / SB)
+            auto sidx = [&](int64_t t, int64_t q) {
+                const size_t run = (size_t)((t / L.SB) * NB + b);
+                return (size_t)bin_slot_index(q, L.run_off[run], L.srun_off[run], B.slot_linear ? 0 : B.sum_u);
+            };
             const int32_t *row0 = L.row0.data();
             segbase[0] = 0;
             for (int64_t t = 0; t < S; ++t) segbase[(size_t)t + 1] = segbase[(size_t)t] + L.cnt[(size_t)(b * S + t)];
@@ -256,7 +280,7 @@ static int bin_fill_host(spmv_plan_s *p, const HostCsr &A, const BinLayout &L) {
                     const int64_t k = kpos[(size_t)(segbase[(size_t)t] + rowk[(size_t)t]++)]++;
                     val1[(size_t)(o1[t] + k)] = A.val[j];
                     cs1[(size_t)(o1[t] + k)] = (uint16_t)(c - t * C);
-                    slot2[(size_t)(o2[t] + k)] = slot;
+                    slot2[sidx(t, o2[t] + k)] = slot;
                 }
                 for (int64_t j = A.row_ptr[r]; j < A.row_ptr[r + 1]; ++j) rowk[(size_t)(A.col[j] / C)] = 0;
             }
@@ -266,7 +290,7 @@ static int bin_fill_host(spmv_plan_s *p, const HostCsr &A, const BinLayout &L) {
                 for (int64_t k = n0; k < n8; ++k) {
                     val1[(size_t)(o1[s] + k)] = 0.0;
                     cs1[(size_t)(o1[s] + k)] = 0;
-                    slot2[(size_t)(o2[s] + k)] = (uint16_t)max_rows;
+                    slot2[sidx(s, o2[s] + k)] = (uint16_t)max_rows;
                 }
                 for (int64_t t = 0; t < n8; t += PAD)
                     dst1[(size_t)((o1[s] + t) >> B.pad_log)] = (int32_t)((o2[s] + t - pb) >> B.pad_log);
@@ -326,6 +350,7 @@ static int bin_finish(spmv_plan_s *p, int64_t n, const BinLayout &L) {
     SPMV_RETURN_IF(upload_vec(p, &B.piece_begin, pbeg));
     SPMV_RETURN_IF(upload_vec(p, &B.piece_end, pend));
     SPMV_RETURN_IF(upload_vec(p, &B.run_off, L.run_off));
+    SPMV_RETURN_IF(upload_vec(p, &B.srun_off, L.srun_off));
     SPMV_RETURN_IF(upload_vec(p, &B.bin_row0, L.row0));
     // Product-buffer placement.  The Mul writes 1-KB segments scattered over
     // the whole buffer; with some allocations of the same size it runs ~15 %
@@ -447,7 +472,8 @@ int build_bin_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, 
     const int st = bin_count_device(p, d_rp, d_col, L.row0, bstart, L.S, L.cnt);
     if (st != SPMV_SUCCESS) return st;  // kBinNeedHostBuild: unsorted rows
     bin_offsets(p, o, L);
-    SPMV_RETURN_IF(bin_fill_device(p, d_rp, d_col, d_val, L.row0, bstart, L.cnt, L.off1, L.off2, L.S, L.E));
+    SPMV_RETURN_IF(bin_fill_device(p, d_rp, d_col, d_val, L.row0, bstart, L.cnt, L.off1, L.off2, L.run_off,
+                                   L.srun_off, L.S, L.E, L.ES));
     return bin_finish(p, p->n, L);
 }
 

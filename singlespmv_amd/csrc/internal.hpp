@@ -197,6 +197,19 @@ constexpr int kBinMaxStrip = 20480;  // Mul: x strip of 160 KB of LDS
 // Sum waves per workgroup W2 (4 or 8): a wave's slice holds kBinLdsDoubles/W2
 // doubles = bin rows + one dummy slot (padding entries add +0.0 there)
 inline int bin_max_rows(int w2) { return kBinLdsDoubles / w2 - 1; }
+// Row slots are stored in 8-entry lane groups per Sum batch (64 lanes x U
+// entries, entry (u, lane) = product position base + u*64 + lane): the slot
+// of product position e of a run starting at product r0 / slot s0 (a
+// multiple of 64*U) sits at s0 + batch*64U + (u/8)*512 + lane*8 + u%8, so a
+// lane reads its U slots as U/8 16-byte loads, each load instruction of the
+// wave covering 1 KB contiguously.
+__host__ __device__ inline int64_t bin_slot_index(int64_t e, int64_t r0, int64_t s0, int U) {
+    if (U == 0) return s0 + (e - r0);  // linear (ablation)
+    const int64_t rel = e - r0, step = 64 * (int64_t)U;
+    const int64_t i = rel / step, w = rel - i * step;
+    const int64_t u = w >> 6, lane = w & 63;
+    return s0 + i * step + (u >> 3) * 512 + lane * 8 + (u & 7);
+}
 struct BinDev {
     int strip = 20480;     // x strip width in columns (<= kBinMaxStrip)
     int pad_log = 3;       // segments padded to 2^pad_log entries (8: 64-B product lines)
@@ -217,6 +230,10 @@ struct BinDev {
     uint16_t *slot2 = nullptr;
     int64_t n_blocks = 1;         // strip blocks of the product layout
     int64_t *run_off = nullptr;   // [n_blocks*n_bins + 1]: run (blk, b) of bin b's products
+    int64_t *srun_off = nullptr;  // [n_blocks*n_bins + 1]: its slots (runs padded to 64*sum_u)
+    int sum_u = 32;               // Sum entries per lane per batch (the slot layout's U)
+    bool slot_linear = false;     // ablation: slots in product order (sum_u layout unused)
+    int64_t strip_block = 0;      // strips per block (SB)
     int32_t *bin_row0 = nullptr;  // [n_bins + 1]
     double *prod = nullptr;       // product buffer (largest group)
     int64_t prod_cap = 0;
@@ -286,7 +303,8 @@ int bin_count_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, 
 int bin_fill_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, const double *d_val,
                     const std::vector<int32_t> &row0, const std::vector<int64_t> &bstart,
                     const std::vector<int32_t> &cnt, const std::vector<int64_t> &off1,
-                    const std::vector<int64_t> &off2, int64_t S, int64_t E);
+                    const std::vector<int64_t> &off2, const std::vector<int64_t> &run_off,
+                    const std::vector<int64_t> &srun_off, int64_t S, int64_t E, int64_t ES);
 // k_convert.hip -- device-input builders (the CSR already lives in HBM).
 int validate_csr_device(const int64_t *d_rp, int64_t m, const int32_t *d_col, int64_t nnz, int64_t n);
 int widen_row_ptr_device(const int32_t *d_rp32, int64_t m, int64_t **d_rp64);  // hipMalloc'd; caller frees

@@ -126,19 +126,48 @@ __global__ __launch_bounds__(kBinMulThreads) void bin_mul_kernel(
 template <int U, int MODE>
 struct SumBatch {
     double v[U];
-    uint32_t s[U];
+    // two 16-bit row slots per word, unpacked at the add (MODE 8: one per word)
+    uint32_t w[(MODE & 8) ? U : U / 2];
+    __device__ __forceinline__ uint32_t slot(int u) const {
+        if constexpr ((MODE & 8) != 0) return w[u];
+        else return (w[u >> 1] >> (16 * (u & 1))) & 0xFFFFu;
+    }
 };
 
+typedef uint32_t bin_u32x4 __attribute__((ext_vector_type(4)));
+
+// sbase: the batch's slot block (bin_slot_index): this lane's slots u..u+7
+// are one 16-byte word, the wave's word q one contiguous KB
 template <int U, int MODE>
 __device__ __forceinline__ void sum_load(SumBatch<U, MODE> &B, int64_t base, int64_t p0, int64_t p1, int lane,
-                                         int64_t pbase, const uint16_t *__restrict__ slot2,
+                                         int64_t pbase, int64_t sbase, const uint16_t *__restrict__ slot2,
                                          const double *__restrict__ prod) {
+    static_assert(U % 8 == 0, "slots are read 8 per 16-byte load");
+    // slots first: the adds consume slot word q before product u >= 8q, and
+    // loads complete in issue order
+    if constexpr ((MODE & 8) != 0) {  // ablation: slots in product order, one 2-byte load per entry
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t e = base + u * 64 + lane;
+            B.w[u] = (uint32_t)__builtin_nontemporal_load(slot2 + sbase + (e < p1 ? e : p0) - base);
+        }
+    }
+    const bin_u32x4 *sp = reinterpret_cast<const bin_u32x4 *>(slot2 + sbase + (int64_t)lane * 8);
+#pragma unroll
+    for (int q = 0; q < ((MODE & 12) ? 0 : U / 8); ++q) {
+        const bin_u32x4 w = __builtin_nontemporal_load(sp + q * 64);
+#pragma unroll
+        for (int h = 0; h < 4; ++h) B.w[4 * q + h] = w[h];
+    }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const int64_t e = base + u * 64 + lane;
         const int64_t ee = e < p1 ? e : p0;
         B.v[u] = (MODE & 1) ? ld_stream(prod + (ee - pbase)) : prod[ee - pbase];
-        B.s[u] = (MODE & 4) ? (uint32_t)((ee * 2654435761u) % 4096u) : (uint32_t)__builtin_nontemporal_load(slot2 + ee);
+    }
+    if ((MODE & 12) == 4) {
+#pragma unroll
+        for (int u = 0; u < U / 2; ++u) B.w[u] = (uint32_t)(((base + u * 64 + lane) * 2654435761u) % 4096u);
     }
 }
 
@@ -149,8 +178,8 @@ __device__ __forceinline__ void sum_add(const SumBatch<U, MODE> &B, int64_t base
     for (int u = 0; u < U; ++u) {
         // masked lanes (past the bin) add +0.0 to the dummy slot
         const bool ok = base + u * 64 + lane < p1;
-        if (MODE & 2) sink += B.v[u] * (double)B.s[u];
-        else atomicAdd(&ys[ok ? B.s[u] : DUMMY], ok ? B.v[u] : 0.0);
+        if (MODE & 2) sink += B.v[u] * (double)B.slot(u);
+        else atomicAdd(&ys[ok ? B.slot(u) : DUMMY], ok ? B.v[u] : 0.0);
     }
 }
 
@@ -162,7 +191,8 @@ __device__ __forceinline__ void sum_add(const SumBatch<U, MODE> &B, int64_t base
 template <int W2, int U, int MODE>
 __global__ __launch_bounds__(64 * W2) void bin_sum_kernel(
     int64_t b0, int64_t b1, int64_t nbins, int64_t nblk, const int64_t *__restrict__ run_off,
-    const int32_t *__restrict__ bin_row0, int64_t pbase, const uint16_t *__restrict__ slot2,
+    const int64_t *__restrict__ srun_off, const int32_t *__restrict__ bin_row0, int64_t pbase,
+    const uint16_t *__restrict__ slot2,
     const double *__restrict__ prod, double *__restrict__ y) {
     constexpr int SLICE = kBinLdsDoubles / W2;
     constexpr int64_t STEP = 64 * U;
@@ -176,29 +206,32 @@ __global__ __launch_bounds__(64 * W2) void bin_sum_kernel(
         for (int i = lane; i < rows; i += 64) ys[i] = 0.0;
         double sink = 0.0;
         // run cursor: batch = [pos, min(pos + STEP, end)) of run k
-        int64_t k = 0, pos = run_off[b], end = run_off[b + 1];
-        auto next = [&](int64_t &lo, int64_t &hi) -> bool {
+        // run k of bin b: products from rs, slots from ss (batch-aligned)
+        int64_t k = 0, pos = run_off[b], end = run_off[b + 1], rs = pos, ss = srun_off[b];
+        auto next = [&](int64_t &lo, int64_t &hi, int64_t &sb) -> bool {
             while (pos >= end) {
                 if (++k >= nblk) return false;
-                pos = run_off[k * nbins + b];
+                pos = rs = run_off[k * nbins + b];
                 end = run_off[k * nbins + b + 1];
+                ss = srun_off[k * nbins + b];
             }
             lo = pos;
             hi = pos + STEP < end ? pos + STEP : end;
+            sb = ss + (lo - rs);
             pos = hi;
             return true;
         };
         SumBatch<U, MODE> A, B;
-        int64_t alo, ahi, blo, bhi;
-        bool has_a = next(alo, ahi);
-        if (has_a) sum_load<U, MODE>(A, alo, alo, ahi, lane, pbase, slot2, prod);
+        int64_t alo, ahi, asb, blo, bhi, bsb;
+        bool has_a = next(alo, ahi, asb);
+        if (has_a) sum_load<U, MODE>(A, alo, alo, ahi, lane, pbase, asb, slot2, prod);
         while (has_a) {
-            const bool has_b = next(blo, bhi);
-            if (has_b) sum_load<U, MODE>(B, blo, blo, bhi, lane, pbase, slot2, prod);
+            const bool has_b = next(blo, bhi, bsb);
+            if (has_b) sum_load<U, MODE>(B, blo, blo, bhi, lane, pbase, bsb, slot2, prod);
             sum_add<U, MODE, SLICE - 1>(A, alo, ahi, lane, ys, sink);
             if (!has_b) break;
-            has_a = next(alo, ahi);
-            if (has_a) sum_load<U, MODE>(A, alo, alo, ahi, lane, pbase, slot2, prod);
+            has_a = next(alo, ahi, asb);
+            if (has_a) sum_load<U, MODE>(A, alo, alo, ahi, lane, pbase, asb, slot2, prod);
             sum_add<U, MODE, SLICE - 1>(B, blo, bhi, lane, ys, sink);
         }
         if ((MODE & 2) && sink == 1.2345e300) ys[0] = sink;
@@ -244,7 +277,7 @@ static void launch_sum_t(const spmv_plan_s *p, int g, double *y) {
     const int64_t b0 = g < 0 ? 0 : B.g_bin[g], b1 = g < 0 ? B.n_bins : B.g_bin[g + 1];
     const int64_t pbase = g < 0 ? 0 : B.g_prod[g];
     hipLaunchKernelGGL((bin_sum_kernel<W2, U, MODE>), dim3((unsigned)B.nwg2), dim3(64 * W2), 0, p->stream, b0, b1,
-                       B.n_bins, B.n_blocks, B.run_off, B.bin_row0, pbase, B.slot2, B.prod, y);
+                       B.n_bins, B.n_blocks, B.run_off, B.srun_off, B.bin_row0, pbase, B.slot2, B.prod, y);
 }
 
 template <int W2, int U>
@@ -257,6 +290,10 @@ static void launch_sum_w(const spmv_plan_s *p, int g, double *y) {
     // default: nontemporal product loads (config 2 Sum 0.308 -> 0.298 ms,
     // neutral at config 3 and the N = 8 shape, profiles/round1/probe/bin_sum_nt_loads.jsonl);
     // bits 2-3 = 1: ordinary loads (ablation)
+    if (p->bin.slot_linear) {  // ablation: slots in product order (SPMV_BIN_SLOT_LINEAR)
+        launch_sum_t<W2, U, 9>(p, g, y);
+        return;
+    }
     switch ((p->bin.dbg >> 2) & 3) {
         case 1: launch_sum_t<W2, U, 0>(p, g, y); break;
         case 2: launch_sum_t<W2, U, 2>(p, g, y); break;

@@ -93,8 +93,9 @@ __global__ __launch_bounds__(256) void bin_place_kernel(
     const int64_t *__restrict__ rp, const int32_t *__restrict__ col, const double *__restrict__ val, int64_t nnz,
     const int64_t *__restrict__ bstart, int64_t NB, const int32_t *__restrict__ row0, int32_t C, int64_t S,
     const int64_t *__restrict__ off1, const int64_t *__restrict__ off2, const int64_t *__restrict__ ks,
-    unsigned long long *__restrict__ cur, const int64_t *__restrict__ pbb, int pad_log, double *__restrict__ val1,
-    uint16_t *__restrict__ cs1, uint16_t *__restrict__ slot2, int32_t *__restrict__ dst1) {
+    unsigned long long *__restrict__ cur, const int64_t *__restrict__ pbb, int pad_log,
+    const int64_t *__restrict__ run_off, const int64_t *__restrict__ srun_off, int64_t SB, int sum_u,
+    double *__restrict__ val1, uint16_t *__restrict__ cs1, uint16_t *__restrict__ slot2, int32_t *__restrict__ dst1) {
     for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < nnz; j += (int64_t)gridDim.x * 256) {
         const EntryPos e = locate(j, rp, bstart, NB, row0);
         const int32_t c = col[j];
@@ -105,7 +106,8 @@ __global__ __launch_bounds__(256) void bin_place_kernel(
         const int64_t pos = (ks[o2 + k] - ks[o2]) + (int64_t)atomicAdd(&cur[o2 + k], 1ull);
         val1[o1 + pos] = val[j];
         cs1[o1 + pos] = (uint16_t)(c - t * C);
-        slot2[o2 + pos] = (uint16_t)(e.r - row0[e.b]);
+        const int64_t run = (t / SB) * NB + e.b;
+        slot2[bin_slot_index(o2 + pos, run_off[run], srun_off[run], sum_u)] = (uint16_t)(e.r - row0[e.b]);
         // every 2^pad_log group of a segment starts with a real entry
         if ((pos & ((1 << pad_log) - 1)) == 0) dst1[(o1 + pos) >> pad_log] = (int32_t)((o2 + pos - pbb[e.b]) >> pad_log);
     }
@@ -113,18 +115,20 @@ __global__ __launch_bounds__(256) void bin_place_kernel(
 
 __global__ __launch_bounds__(256) void bin_pad_kernel(const int32_t *__restrict__ cnt, int64_t nseg,
                                                       const int64_t *__restrict__ off1,
-                                                      const int64_t *__restrict__ off2, int pad_log, int max_rows,
-                                                      double *__restrict__ val1, uint16_t *__restrict__ cs1,
-                                                      uint16_t *__restrict__ slot2) {
+                                                      int pad_log, double *__restrict__ val1,
+                                                      uint16_t *__restrict__ cs1) {
     const int64_t PAD = (int64_t)1 << pad_log;
     for (int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x; s < nseg; s += (int64_t)gridDim.x * 256) {
         const int64_t n0 = cnt[s], n8 = (n0 + PAD - 1) & ~(PAD - 1);
         for (int64_t k = n0; k < n8; ++k) {
             val1[off1[s] + k] = 0.0;
             cs1[off1[s] + k] = 0;
-            slot2[off2[s] + k] = (uint16_t)max_rows;
         }
     }
+}
+
+__global__ __launch_bounds__(256) void fill_u16_kernel(uint16_t *__restrict__ a, int64_t n, uint16_t v) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) a[i] = v;
 }
 
 // hipMalloc'd scratch, freed (after the stream drains) on every exit path
@@ -194,7 +198,8 @@ int bin_count_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, 
 int bin_fill_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, const double *d_val,
                     const std::vector<int32_t> &row0, const std::vector<int64_t> &bstart,
                     const std::vector<int32_t> &cnt, const std::vector<int64_t> &off1,
-                    const std::vector<int64_t> &off2, int64_t S, int64_t E) {
+                    const std::vector<int64_t> &off2, const std::vector<int64_t> &run_off,
+                    const std::vector<int64_t> &srun_off, int64_t S, int64_t E, int64_t ES) {
     BinDev &B = p->bin;
     const hipStream_t st = p->stream;
     const int64_t NB = (int64_t)row0.size() - 1, C = B.strip;
@@ -209,19 +214,24 @@ int bin_fill_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, c
     B.val1 = (double *)q;
     SPMV_RETURN_IF(p->arena.alloc(&q, sizeof(uint16_t) * (size_t)E));
     B.cs1 = (uint16_t *)q;
-    SPMV_RETURN_IF(p->arena.alloc(&q, sizeof(uint16_t) * (size_t)E));
+    SPMV_RETURN_IF(p->arena.alloc(&q, sizeof(uint16_t) * (size_t)std::max<int64_t>(ES, 1)));
     B.slot2 = (uint16_t *)q;
     SPMV_RETURN_IF(p->arena.alloc(&q, sizeof(int32_t) * (size_t)std::max<int64_t>(E >> B.pad_log, 1)));
     B.dst1 = (int32_t *)q;
     Scratch sc{st, {}};
     int32_t *d_row0, *d_cnt;
-    int64_t *d_bstart, *d_off1, *d_off2, *d_pbb, *d_ks;
+    int64_t *d_bstart, *d_off1, *d_off2, *d_pbb, *d_ks, *d_run, *d_srun;
     unsigned long long *d_kh;
     SPMV_RETURN_IF(sc.upload(&d_row0, row0));
     SPMV_RETURN_IF(sc.upload(&d_bstart, bstart));
     SPMV_RETURN_IF(sc.upload(&d_cnt, cnt));
     SPMV_RETURN_IF(sc.upload(&d_off1, off1));
     SPMV_RETURN_IF(sc.upload(&d_off2, off2));
+    SPMV_RETURN_IF(sc.upload(&d_run, run_off));
+    SPMV_RETURN_IF(sc.upload(&d_srun, srun_off));
+    // every slot starts as the dummy slot (segment padding and the padding of
+    // each slot run to whole Sum batches)
+    hipLaunchKernelGGL(fill_u16_kernel, dim3(grid_of(ES)), dim3(256), 0, st, B.slot2, ES, (uint16_t)B.max_rows);
     SPMV_RETURN_IF(sc.upload(&d_pbb, pbb));
     SPMV_RETURN_IF(sc.alloc(&d_kh, (size_t)E));
     SPMV_RETURN_IF(sc.alloc(&d_ks, (size_t)E));
@@ -232,10 +242,11 @@ int bin_fill_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, c
     SPMV_RETURN_IF(exclusive_scan_i64((const int64_t *)d_kh, d_ks, E, st, sc.v));
     SPMV_HIP_TRY(hipMemsetAsync(d_kh, 0, 8 * (size_t)E, st));  // now the k-run cursors
     hipLaunchKernelGGL(bin_place_kernel, dim3(grid), dim3(256), 0, st, d_rp, d_col, d_val, p->nnz, d_bstart, NB,
-                       d_row0, (int32_t)C, S, d_off1, d_off2, d_ks, d_kh, d_pbb, B.pad_log, B.val1, B.cs1, B.slot2,
+                       d_row0, (int32_t)C, S, d_off1, d_off2, d_ks, d_kh, d_pbb, B.pad_log, d_run, d_srun,
+                       B.strip_block, B.slot_linear ? 0 : B.sum_u, B.val1, B.cs1, B.slot2,
                        B.dst1);
-    hipLaunchKernelGGL(bin_pad_kernel, dim3(grid_of(NB * S)), dim3(256), 0, st, d_cnt, NB * S, d_off1, d_off2,
-                       B.pad_log, B.max_rows, B.val1, B.cs1, B.slot2);
+    hipLaunchKernelGGL(bin_pad_kernel, dim3(grid_of(NB * S)), dim3(256), 0, st, d_cnt, NB * S, d_off1, B.pad_log,
+                       B.val1, B.cs1);
     return finish(st, "fill");
 }
 
