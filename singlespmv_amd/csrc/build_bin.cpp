@@ -72,10 +72,24 @@ static int bin_params(spmv_plan_s *p, const spmv_options_t &o, int64_t m, int64_
     // (nnz per strip x bin) is ~128 entries at config 2 (pad 16 best) and
     // 16-64 on the N = 2..8 weak-scaling shapes (pad 8 best: 22 % padding
     // instead of 43 % at N = 8, profiles/round1/probe/bin_wide.jsonl)
+    //
+    // Short segments (the N = 4 and N = 8 rank shapes: 42 and 21 entries at
+    // 4 waves) take 2 Sum waves per workgroup instead: 10239-row bins double
+    // the segments, so the Mul streams less padding (N = 8 shape: Mul
+    // 0.83 -> 0.74-0.77 ms, Sum 0.33 -> 0.35, total 1.155 -> 1.09-1.12 ms;
+    // N = 4: 1.00 -> 0.97-1.00; N = 2 and config 2 stay faster with 4,
+    // profiles/round1/probe/bin_sum_waves_wide.jsonl)
     {
         const int64_t S0 = std::max<int64_t>(1, (n + C - 1) / C);
-        const int64_t NB0 = std::max<int64_t>(1, (m + bin_max_rows(B.sum_waves) - 1) / bin_max_rows(B.sum_waves));
-        const double seg = (double)nnz / ((double)S0 * (double)NB0);
+        auto seg_for = [&](int w) {
+            const int64_t NB0 = std::max<int64_t>(1, (m + bin_max_rows(w) - 1) / bin_max_rows(w));
+            return (double)nnz / ((double)S0 * (double)NB0);
+        };
+        double seg = seg_for(4);
+        if (seg < 60.0) {
+            B.sum_waves = 2;
+            seg = seg_for(2);
+        }
         B.pad_log = seg >= 96.0 ? 4 : 3;
     }
     if (const char *e = std::getenv("SPMV_BIN_PADLOG")) B.pad_log = std::min(5, std::max(3, std::atoi(e)));

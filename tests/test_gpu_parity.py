@@ -644,7 +644,8 @@ def test_bin_refuses_huge_sparse_grid_and_auto_avoids_it():
     nearly empty (all padding) -- AUTO does not pick BIN; a segment grid
     beyond 2^28 is refused with NOT_SUPPORTED."""
     rng = np.random.default_rng(3)
-    m, n, per = 16_000_000, 2_000_000_000, 2  # 4096 bins x 97657 strips > 2^28
+    # short segments -> 2 Sum waves, 10239-row bins: 3584 bins x 97657 strips > 2^28
+    m, n, per = 32_000_000, 2_000_000_000, 2
     rp = np.arange(0, per * m + 1, per, dtype=np.int64)
     col = np.sort(rng.integers(0, n, size=(m, per)), axis=1).astype(np.int32).ravel()
     val = rng.random(per * m)
