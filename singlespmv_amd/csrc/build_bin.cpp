@@ -391,12 +391,21 @@ static int bin_finish(spmv_plan_s *p, int64_t n, const BinLayout &L) {
         // spaced ones fast, profiles/round1/probe/bin_placement_spacers.jsonl).
         // Spacers only when the device has room for them with 8 GB to spare.
         int64_t gap_mb = 16384;
-        if (const char *e = std::getenv("SPMV_BIN_PLACEMENT_GAP_MB")) gap_mb = std::atoll(e);
+        const char *gap_env = std::getenv("SPMV_BIN_PLACEMENT_GAP_MB");
+        if (gap_env) gap_mb = std::atoll(gap_env);
         {
             size_t free_b = 0, total_b = 0;
             if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) {
                 (void)hipGetLastError();
                 free_b = 0;
+            }
+            // spread the candidates over all free memory (gaps of at least
+            // 16 GB): memory freed by an earlier plan's search tends to be
+            // the slow kind, and equal 16 GB steps left every candidate of
+            // a second plan inside it (bin_placement_k8_default.txt)
+            if (!gap_env && K > 1) {
+                const size_t rest = (size_t)K * prod_bytes + ((size_t)8 << 30);
+                if (free_b > rest) gap_mb = std::max<int64_t>(gap_mb, (int64_t)((free_b - rest) / (size_t)(K - 1) >> 20));
             }
             // as many spaced candidates as fit (at least 2), else 4 unspaced
             auto need = [&](int k) {
