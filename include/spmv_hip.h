@@ -103,7 +103,13 @@ typedef struct spmv_options {
 /* Fill `opt` with defaults (AUTO format, current device, auto tuning). */
 void spmv_options_default(spmv_options_t *opt);
 
-/* Plan from a host sorted COO (the reference SpMat, src/util.h:7-19).
+/* Plan builds are untimed setup (OptimizeProblem, src/main.cpp:36).  BIN and
+ * DIA plans whose largest buffer exceeds 256 MB time up to 8 placements of
+ * it (the product buffer / the diagonal values), spread over the free device
+ * memory, and keep the fastest: the build briefly allocates most of the
+ * free HBM and returns it before the create call returns.
+ *
+ * Plan from a host sorted COO (the reference SpMat, src/util.h:7-19).
  * Rows must be sorted ascending (LoadSparseMatrix guarantees it); columns
  * within a row may be in any order, duplicates are summed. */
 int spmv_plan_create_coo(int32_t m, int32_t n, int32_t nnz, const int32_t *row_idx,
