@@ -10,19 +10,27 @@ across calls as in the reference driver, src/main.cpp:36-102); y slices are
 gathered with RCCL all_gather, timed separately ("collective_ms").
 
 A step = one y = A x over the rank's rows (device-resident x and y).  W
-untimed warm-up steps, then K steps bracketed by barrier +
-torch.cuda.synchronize(); the max over ranks is the step time.  The same K
-steps are timed with HIP events on the plan's stream (spmv_time): that
-per-launch duration feeds `roofline.achieved`.
+untimed warm-up steps, then T trials of exactly K steps, each bracketed by
+barrier + torch.cuda.synchronize(); a trial's time is the max over ranks and
+`value` comes from the fastest trial -- the reference driver's "min over
+trials of the mean per call" (src/main.cpp:58-102).  The same K steps are
+timed with HIP events on the plan's stream (spmv_time): that per-launch
+duration feeds `roofline.achieved`.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4]
-                  [--formats auto,csr,ell,ss,hyb] [--no-cpu]
+`--gpus N` with no torchrun environment starts `torch.distributed.run` with N
+ranks (one per GPU) as a child process before anything touches the GPU, and
+exits with the child's return code.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--trials T]
+                  [--config c2|c3|c4] [--formats auto,csr,ell,ss,css] [--no-cpu]
 
 Prints ONE JSON line on rank 0.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -68,10 +76,15 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--trials", type=int, default=5,
+                    help="timed trials of K steps; value = the fastest (src/main.cpp:58-102)")
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--rows", type=int, default=0, help="rows per GPU (default: the config's)")
-    ap.add_argument("--formats", default="auto,csr,ell,ss,css,bin",
+    ap.add_argument("--formats", default="auto,csr,ell,ss,css",
                     help="first entry is the headline plan; the rest are reported alongside")
+    ap.add_argument("--placement", default="search", choices=["search", "plain", "vmm", "auto"],
+                    help="plan-build placement of the BIN product buffer / DIA values (spmv_hip.h "
+                         "SPMV_PLACEMENT_*): the bench owns the GPU, so it asks for the build-time search")
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     ap.add_argument("--cpu-seconds", type=float, default=2.0)
     ap.add_argument("--verify", action="store_true",
@@ -83,8 +96,45 @@ def parse():
     return ap.parse_args()
 
 
+def self_launch(args):
+    """--gpus N outside torchrun: run this script under torch.distributed.run
+    with N ranks (rendezvous on 127.0.0.1) and return its exit code.  Called
+    before any GPU call in this process (device_count() does not initialise
+    the GPU); None = run in-process."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus <= 1 or world == args.gpus or args.sim_world:
+        return None
+    if "WORLD_SIZE" in os.environ:
+        print(json.dumps({"error": f"--gpus {args.gpus} inside a launcher with WORLD_SIZE={world}"}))
+        return 2
+    if os.environ.get("BENCH_DIST_BACKEND", "nccl") == "nccl":
+        import torch
+        ndev = torch.cuda.device_count()
+        if ndev < args.gpus:
+            print(json.dumps({"error": f"--gpus {args.gpus} but {ndev} GPUs visible "
+                                       "(BENCH_DIST_BACKEND=gloo shares one GPU between ranks)"}))
+            return 2
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def traffic_key(config: str, m: int, n: int, kernel: str) -> str:
+    """profiles/pmc_traffic*.json key: the PMC bytes of one launch of
+    `kernel` on an m x n rank shape of `config` (none for other shapes)."""
+    return f"{config}:{m}x{n}:{kernel}"
+
+
 def main():
     args = parse()
+    rc = self_launch(args)
+    if rc is not None:
+        return rc
     # host cores of this process, read before any OpenMP runtime pins the
     # main thread to one place
     host_cores = len(os.sched_getaffinity(0))
@@ -110,9 +160,6 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE",
-              file=sys.stderr)
     # BENCH_DIST_BACKEND=gloo lets several ranks share one GPU (development
     # rehearsal of the multi-GPU flow); the driver's runs use nccl = RCCL.
     backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")
@@ -142,6 +189,9 @@ def main():
                        seed=42)
     (row0, row1), rp, col, val = sdist.shard_generated(spec, rank, shape_world)
     nnz_local = int(rp[-1])
+    # total flops of the job: every rank's own nnz (power-law rows make the
+    # equal row blocks unequal in nnz)
+    nnz_total = int(round(sdist.sum_over_ranks([float(nnz_local)], dev)[0]))
     t_gen = time.time() - t0
 
     # x: generated once on rank 0, replicated by RCCL broadcast over xGMI
@@ -164,7 +214,7 @@ def main():
     for fi, fmt in enumerate(fmts):
         tp = time.time()
         try:
-            plan = sp.Plan.from_csr(rows, n_glob, rp, col, val, fmt=fmt, device=local)
+            plan = sp.Plan.from_csr(rows, n_glob, rp, col, val, fmt=fmt, device=local, placement=args.placement)
         except sp.SpmvError as e:
             results[fmt] = {"error": str(e)}
             continue
@@ -176,29 +226,38 @@ def main():
         # warm-up
         if args.warmup:
             plan.time(x, y, args.warmup)
-        torch.cuda.synchronize()
-        if distributed:
-            dist.barrier()
-        torch.cuda.synchronize()
-        tw = time.perf_counter()
-        ev_ms = plan.time(x, y, args.steps)  # K launches between HIP events
-        torch.cuda.synchronize()
-        if distributed:
-            dist.barrier()
-        wall = time.perf_counter() - tw
-        wall_max, ev_max = sdist.max_over_ranks([wall, ev_ms], dev)
+        trials = []  # (max-over-ranks wall s, this rank's event ms)
+        for _ in range(args.trials if fi == 0 else min(args.trials, 2)):
+            torch.cuda.synchronize()
+            if distributed:
+                dist.barrier()
+            torch.cuda.synchronize()
+            tw = time.perf_counter()
+            ev_ms = plan.time(x, y, args.steps)  # K launches between HIP events
+            torch.cuda.synchronize()
+            if distributed:
+                dist.barrier()
+            wall = time.perf_counter() - tw
+            wall_max, _ = sdist.max_over_ranks([wall, ev_ms], dev)
+            trials.append((wall_max, ev_ms))
+        wall_max, ev_ms = min(trials)
         launch_s = ev_ms / 1e3 / args.steps
-        flops_total = 2.0 * nnz_local * world * args.steps
+        flops_total = 2.0 * nnz_total * args.steps
         r = {
             "format": info["format"], "kernel": info["kernel"],
             "gflops": flops_total / wall_max / 1e9,
             "ms_per_step": wall_max / args.steps * 1e3,
+            "trials_ms_per_step": [round(t[0] / args.steps * 1e3, 5) for t in trials],
             "event_ms_per_launch": launch_s * 1e3,
             "achieved_gbs": info["algo_bytes"] / launch_s / 1e9,
             "algo_bytes": info["algo_bytes"], "stored_slots": info["stored_slots"],
             "device_bytes": info["device_bytes"], "plan_build_s": round(t_plan, 3),
             "n_kernels": info["n_kernels"],
+            "placement": info["placement"],
         }
+        if info["placement_candidates"]:
+            r["placement_candidates_ms"] = [round(info["placement_best_ms"], 4), round(info["placement_worst_ms"], 4),
+                                            info["placement_candidates"]]
         relevant = {"csr": ("csr_lanes",), "ss": ("ss_sigma",), "ell": ("ell_width",),
                     "hyb": ("ell_width",), "dia": ("n_diags",), "css": ("css_passes", "css_slabs"),
                     "bin": ("bin_bins", "bin_strips", "bin_strip_cols", "bin_pad", "bin_sum_waves")}
@@ -256,7 +315,7 @@ def main():
         torch.cuda.synchronize()
         dist.barrier()
         t_it = sdist.max_over_ranks([time.perf_counter() - ti], dev)[0] / args.steps
-        iterative = {"ms_per_iter": t_it * 1e3, "gflops": 2.0 * nnz_local * world / t_it / 1e9,
+        iterative = {"ms_per_iter": t_it * 1e3, "gflops": 2.0 * nnz_total / t_it / 1e9,
                      "step": "local SpMV + all_gather(y slices -> next x)"}
         del x_it
         plan.set_stream(stream)
@@ -290,40 +349,34 @@ def main():
             yref = oracle.csr_spmv(grp, gcol, gval, x.cpu().numpy())
             verify_rel = float(np.max(np.abs(y_full - yref) / np.maximum(np.abs(yref), 1e-300)))
 
-    # CPU baseline: the oracle's restatement of opt_crs SpMV (OpenMP, all host
-    # cores of this rank's affinity), reference timing method, rank 0 at N=1
+    # CPU baseline: the oracle's restatement of opt_crs SpMV (src/opt_crs.cpp:
+    # 44-70; OpenMP static over rows, every host core of this process's
+    # affinity, pinned), timed with the reference driver's method
+    # (src/main.cpp:58-102: doubling warm-up to --cpu-seconds, min over 3
+    # trials of the mean per call) on rank 0 at N = 1.  The reference's own
+    # compiled opt_crs never ships to the GPU box; it was
+    # timed beside the port in the build container (profiles/round2/cpu_ref_vs_port.json).
     cpu = None
     max_rel = None
     if rank == 0 and world == 1 and not args.no_cpu:
         import oracle
         nthreads = min(host_cores, int(os.environ.get("OMP_NUM_THREADS", host_cores)))
         x_host = x.cpu().numpy()
-        if oracle.ref_available("crs"):
-            # the reference's own opt_crs (src/opt_crs.cpp, compiled from its
-            # sources into oracle/_ref) under its driver's timing method
-            row_idx = np.repeat(np.arange(rows, dtype=np.int32), np.diff(rp))
-            t_cpu, loop, y_cpu = oracle.ref_time("crs", rows, n_glob, row_idx, col, val, x_host,
-                                                 min_seconds=args.cpu_seconds, ntry=3)
-            # the 1-thread figure BASELINE.md §4 asks for (short doubling
-            # warm-up, one trial: a bounded sample of the same matrix)
-            t_cpu1, _, _ = oracle.ref_time("crs", rows, n_glob, row_idx, col, val, x_host,
-                                           min_seconds=0.5, ntry=1, nthreads=1)
-            del row_idx
-            kind_cpu, what = "reference", "reference opt_crs (src/opt_crs.cpp:44-70) built from its sources"
-        else:
-            t_cpu, loop, y_cpu = oracle.csr_time(rp, col, val, x_host, nthreads=nthreads,
-                                                 min_seconds=args.cpu_seconds, ntry=3)
-            t_cpu1, _, _ = oracle.csr_time(rp, col, val, x_host, nthreads=1, min_seconds=0.5, ntry=1)
-            kind_cpu, what = "port", "oracle opt_crs restatement (OpenMP static)"
+        t_cpu, loop, y_cpu = oracle.csr_time(rp, col, val, x_host, nthreads=nthreads,
+                                             min_seconds=args.cpu_seconds, ntry=3)
+        # the 1-thread figure BASELINE.md §4 asks for (short doubling warm-up,
+        # one trial: a bounded sample of the same matrix)
+        t_cpu1, _, _ = oracle.csr_time(rp, col, val, x_host, nthreads=1, min_seconds=0.5, ntry=1)
         ygpu = y_head.cpu().numpy()
         max_rel = float(np.max(np.abs(ygpu - y_cpu) / np.maximum(np.abs(y_cpu), 1e-300)))
         cpu = {"value": 2.0 * nnz_local / t_cpu / 1e9, "unit": "GFLOP/s", "cores": nthreads,
-               "kind": kind_cpu, "nproc": os.cpu_count(),
+               "kind": "port", "nproc": os.cpu_count(),
                "omp_proc_bind": os.environ.get("OMP_PROC_BIND"),
                "omp_places": os.environ.get("OMP_PLACES"),
-               "sample": f"full {rows}-row matrix, {what}, "
-                         f"{loop} calls x 3 trials after a {args.cpu_seconds:.0f} s doubling warm-up, "
-                         f"min mean per call",
+               "sample": f"full {rows}-row matrix ({nnz_local} nnz), oracle opt_crs restatement "
+                         f"(oracle/oracle.c, src/opt_crs.cpp:44-70), {loop} calls x 3 trials after a "
+                         f"{args.cpu_seconds:.0f} s doubling warm-up, min mean per call, "
+                         f"{nthreads} threads = the host cores of this process's affinity",
                "ms_per_call": t_cpu * 1e3,
                "gbs": (12 * nnz_local + 4 * (rows + 1) + 16 * rows) / t_cpu / 1e9,
                "value_1thread": 2.0 * nnz_local / t_cpu1 / 1e9,
@@ -350,6 +403,8 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
+        "trials": args.trials,
+        "placement": args.placement,
         "ms_per_step": r["ms_per_step"],
         "higher_is_better": True,
         "scaling": "weak",
@@ -357,7 +412,7 @@ def main():
         "dtype": "f64",
         "data": "synthetic (seeded generator, seed 42; x seed 43)",
         "config": {"workload": f"{args.config}: {desc}", "rows_per_gpu": rows,
-                   "m": m_glob, "n": n_glob, "nnz_per_gpu": nnz_local,
+                   "m": m_glob, "n": n_glob, "nnz_per_gpu": nnz_local, "nnz_total": nnz_total,
                    "format": r["format"], "kernel": r["kernel"],
                    "parallelism": f"row-partition x{world}, x replicated (RCCL broadcast)"},
         "achieved_gbs": achieved,
@@ -385,7 +440,7 @@ def main():
     # roofline.traffic: PMC bytes per launch of this kernel/config -- the
     # calibrated figure where one exists (FETCH_SIZE calibrated on a known
     # byte count of the same access pattern), else raw FETCH+WRITE
-    key = f"{args.config}:{rows}:{r['kernel']}"
+    key = traffic_key(args.config, rows, n_glob, r["kernel"])
     for fname, kind in (("pmc_traffic_calibrated.json", "pmc_calibrated"), ("pmc_traffic.json", "pmc_raw")):
         path = os.path.join(ROOT, "profiles", fname)
         try:

@@ -18,6 +18,15 @@
  * x only on the first call (the reference driver never changes x,
  * src/main.cpp:36-102).  y is downloaded on every call (opt_cusparse.cpp:82).
  *
+ * SPMV_HIP_PLACEMENT=search|vmm|plain picks the placement of the BIN product
+ * buffer / DIA values (spmv_hip.h SPMV_PLACEMENT_*; default plain).
+ *
+ * Multi-GPU: SPMV_HIP_GPUS=N (set, N >= 1) makes OptimizeProblem build a dist plan
+ * over devices 0..N-1 (spmv_dist_create_csr: nnz-balanced row ranges, one
+ * plan per device, x broadcast and y all-gathered by RCCL over xGMI) and SpMV
+ * run it -- the unchanged reference driver then spans the node (BASELINE
+ * config 5).  SPMV_HIP_X_RESIDENT applies to the broadcast x the same way.
+ *
  * Errors: the signatures are void, so a failure prints spmv_last_error() and
  * exits, as CUDA_SAFE_CALL does in the reference (src/util.h:48-55).
  */
@@ -37,6 +46,8 @@ struct SpMatOpt {
     int format;       /* resolved spmv_format_t */
     double *d_x;      /* device copy of x (owned by the plan's allocator) */
     int x_uploaded;
+    spmv_dist_t dist; /* SPMV_HIP_GPUS > 1: the multi-GPU plan (plan is NULL) */
+    int n_gpus;
 };
 
 struct VecOpt {

@@ -51,7 +51,7 @@
 extern "C" {
 #endif
 
-#define SPMV_HIP_API_VERSION 1
+#define SPMV_HIP_API_VERSION 2
 
 /* ---- status codes -------------------------------------------------------- */
 typedef enum spmv_status {
@@ -97,17 +97,33 @@ typedef struct spmv_options {
     int32_t css_pace;       /* CSS: 0/1 pace against every XCD, 2 own XCD only */
     int32_t bin_strip_cols;  /* BIN: x strip width, 64..20480 columns (0 = 20480) */
     int32_t bin_groups;      /* BIN: row groups sharing one product buffer (0 = 1) */
-    int32_t reserved[3];
+    int32_t bin_sum_waves;   /* BIN: Sum waves per workgroup 2 | 4 | 8 (0 = auto) */
+    int32_t bin_pad;         /* BIN: segment padding 8 | 16 | 32 entries (0 = auto) */
+    int32_t csr_row_ptr64;   /* CSR: 1 = 64-bit row pointers below 2^31 nnz too */
+    int32_t placement;       /* BIN product buffer / DIA values, see SPMV_PLACEMENT_* */
+    int32_t reserved[4];
 } spmv_options_t;
+
+/* Placement of the large scratch/value buffer of BIN and DIA plans (the BIN
+ * product buffer, the DIA values).  The same launch runs up to ~15 % slower
+ * from some physical HBM regions than from others. */
+#define SPMV_PLACEMENT_AUTO 0   /* = PLAIN                                           */
+#define SPMV_PLACEMENT_PLAIN 1  /* one hipMalloc, nothing timed: create holds no
+                                   device memory beyond the plan's own            */
+#define SPMV_PLACEMENT_SEARCH 2 /* buffers >= 256 MB: up to 8 candidates spread
+                                   over all free HBM, each timed with one launch
+                                   over a zero x, the fastest kept -- create
+                                   briefly holds most of the free device memory;
+                                   for callers that own the GPU (the bench)       */
+#define SPMV_PLACEMENT_VMM 3    /* hipMemCreate handles of 2 MB mapped into one
+                                   VA range                                       */
 
 /* Fill `opt` with defaults (AUTO format, current device, auto tuning). */
 void spmv_options_default(spmv_options_t *opt);
 
-/* Plan builds are untimed setup (OptimizeProblem, src/main.cpp:36).  BIN and
- * DIA plans whose largest buffer exceeds 256 MB time up to 8 placements of
- * it (the product buffer / the diagonal values), spread over the free device
- * memory, and keep the fastest: the build briefly allocates most of the
- * free HBM and returns it before the create call returns.
+/* Plan builds are untimed setup (OptimizeProblem, src/main.cpp:36).  They
+ * allocate the plan's device arrays and nothing else, unless the options ask
+ * for SPMV_PLACEMENT_SEARCH.
  *
  * Plan from a host sorted COO (the reference SpMat, src/util.h:7-19).
  * Rows must be sorted ascending (LoadSparseMatrix guarantees it); columns
@@ -166,9 +182,23 @@ int spmv_stream_probe(int32_t device, int64_t bytes, int32_t iters, double *read
  * gather-bound SpMV), 8 gathers in flight per lane, best of 5 launches. */
 int spmv_gather_probe(int32_t device, int64_t n, int64_t table_bytes, double *g_per_s);
 
+/* Exactness guard of the BIN and CSS formats: `rounds` wave-wide atomic adds
+ * of f64 into 64 LDS slots (one ds_add_f64 instruction each; lane l of round
+ * r adds val[r*64+l] to slot[r*64+l]); out[64] = the slots afterwards.  BIN
+ * and CSS are bit-identical to the sequential opt_crs sum only if lanes of
+ * one instruction that hit the same slot are applied in lane order. */
+int spmv_lds_order_probe(int32_t device, int32_t rounds, const int32_t *slot, const double *val,
+                         double *out);
+
 /* ---- execution ----------------------------------------------------------- */
 #define SPMV_X_DEVICE 0x1u /* x is a device pointer (else host: H2D per call) */
-#define SPMV_Y_DEVICE 0x2u /* y is a device pointer (else host: D2H per call) */
+#define SPMV_Y_DEVICE 0x2u /* y is a device pointer (else host: D2H per call).
+                              COO plans add into y with device f64 atomics
+                              (-munsafe-fp-atomics): a device y must be
+                              ordinary (coarse-grained) device memory, as
+                              hipMalloc returns -- not fine-grained or host-
+                              mapped memory, where those atomics are not
+                              performed atomically                            */
 #define SPMV_ASYNC 0x4u    /* device x and y: return without synchronising    */
 #define SPMV_X_STAGED 0x8u /* re-use the host x uploaded by the previous call
                               (x may be NULL); error if none was staged       */
@@ -214,6 +244,10 @@ typedef struct spmv_plan_info {
     int32_t bin_pad;         /* BIN: segment padding (entries)                 */
     int32_t bin_sum_waves;   /* BIN: Sum waves per workgroup                   */
     int32_t bin_groups;      /* BIN: row groups (Mul launches)                 */
+    int32_t placement;       /* BIN/DIA: the SPMV_PLACEMENT_* the build used   */
+    int32_t placement_candidates; /* SEARCH: candidates timed                  */
+    float placement_best_ms;  /* SEARCH: fastest / slowest candidate launch    */
+    float placement_worst_ms;
 } spmv_plan_info_t;
 
 int spmv_plan_info(spmv_plan_t plan, spmv_plan_info_t *info);
@@ -221,6 +255,43 @@ int spmv_plan_info(spmv_plan_t plan, spmv_plan_info_t *info);
 const char *spmv_status_string(int status);
 /* Detail of the last failure on the calling thread ("" if none). */
 const char *spmv_last_error(void);
+
+/* ---- multi-GPU in one process (new -- the reference is
+ * single-device) -------------------------------------------------------------
+ * The matrix is cut into nnz-balanced row ranges (spmv_partition_rows), one
+ * plan per device over its rows with global column indices (n columns each).
+ * x is copied to the first device and replicated by an RCCL broadcast over
+ * xGMI; every device computes its rows; the y slices (padded to the longest
+ * range) are all-gathered by RCCL into a full y on every device, and the
+ * first device's copy is returned.  A C/C++ caller of the drop-in (the
+ * reference driver, src/main.cpp:36,87) reaches config 5 through it; see
+ * opt_hip.h SPMV_HIP_GPUS. */
+typedef struct spmv_dist_s *spmv_dist_t;
+
+/* The row cut a dist plan uses: cuts[parts+1] (spmv_partition_rows) and the
+ * padded slice length (the longest range, >= 1).  Host only. */
+int spmv_dist_layout(const int64_t *row_ptr, int64_t m, int32_t parts, int64_t *cuts, int64_t *slice_rows);
+
+/* devices: n_devices distinct ordinals, or NULL for 0..n_devices-1.  opt
+ * applies to every per-device plan (opt->device is ignored). */
+int spmv_dist_create_csr(int32_t n_devices, const int32_t *devices, int64_t m, int64_t n, int64_t nnz,
+                         const int64_t *row_ptr, const int32_t *col_idx, const double *val,
+                         const spmv_options_t *opt, spmv_dist_t *dist);
+
+/* y = A x with host x (n doubles) and host y (m doubles; NULL: the result
+ * stays on the devices).  SPMV_X_STAGED: re-use the x broadcast by the
+ * previous call (x may be NULL).  Returns after every device is done. */
+int spmv_dist_execute(spmv_dist_t dist, const double *x, double *y, uint32_t flags);
+
+/* Per-step times over `iters` steps with the staged x: the local SpMV (max
+ * over devices of the event time on each device's stream) and, separately,
+ * the all-gather of the y slices. */
+int spmv_dist_time(spmv_dist_t dist, int32_t iters, double *spmv_ms, double *gather_ms);
+
+/* n_devices, the row cuts (n_devices + 1, optional) and the per-device plans
+ * (optional; owned by the dist plan). */
+int spmv_dist_info(spmv_dist_t dist, int32_t *n_devices, int64_t *cuts, spmv_plan_t *plans);
+int spmv_dist_destroy(spmv_dist_t dist);
 
 /* ---- host utilities ------------------------------------------------------ */
 

@@ -32,7 +32,9 @@ except Exception:  # pragma: no cover - torch is part of the image
     torch = None
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libspmv_hip.so")
+# SPMV_HIP_LIBRARY selects another build of the same C-ABI (the tools/
+# experiments load probes_build/libspmv_hip.so, `make probes`)
+LIB_PATH = os.environ.get("SPMV_HIP_LIBRARY") or os.path.join(HERE, "libspmv_hip.so")
 OPT_LIB_PATH = os.path.join(HERE, "libopt_hip.so")
 
 FORMATS = {"auto": 0, "csr": 1, "crs": 1, "ell": 2, "ss": 3, "dia": 4, "hyb": 5, "css": 6, "coo": 7, "jds": 8, "bin": 9}
@@ -54,7 +56,11 @@ class Options(C.Structure):
                 ("ell_width", C.c_int32), ("ss_sigma", C.c_int32), ("dia_max_diags", C.c_int32),
                 ("dia_max_fill", C.c_double), ("css_slab_shift", C.c_int32), ("css_lag", C.c_int32),
                 ("css_pace", C.c_int32), ("bin_strip_cols", C.c_int32), ("bin_groups", C.c_int32),
-                ("reserved", C.c_int32 * 3)]
+                ("bin_sum_waves", C.c_int32), ("bin_pad", C.c_int32), ("csr_row_ptr64", C.c_int32),
+                ("placement", C.c_int32), ("reserved", C.c_int32 * 4)]
+
+
+PLACEMENTS = {"auto": 0, "plain": 1, "search": 2, "vmm": 3}
 
 
 class PlanInfo(C.Structure):
@@ -65,12 +71,15 @@ class PlanInfo(C.Structure):
                 ("css_passes", C.c_int32), ("css_slabs", C.c_int32), ("n_kernels", C.c_int32), ("overflow_nnz", C.c_int64), ("empty_rows", C.c_int64),
                 ("css_split_rows", C.c_int64), ("kernel", C.c_char * 64),
                 ("bin_bins", C.c_int64), ("bin_strips", C.c_int64), ("bin_strip_cols", C.c_int32),
-                ("bin_pad", C.c_int32), ("bin_sum_waves", C.c_int32), ("bin_groups", C.c_int32)]
+                ("bin_pad", C.c_int32), ("bin_sum_waves", C.c_int32), ("bin_groups", C.c_int32),
+                ("placement", C.c_int32), ("placement_candidates", C.c_int32),
+                ("placement_best_ms", C.c_float), ("placement_worst_ms", C.c_float)]
 
     def as_dict(self):
         d = {k: getattr(self, k) for k, _ in self._fields_}
         d["kernel"] = self.kernel.decode()
         d["format"] = FORMAT_NAMES.get(self.format, str(self.format))
+        d["placement"] = {v: k for k, v in PLACEMENTS.items()}.get(self.placement, str(self.placement))
         return d
 
 
@@ -89,7 +98,8 @@ EXPORTS = [
     "spmv_status_string", "spmv_last_error", "spmv_load_mtx", "spmv_load_mtx_csr", "spmv_free_host",
     "spmv_srand", "spmv_rand_vector", "spmv_verify_coo", "spmv_coo_to_csr", "spmv_gen_count",
     "spmv_gen_fill", "spmv_gen_vector", "spmv_partition_rows", "spmv_save_csr_bin",
-    "spmv_load_csr_bin",
+    "spmv_load_csr_bin", "spmv_lds_order_probe", "spmv_dist_layout", "spmv_dist_create_csr",
+    "spmv_dist_execute", "spmv_dist_time", "spmv_dist_info", "spmv_dist_destroy",
 ]
 
 _lib = None
@@ -120,6 +130,13 @@ def lib():
     L.spmv_profile.argtypes = [vp, vp, vp, i32, C.POINTER(f64), i32, C.POINTER(i32)]
     L.spmv_stream_probe.argtypes = [i32, i64, i32, C.POINTER(f64)]
     L.spmv_gather_probe.argtypes = [i32, i64, i64, C.POINTER(f64)]
+    L.spmv_lds_order_probe.argtypes = [i32, i32, _I32P, _F64P, _F64P]
+    L.spmv_dist_layout.argtypes = [_I64P, i64, i32, _I64P, C.POINTER(i64)]
+    L.spmv_dist_create_csr.argtypes = [i32, vp, i64, i64, i64, vp, vp, vp, C.POINTER(Options), C.POINTER(vp)]
+    L.spmv_dist_execute.argtypes = [vp, vp, vp, C.c_uint32]
+    L.spmv_dist_time.argtypes = [vp, i32, C.POINTER(f64), C.POINTER(f64)]
+    L.spmv_dist_info.argtypes = [vp, C.POINTER(i32), vp, vp]
+    L.spmv_dist_destroy.argtypes = [vp]
     L.spmv_phase_name.argtypes = [vp, i32]
     L.spmv_phase_name.restype = C.c_char_p
     L.spmv_plan_info.argtypes = [vp, C.POINTER(PlanInfo)]
@@ -287,6 +304,19 @@ def gather_probe(device: int = 0, n: int = 64 << 20, table_bytes: int = 1 << 20)
     return g.value
 
 
+def lds_order_probe(slots, vals, device: int = 0) -> np.ndarray:
+    """64 LDS slots after len(slots)//64 wave-wide ds_add_f64 rounds (lane l
+    of round r adds vals[r*64+l] to slots[r*64+l]): the lane-order guarantee
+    BIN and CSS exactness rests on (spmv_lds_order_probe)."""
+    s = np.ascontiguousarray(slots, np.int32)
+    v = np.ascontiguousarray(vals, np.float64)
+    if s.shape != v.shape or s.size == 0 or s.size % 64:
+        raise ValueError("slots and vals: equal length, a positive multiple of 64")
+    out = np.empty(64, np.float64)
+    _check(lib().spmv_lds_order_probe(device, s.size // 64, s, v, out), "spmv_lds_order_probe")
+    return out
+
+
 def coo_to_csr(m: int, row_idx: np.ndarray) -> np.ndarray:
     rp = np.empty(m + 1, np.int64)
     _check(lib().spmv_coo_to_csr(m, len(row_idx), np.ascontiguousarray(row_idx, np.int32), rp),
@@ -298,7 +328,8 @@ def coo_to_csr(m: int, row_idx: np.ndarray) -> np.ndarray:
 def make_options(fmt="auto", device: int = -1, csr_lanes: int = 0, ell_width: int = 0,
                  ss_sigma: int = 0, dia_max_diags: int = 0, dia_max_fill: float = 0.0,
                  css_slab_shift: int = 0, css_lag: int = 0, css_pace: int = 0,
-                 bin_strip_cols: int = 0, bin_groups: int = 0) -> Options:
+                 bin_strip_cols: int = 0, bin_groups: int = 0, bin_sum_waves: int = 0,
+                 bin_pad: int = 0, csr_row_ptr64: bool = False, placement="auto") -> Options:
     o = Options()
     lib().spmv_options_default(C.byref(o))
     o.format = FORMATS[fmt] if isinstance(fmt, str) else int(fmt)
@@ -306,7 +337,40 @@ def make_options(fmt="auto", device: int = -1, csr_lanes: int = 0, ell_width: in
     o.dia_max_diags, o.dia_max_fill = dia_max_diags, dia_max_fill
     o.css_slab_shift, o.css_lag, o.css_pace = css_slab_shift, css_lag, css_pace
     o.bin_strip_cols, o.bin_groups = bin_strip_cols, bin_groups
+    o.bin_sum_waves, o.bin_pad, o.csr_row_ptr64 = bin_sum_waves, bin_pad, 1 if csr_row_ptr64 else 0
+    o.placement = PLACEMENTS[placement] if isinstance(placement, str) else int(placement)
     return o
+
+
+def _check_vec(a, length: int, name: str, device: int, writable: bool) -> None:
+    """A vector handed to the C-ABI: float64, C-contiguous, at least `length`
+    elements, and -- for a device tensor -- on the plan's device.  Raises
+    ValueError instead of letting the kernels or the D2H copy run past it."""
+    if isinstance(a, np.ndarray):
+        if a.dtype != np.float64:
+            raise ValueError(f"{name} must be float64, got {a.dtype}")
+        if not a.flags.c_contiguous:
+            raise ValueError(f"{name} must be C-contiguous")
+        if writable and not a.flags.writeable:
+            raise ValueError(f"{name} is read-only")
+        if a.size < length:
+            raise ValueError(f"{name} holds {a.size} values, the plan needs {length}")
+        return
+    if torch is not None and isinstance(a, torch.Tensor):
+        if a.dtype != torch.float64:
+            raise ValueError(f"{name} must be torch.float64, got {a.dtype}")
+        if not a.is_contiguous():
+            raise ValueError(f"{name} must be contiguous")
+        if a.numel() < length:
+            raise ValueError(f"{name} holds {a.numel()} values, the plan needs {length}")
+        if a.is_cuda and a.device.index != device:
+            raise ValueError(f"{name} is on cuda:{a.device.index}, the plan on cuda:{device}")
+        if not a.is_cuda:
+            raise ValueError(f"{name}: pass CPU data as a numpy array (host buffer)")
+        return
+    if a is None and length == 0:
+        return
+    raise ValueError(f"{name} must be a numpy array or a torch tensor (raw addresses: use the C-ABI)")
 
 
 class Plan:
@@ -315,6 +379,12 @@ class Plan:
     def __init__(self, handle: int, keep=None):
         self._h = C.c_void_p(handle)
         self._keep = keep
+        i = self.info()
+        self.m, self.n, self.device = i["m"], i["n"], i["device"]
+
+    def _check_xy(self, x, y) -> None:
+        _check_vec(x, self.n, "x", self.device, writable=False)
+        _check_vec(y, self.m, "y", self.device, writable=True)
 
     # construction -------------------------------------------------------
     @classmethod
@@ -364,11 +434,10 @@ class Plan:
         """y = alpha * A x (alpha = 1: y = A x).  numpy arrays are host buffers
         (H2D x / D2H y per call, as src/opt_cusparse.cpp:72,82); torch CUDA
         tensors are device buffers."""
+        self._check_xy(x, y)
         flags = (X_DEVICE if _is_device(x) else 0) | (Y_DEVICE if _is_device(y) else 0)
         if async_:
             flags |= ASYNC
-        if isinstance(y, np.ndarray) and not y.flags.c_contiguous:
-            raise ValueError("y must be C-contiguous")
         if alpha == 1.0:
             _check(lib().spmv_execute(self._h, _ptr(x), _ptr(y), flags), "spmv_execute")
         else:
@@ -392,6 +461,9 @@ class Plan:
     def time(self, x_dev, y_dev, iters: int) -> float:
         """Milliseconds for `iters` back-to-back executes (HIP events on the
         plan's stream)."""
+        self._check_xy(x_dev, y_dev)
+        if not (_is_device(x_dev) or self.n == 0) or not (_is_device(y_dev) or self.m == 0):
+            raise ValueError("time() needs device tensors for x and y")
         ms = C.c_double()
         _check(lib().spmv_time(self._h, _ptr(x_dev), _ptr(y_dev), iters, C.byref(ms)), "spmv_time")
         return ms.value
@@ -399,6 +471,9 @@ class Plan:
     def profile(self, x_dev, y_dev, iters: int = 10) -> dict:
         """Mean ms per phase of one execute ({"tile": .., "fixup": ..} for SS),
         the counterpart of the reference's g_profile Mul/Sum split."""
+        self._check_xy(x_dev, y_dev)
+        if not (_is_device(x_dev) or self.n == 0) or not (_is_device(y_dev) or self.m == 0):
+            raise ValueError("profile() needs device tensors for x and y")
         ms = (C.c_double * 8)()
         n = C.c_int32()
         _check(lib().spmv_profile(self._h, _ptr(x_dev), _ptr(y_dev), iters, ms, 8, C.byref(n)),
@@ -414,6 +489,65 @@ class Plan:
     def destroy(self) -> None:
         if self._h is not None and self._h.value:
             lib().spmv_plan_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.destroy()
+        except Exception:
+            pass
+
+
+def dist_layout(row_ptr, parts: int):
+    """(cuts, slice_rows) of a multi-GPU plan over `parts` devices
+    (spmv_dist_layout: nnz-balanced cuts, slices padded to the longest)."""
+    rp = np.ascontiguousarray(row_ptr, np.int64)
+    cuts = np.empty(parts + 1, np.int64)
+    sl = C.c_int64()
+    _check(lib().spmv_dist_layout(rp, len(rp) - 1, parts, cuts, C.byref(sl)), "spmv_dist_layout")
+    return cuts, sl.value
+
+
+class DistPlan:
+    """One process over N local GPUs (spmv_dist_*): row ranges per device,
+    x broadcast and y all-gather by RCCL -- the C-ABI multi-GPU path."""
+
+    def __init__(self, m: int, n: int, row_ptr, col, val, devices, fmt="auto", **opts):
+        rp = np.ascontiguousarray(row_ptr, np.int64)
+        col = np.ascontiguousarray(col, np.int32)
+        val = np.ascontiguousarray(val, np.float64)
+        devs = np.ascontiguousarray(devices, np.int32)
+        o = make_options(fmt, **opts)
+        h = C.c_void_p()
+        _check(lib().spmv_dist_create_csr(len(devs), devs.ctypes.data, m, n, len(val), rp.ctypes.data,
+                                          col.ctypes.data, val.ctypes.data, C.byref(o), C.byref(h)),
+               "spmv_dist_create_csr")
+        self._h, self.m, self.n, self.n_devices = h, m, n, len(devs)
+
+    def execute(self, x, y=None, staged: bool = False) -> None:
+        """y = A x on host arrays (y None: result left on the devices)."""
+        if not staged:
+            _check_vec(x, self.n, "x", -1, writable=False)
+        if y is not None:
+            _check_vec(y, self.m, "y", -1, writable=True)
+        _check(lib().spmv_dist_execute(self._h, None if staged else _ptr(x), _ptr(y), X_STAGED if staged else 0),
+               "spmv_dist_execute")
+
+    def time(self, iters: int):
+        """(local SpMV ms, y all-gather ms) per step, staged x."""
+        a, g = C.c_double(), C.c_double()
+        _check(lib().spmv_dist_time(self._h, iters, C.byref(a), C.byref(g)), "spmv_dist_time")
+        return a.value, g.value
+
+    def cuts(self) -> np.ndarray:
+        nd = C.c_int32()
+        cuts = np.empty(self.n_devices + 1, np.int64)
+        _check(lib().spmv_dist_info(self._h, C.byref(nd), cuts.ctypes.data, None), "spmv_dist_info")
+        return cuts
+
+    def destroy(self) -> None:
+        if self._h is not None and self._h.value:
+            lib().spmv_dist_destroy(self._h)
             self._h = C.c_void_p()
 
     def __del__(self):

@@ -40,13 +40,14 @@ struct BinLayout {
     std::vector<int64_t> srun_off;      // [NBK * NB + 1] slot runs, each padded to 64*sum_u
     int64_t ES = 0, SB = 1;             // slot entries; strips per block
     std::vector<int64_t> strip_start;   // [G * (S + 1)] Mul-order start of (group, strip)
+    std::vector<int64_t> mul_bins;      // [NB] bins in Mul visiting order within each strip (per group)
     int64_t rpad(int64_t v) const { return (v + PAD - 1) & ~(PAD - 1); }
 };
 
 // ---- parameters (strip width, workgroups, padding, Sum waves) -----------
 static int bin_params(spmv_plan_s *p, const spmv_options_t &o, int64_t m, int64_t n, int64_t nnz) {
     BinDev &B = p->bin;
-    if (const char *d = std::getenv("SPMV_BIN_DEBUG")) B.dbg = std::atoi(d);
+    if (const char *d = probe_env("SPMV_BIN_DEBUG")) B.dbg = std::atoi(d);
     int ncu = 0;
     SPMV_HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, p->device));
     if (ncu <= 0) ncu = 256;
@@ -55,7 +56,7 @@ static int bin_params(spmv_plan_s *p, const spmv_options_t &o, int64_t m, int64_
     const int64_t C = B.strip;
     B.nwg1 = ncu;  // one 1024-thread workgroup per CU (the x strip fills the LDS)
     B.nwg2 = ncu;  // 160 KB of LDS y slices per workgroup
-    if (const char *e = std::getenv("SPMV_BIN_CUS")) {  // experiment: a subset of the CUs
+    if (const char *e = probe_env("SPMV_BIN_CUS")) {  // experiment: a subset of the CUs
         const int k = std::atoi(e);
         if (k > 0 && k < ncu) {
             B.nwg1 = k;
@@ -92,15 +93,24 @@ static int bin_params(spmv_plan_s *p, const spmv_options_t &o, int64_t m, int64_
         }
         B.pad_log = seg >= 96.0 ? 4 : 3;
     }
-    if (const char *e = std::getenv("SPMV_BIN_PADLOG")) B.pad_log = std::min(5, std::max(3, std::atoi(e)));
-    if (const char *e = std::getenv("SPMV_BIN_SUMWAVES")) {
+    if (o.bin_sum_waves) {
+        SPMV_CHECK_ARG(o.bin_sum_waves == 2 || o.bin_sum_waves == 4 || o.bin_sum_waves == 8,
+                       "bin_sum_waves must be 0, 2, 4 or 8");
+        B.sum_waves = o.bin_sum_waves;
+    }
+    if (o.bin_pad) {
+        SPMV_CHECK_ARG(o.bin_pad == 8 || o.bin_pad == 16 || o.bin_pad == 32, "bin_pad must be 0, 8, 16 or 32");
+        B.pad_log = o.bin_pad == 8 ? 3 : o.bin_pad == 16 ? 4 : 5;
+    }
+    if (const char *e = probe_env("SPMV_BIN_PADLOG")) B.pad_log = std::min(5, std::max(3, std::atoi(e)));
+    if (const char *e = probe_env("SPMV_BIN_SUMWAVES")) {
         const int w = std::atoi(e);
         B.sum_waves = w == 2 || w == 4 ? w : 8;
     }
     B.max_rows = bin_max_rows(B.sum_waves);
     B.sum_u = B.sum_waves == 8 ? 8 : 32;  // must match launch_sum's <W2, U> pairs
     B.slot_linear = false;
-    if (const char *e = std::getenv("SPMV_BIN_SLOT_LINEAR")) B.slot_linear = std::atoi(e) != 0;
+    if (const char *e = probe_env("SPMV_BIN_SLOT_LINEAR")) B.slot_linear = std::atoi(e) != 0;
     p->algo_bytes = 12 * nnz + 8 * n + 8 * m;
     p->n_kernels = 2;
     p->kernel_name = "bin_mul_kernel+bin_sum_kernel";
@@ -166,7 +176,7 @@ static void bin_offsets(spmv_plan_s *p, const spmv_options_t &o, BinLayout &L) {
     int G = o.bin_groups > 0 ? o.bin_groups : 1;
     if (G > NB) G = (int)NB;
     B.G = G;
-    if (const char *e = std::getenv("SPMV_BIN_REUSE")) B.reuse = std::atoi(e) != 0;
+    if (const char *e = probe_env("SPMV_BIN_REUSE")) B.reuse = std::atoi(e) != 0;
     B.g_bin.assign((size_t)G + 1, NB);
     B.g_prod.assign((size_t)G + 1, E);
     B.g_bin[0] = 0;
@@ -189,7 +199,7 @@ static void bin_offsets(spmv_plan_s *p, const spmv_options_t &o, BinLayout &L) {
     // ms at SB = S, 0.37 at 32, 0.67 at 8), so the default is SB = S: one
     // block, the plain bin-major layout.
     int64_t SB = S;
-    if (const char *e = std::getenv("SPMV_BIN_SB")) SB = std::max<int64_t>(1, std::atoll(e));
+    if (const char *e = probe_env("SPMV_BIN_SB")) SB = std::max<int64_t>(1, std::atoll(e));
     if (B.reuse || SB > S) SB = S;
     const int64_t NBK = (S + SB - 1) / SB;
     B.n_blocks = NBK;
@@ -222,12 +232,29 @@ static void bin_offsets(spmv_plan_s *p, const spmv_options_t &o, BinLayout &L) {
         L.SB = SB;
         B.strip_block = SB;
     }
+    // The Mul visits the bins of a strip in a scrambled order (b -> b * P mod
+    // bins, P coprime, near the golden ratio of the group's bin count), so the
+    // product segments it writes one after the other land far apart and in no
+    // regular stride in the Sum-ordered buffer (in bin order they sit one
+    // bin's product run apart).
+    L.mul_bins.resize((size_t)NB);
+    if (const char *e = probe_env("SPMV_BIN_MUL_PERM")) B.mul_perm = std::atoi(e) != 0;
+    for (int g = 0; g < G; ++g) {
+        const int64_t g0 = B.g_bin[(size_t)g], nbg = B.g_bin[(size_t)g + 1] - g0;
+        int64_t P = 1;
+        if (B.mul_perm && nbg > 2) {
+            P = std::max<int64_t>(1, (int64_t)(0.6180339887 * (double)nbg)) | 1;
+            while (std::__gcd(P, nbg) != 1) P += 2;
+        }
+        for (int64_t i = 0; i < nbg; ++i) L.mul_bins[(size_t)(g0 + i)] = g0 + (int64_t)(((__int128)i * P) % nbg);
+    }
     L.strip_start.assign((size_t)G * (S + 1), 0);
     for (int g = 0; g < G; ++g) {
         int64_t cur = B.g_prod[(size_t)g];
         for (int64_t t = 0; t < S; ++t) {
             L.strip_start[(size_t)(g * (S + 1) + t)] = cur;
-            for (int64_t b = B.g_bin[(size_t)g]; b < B.g_bin[(size_t)g + 1]; ++b) {
+            for (int64_t i = B.g_bin[(size_t)g]; i < B.g_bin[(size_t)g + 1]; ++i) {
+                const int64_t b = L.mul_bins[(size_t)i];
                 L.off1[(size_t)(b * S + t)] = cur;
                 cur += L.rpad(L.cnt[(size_t)(b * S + t)]);
             }
@@ -318,8 +345,139 @@ static int bin_fill_host(spmv_plan_s *p, const HostCsr &A, const BinLayout &L) {
     return SPMV_SUCCESS;
 }
 
-// ---- Mul pieces, small tables, product buffer (placement search) -----------
-static int bin_finish(spmv_plan_s *p, int64_t n, const BinLayout &L) {
+// ---- product buffer placement ---------------------------------------------
+// The Mul writes 1-KB segments scattered over the whole product buffer; with
+// some allocations of the same size it runs ~15 % slower (config 2: 0.66 vs
+// 0.56 ms for ONE plan whose buffer was re-allocated between timings,
+// profiles/round1/probe/bin_realloc.jsonl).
+
+static int alloc_prod_plain(spmv_plan_s *p, size_t prod_bytes) {
+    // (hipDeviceMallocContiguous was tried for the product buffer: plans built
+    // after another plan was freed returned WRONG sums -- the buffer behaved
+    // as if aliased -- so it is not used; tools/dbg_bin.py reproduces it.)
+    void *q = nullptr;
+    SPMV_RETURN_IF(p->arena.alloc(&q, prod_bytes));
+    p->bin.prod = (double *)q;
+    return SPMV_SUCCESS;
+}
+
+// SPMV_PLACEMENT_SEARCH: keep the fastest of up to K candidates, each timed
+// with a Mul pass over a zero x at build time (results never depend on it).
+// Up to 8 candidates: best-of-4 still left 5 of 9 config-2 plans in the slow
+// mode, best-of-8 1 of 9 (profiles/round1/probe/bin_placement_k8.txt).
+static int bin_place_search(spmv_plan_s *p, int64_t n, size_t prod_bytes) {
+    BinDev &B = p->bin;
+    int K = 8;
+    if (const char *e = probe_env("SPMV_BIN_PLACEMENT")) K = std::max(1, std::min(12, std::atoi(e)));
+    if (K == 1) return alloc_prod_plain(p, prod_bytes);
+    double *xz = nullptr;
+    SPMV_HIP_TRY(hipMalloc(&xz, sizeof(double) * (size_t)std::max<int64_t>(n, 1)));
+    if (hipMemset(xz, 0, sizeof(double) * (size_t)std::max<int64_t>(n, 1)) != hipSuccess) {
+        (void)hipFree(xz);
+        SPMV_HIP_TRY(hipGetLastError());
+    }
+    std::vector<double *> cand;
+    std::vector<float> t;
+    int st = SPMV_SUCCESS;
+    // Consecutive allocations tend to share the fast or the slow mode;
+    // candidates spaced by 16 GB spacer allocations land in different
+    // regions of device memory (all 6 unspaced candidates slow, 3 of 6
+    // spaced ones fast, profiles/round1/probe/bin_placement_spacers.jsonl).
+    // Spacers only when the device has room for them with 8 GB to spare.
+    int64_t gap_mb = 16384;
+    const char *gap_env = probe_env("SPMV_BIN_PLACEMENT_GAP_MB");
+    if (gap_env) gap_mb = std::atoll(gap_env);
+    {
+        size_t free_b = 0, total_b = 0;
+        if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) {
+            (void)hipGetLastError();
+            free_b = 0;
+        }
+        // spread the candidates over all free memory (gaps of at least
+        // 16 GB): memory freed by an earlier plan's search tends to be
+        // the slow kind, and equal 16 GB steps left every candidate of
+        // a second plan inside it (bin_placement_k8_default.txt)
+        if (!gap_env) {
+            const size_t rest = (size_t)K * prod_bytes + ((size_t)8 << 30);
+            if (free_b > rest) gap_mb = std::max<int64_t>(gap_mb, (int64_t)((free_b - rest) / (size_t)(K - 1) >> 20));
+        }
+        // as many spaced candidates as fit (at least 2), else 4 unspaced
+        auto need = [&](int k) {
+            return (size_t)(k - 1) * ((size_t)gap_mb << 20) + (size_t)k * prod_bytes + ((size_t)8 << 30);
+        };
+        while (K > 2 && free_b < need(K)) --K;
+        if (free_b < need(K)) {
+            gap_mb = 0;
+            K = std::min(K, 4);
+        }
+    }
+    std::vector<void *> spacers;
+    for (int k = 0; k < K; ++k) {
+        if (k > 0 && gap_mb > 0) {
+            void *g = nullptr;
+            if (hipMalloc(&g, (size_t)gap_mb << 20) == hipSuccess) spacers.push_back(g);
+            else (void)hipGetLastError();
+        }
+        if (alloc_prod_plain(p, prod_bytes) != SPMV_SUCCESS) {
+            // out of room for another candidate: rank the ones timed so far
+            (void)hipGetLastError();
+            break;
+        }
+        cand.push_back(B.prod);
+        float ms = 0;
+        st = bin_time_mul(p, xz, &ms);
+        if (st != SPMV_SUCCESS) break;  // a failed timing is never ranked
+        t.push_back(ms);
+        // the modes differ by ~15 %: once both have been seen, stop
+        if (k >= 3 && *std::min_element(t.begin(), t.end()) < 0.93f * *std::max_element(t.begin(), t.end()))
+            break;
+    }
+    for (void *g : spacers) (void)hipFree(g);
+    (void)hipFree(xz);
+    if (st != SPMV_SUCCESS || t.empty()) {
+        for (double *c : cand) p->arena.free(c);
+        B.prod = nullptr;
+        if (st == SPMV_SUCCESS) {
+            set_error("BIN: no product buffer could be allocated");
+            st = SPMV_ERROR_OUT_OF_MEMORY;
+        }
+        return st;
+    }
+    const size_t best = (size_t)(std::min_element(t.begin(), t.end()) - t.begin());
+    for (size_t k = 0; k < cand.size(); ++k)
+        if (k != best) p->arena.free(cand[k]);
+    B.prod = cand[best];
+    B.placement_ms.assign(t.begin(), t.end());
+    return SPMV_SUCCESS;
+}
+
+static int bin_place_prod(spmv_plan_s *p, int64_t n, size_t prod_bytes, const spmv_options_t &o) {
+    BinDev &B = p->bin;
+    int mode = o.placement;
+    SPMV_CHECK_ARG(mode >= SPMV_PLACEMENT_AUTO && mode <= SPMV_PLACEMENT_VMM, "unknown placement mode");
+    if (const char *e = probe_env("SPMV_PLACEMENT_MODE")) mode = std::atoi(e);
+    // AUTO = one plain allocation: no transient memory beyond the plan.  The
+    // search is opt-in (SPMV_PLACEMENT_SEARCH) -- it is the only method that
+    // found the Mul's fast mode reliably, but it briefly holds most of the
+    // free HBM; VMM 2-MB handles were fast on some boxes and not on others
+    // (profiles/round2/placement/, DESIGN §4a "Placement").
+    if (mode == SPMV_PLACEMENT_AUTO) mode = SPMV_PLACEMENT_PLAIN;
+    if (mode == SPMV_PLACEMENT_SEARCH && prod_bytes < ((size_t)256 << 20)) mode = SPMV_PLACEMENT_PLAIN;
+    B.placement = mode;
+    if (mode == SPMV_PLACEMENT_SEARCH) return bin_place_search(p, n, prod_bytes);
+    if (mode == SPMV_PLACEMENT_VMM) {
+        size_t chunk = (size_t)2 << 20;
+        if (const char *e = probe_env("SPMV_VMM_CHUNK_MB")) chunk = (size_t)std::max(1, std::atoi(e)) << 20;
+        void *q = nullptr;
+        SPMV_RETURN_IF(p->arena.alloc_vmm(&q, prod_bytes, chunk, p->device));
+        B.prod = (double *)q;
+        return SPMV_SUCCESS;
+    }
+    return alloc_prod_plain(p, prod_bytes);
+}
+
+// ---- Mul pieces, small tables, product buffer -----------------------------
+static int bin_finish(spmv_plan_s *p, int64_t n, const BinLayout &L, const spmv_options_t &o) {
     BinDev &B = p->bin;
     const int64_t S = L.S, E = L.E;
     // Mul pieces: each workgroup takes an nnz-balanced range of its group's
@@ -349,16 +507,6 @@ static int bin_finish(spmv_plan_s *p, int64_t n, const BinLayout &L) {
     if (B.reuse)
         for (int g = 0; g < B.G; ++g) B.prod_cap = std::max(B.prod_cap, B.g_prod[(size_t)g + 1] - B.g_prod[(size_t)g]);
     const size_t prod_bytes = sizeof(double) * (size_t)std::max<int64_t>(B.prod_cap, 1);
-    auto alloc_prod = [&]() -> int {
-        // plain hipMalloc.  (hipDeviceMallocContiguous was tried for the
-        // product buffer: plans built after another plan was freed returned
-        // WRONG sums -- the buffer behaved as if aliased -- so it is not used;
-        // tools/dbg_bin.py reproduces it.)
-        void *q = nullptr;
-        SPMV_RETURN_IF(p->arena.alloc(&q, prod_bytes));
-        B.prod = (double *)q;
-        return SPMV_SUCCESS;
-    };
     SPMV_RETURN_IF(upload_vec(p, &B.piece_off, piece_off));
     SPMV_RETURN_IF(upload_vec(p, &B.piece_strip, pstrip));
     SPMV_RETURN_IF(upload_vec(p, &B.piece_begin, pbeg));
@@ -366,84 +514,7 @@ static int bin_finish(spmv_plan_s *p, int64_t n, const BinLayout &L) {
     SPMV_RETURN_IF(upload_vec(p, &B.run_off, L.run_off));
     SPMV_RETURN_IF(upload_vec(p, &B.srun_off, L.srun_off));
     SPMV_RETURN_IF(upload_vec(p, &B.bin_row0, L.row0));
-    // Product-buffer placement.  The Mul writes 1-KB segments scattered over
-    // the whole buffer; with some allocations of the same size it runs ~15 %
-    // slower (config 2: 0.66 vs 0.56 ms for ONE plan whose buffer was
-    // re-allocated between timings, profiles/round1/probe/bin_realloc.jsonl).
-    // For large buffers keep the fastest of K candidates, each timed with a
-    // Mul pass over a zero x at build time (results never depend on it).
-    // Up to 8 candidates: best-of-4 still left 5 of 9 config-2 plans in the
-    // slow mode, best-of-8 1 of 9 (profiles/round1/probe/bin_placement_k8.txt).
-    int K = prod_bytes >= ((size_t)256 << 20) ? 8 : 1;
-    if (const char *e = std::getenv("SPMV_BIN_PLACEMENT")) K = std::max(1, std::min(12, std::atoi(e)));
-    if (K == 1) {
-        SPMV_RETURN_IF(alloc_prod());
-    } else {
-        double *xz = nullptr;
-        SPMV_HIP_TRY(hipMalloc(&xz, sizeof(double) * (size_t)std::max<int64_t>(n, 1)));
-        SPMV_HIP_TRY(hipMemset(xz, 0, sizeof(double) * (size_t)std::max<int64_t>(n, 1)));
-        std::vector<double *> cand;
-        std::vector<float> t;
-        int st = SPMV_SUCCESS;
-        // Consecutive allocations tend to share the fast or the slow mode;
-        // candidates spaced by 16 GB spacer allocations land in different
-        // regions of device memory (all 6 unspaced candidates slow, 3 of 6
-        // spaced ones fast, profiles/round1/probe/bin_placement_spacers.jsonl).
-        // Spacers only when the device has room for them with 8 GB to spare.
-        int64_t gap_mb = 16384;
-        const char *gap_env = std::getenv("SPMV_BIN_PLACEMENT_GAP_MB");
-        if (gap_env) gap_mb = std::atoll(gap_env);
-        {
-            size_t free_b = 0, total_b = 0;
-            if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) {
-                (void)hipGetLastError();
-                free_b = 0;
-            }
-            // spread the candidates over all free memory (gaps of at least
-            // 16 GB): memory freed by an earlier plan's search tends to be
-            // the slow kind, and equal 16 GB steps left every candidate of
-            // a second plan inside it (bin_placement_k8_default.txt)
-            if (!gap_env && K > 1) {
-                const size_t rest = (size_t)K * prod_bytes + ((size_t)8 << 30);
-                if (free_b > rest) gap_mb = std::max<int64_t>(gap_mb, (int64_t)((free_b - rest) / (size_t)(K - 1) >> 20));
-            }
-            // as many spaced candidates as fit (at least 2), else 4 unspaced
-            auto need = [&](int k) {
-                return (size_t)(k - 1) * ((size_t)gap_mb << 20) + (size_t)k * prod_bytes + ((size_t)8 << 30);
-            };
-            while (K > 2 && free_b < need(K)) --K;
-            if (free_b < need(K)) {
-                gap_mb = 0;
-                K = std::min(K, 4);
-            }
-        }
-        std::vector<void *> spacers;
-        for (int k = 0; k < K && st == SPMV_SUCCESS; ++k) {
-            if (k > 0 && gap_mb > 0) {
-                void *g = nullptr;
-                if (hipMalloc(&g, (size_t)gap_mb << 20) == hipSuccess) spacers.push_back(g);
-                else (void)hipGetLastError();
-            }
-            st = alloc_prod();
-            if (st != SPMV_SUCCESS) break;
-            float ms = 0;
-            st = bin_time_mul(p, xz, &ms);
-            cand.push_back(B.prod);
-            t.push_back(ms);
-            // the modes differ by ~15 %: once both have been seen, stop
-            if (k >= 3 && *std::min_element(t.begin(), t.end()) < 0.93f * *std::max_element(t.begin(), t.end()))
-                break;
-        }
-        for (void *g : spacers) (void)hipFree(g);
-        (void)hipFree(xz);
-        if (cand.empty()) return st;
-        (void)hipGetLastError();
-        const size_t best = (size_t)(std::min_element(t.begin(), t.end()) - t.begin());
-        for (size_t k = 0; k < cand.size(); ++k)
-            if (k != best) p->arena.free(cand[k]);
-        B.prod = cand[best];
-        B.placement_ms.assign(t.begin(), t.end());
-    }
+    SPMV_RETURN_IF(bin_place_prod(p, n, prod_bytes, o));
     if (B.dbg & 16) {
         std::fprintf(stderr, "[bin] val1 %p cs1 %p dst1 %p slot2 %p prod %p (E %lld) placement ms:", (void *)B.val1,
                      (void *)B.cs1, (void *)B.dst1, (void *)B.slot2, (void *)B.prod, (long long)E);
@@ -474,7 +545,7 @@ int build_bin(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
     }
     bin_offsets(p, o, L);
     SPMV_RETURN_IF(bin_fill_host(p, A, L));
-    return bin_finish(p, A.n, L);
+    return bin_finish(p, A.n, L, o);
 }
 
 int build_bin_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, const double *d_val,
@@ -497,7 +568,7 @@ int build_bin_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, 
     bin_offsets(p, o, L);
     SPMV_RETURN_IF(bin_fill_device(p, d_rp, d_col, d_val, L.row0, bstart, L.cnt, L.off1, L.off2, L.run_off,
                                    L.srun_off, L.S, L.E, L.ES));
-    return bin_finish(p, p->n, L);
+    return bin_finish(p, p->n, L, o);
 }
 
 }  // namespace spmv

@@ -202,7 +202,7 @@ int spmv_plan_create_csr_device(int64_t m, int64_t n, int64_t nnz, const int64_t
     }
     SPMV_RETURN_IF(validate_csr_device(d_row_ptr, m, d_col_idx, nnz, n));
     const bool on_device = o.format == SPMV_FORMAT_CSR || o.format == SPMV_FORMAT_SS ||
-                           (o.format == SPMV_FORMAT_BIN && !std::getenv("SPMV_BIN_HOST_BUILD"));
+                           (o.format == SPMV_FORMAT_BIN && !probe_env("SPMV_BIN_HOST_BUILD"));
     if (on_device) {
         spmv_plan_s *p = new (std::nothrow) spmv_plan_s;
         if (!p) {
@@ -463,6 +463,14 @@ int spmv_bin_realloc_prod(spmv_plan_t p) {
     return 0;
 }
 
+// internal (placement experiments): the BIN product buffer
+int spmv_bin_prod(spmv_plan_t p, void **buf, int64_t *bytes) {
+    if (!p || p->format != SPMV_FORMAT_BIN || !p->bin.prod || !buf || !bytes) return -1;
+    *buf = p->bin.prod;
+    *bytes = 8 * std::max<int64_t>(p->bin.prod_cap, 1);
+    return 0;
+}
+
 int spmv_plan_info(spmv_plan_t p, spmv_plan_info_t *info) {
     SPMV_CHECK_ARG(p != nullptr && info != nullptr, "NULL argument");
     std::memset(info, 0, sizeof(*info));
@@ -493,6 +501,19 @@ int spmv_plan_info(spmv_plan_t p, spmv_plan_info_t *info) {
         info->bin_pad = 1 << p->bin.pad_log;
         info->bin_sum_waves = p->bin.sum_waves;
         info->bin_groups = p->bin.G;
+    }
+    const std::vector<float> *pm = nullptr;
+    if (p->format == SPMV_FORMAT_BIN) {
+        info->placement = p->bin.placement;
+        pm = &p->bin.placement_ms;
+    } else if (p->format == SPMV_FORMAT_DIA) {
+        info->placement = p->dia.placement;
+        pm = &p->dia.placement_ms;
+    }
+    if (pm && !pm->empty()) {
+        info->placement_candidates = (int32_t)pm->size();
+        info->placement_best_ms = *std::min_element(pm->begin(), pm->end());
+        info->placement_worst_ms = *std::max_element(pm->begin(), pm->end());
     }
     return SPMV_SUCCESS;
 }

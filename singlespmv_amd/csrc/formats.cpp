@@ -32,7 +32,89 @@ int DevArena::alloc(void **p, size_t n) {
     return SPMV_SUCCESS;
 }
 
+// Physical memory in `chunk`-byte handles (hipMemCreate) mapped back to back
+// into one reserved VA range.  chunk is rounded to the allocation granularity.
+int DevArena::alloc_vmm(void **p, size_t n, size_t chunk, int device) {
+    hipMemAllocationProp prop = {};
+    prop.type = hipMemAllocationTypePinned;
+    prop.location.type = hipMemLocationTypeDevice;
+    prop.location.id = device;
+    size_t gran = 0;
+    SPMV_HIP_TRY(hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityRecommended));
+    if (gran == 0) gran = (size_t)2 << 20;
+    if (n == 0) n = 16;
+    const size_t need = (n + gran - 1) / gran * gran;
+    chunk = std::min(need, std::max(gran, (chunk + gran - 1) / gran * gran));
+    const size_t total = (n + chunk - 1) / chunk * chunk;
+    VmmMap m;
+    m.bytes = total;
+    m.chunk = chunk;
+    auto undo = [&](hipError_t e, const char *what) {
+        set_error(std::string(what) + ": " + hipGetErrorString(e));
+        (void)hipGetLastError();
+        for (size_t k = 0; k < m.handles.size(); ++k) {
+            (void)hipMemUnmap((char *)m.va + k * chunk, chunk);
+            (void)hipMemRelease(m.handles[k]);
+        }
+        if (m.va) (void)hipMemAddressFree(m.va, total);
+        return e == hipErrorOutOfMemory ? SPMV_ERROR_OUT_OF_MEMORY : SPMV_ERROR_HIP;
+    };
+    hipError_t e = hipMemAddressReserve(&m.va, total, gran, nullptr, 0);
+    if (e != hipSuccess) return undo(e, "hipMemAddressReserve");
+    // all handles first, then mapped -- in creation order, or (probe build,
+    // SPMV_VMM_SHUFFLE) handle k at chunk slot k * P mod count
+    const size_t cnt = total / chunk;
+    for (size_t k = 0; k < cnt; ++k) {
+        hipMemGenericAllocationHandle_t h;
+        e = hipMemCreate(&h, chunk, &prop, 0);
+        if (e != hipSuccess) return undo(e, "hipMemCreate");
+        m.handles.push_back(h);
+    }
+    size_t P = 1;
+    if (const char *sh = probe_env("SPMV_VMM_SHUFFLE"))
+        if (std::atoi(sh) && cnt > 2) {
+            P = (size_t)(0.6180339887 * (double)cnt) | 1;
+            while (std::gcd(P, cnt) != 1) P += 2;
+        }
+    std::vector<hipMemGenericAllocationHandle_t> slot(cnt);
+    for (size_t k = 0; k < cnt; ++k) slot[(k * P) % cnt] = m.handles[k];
+    m.handles = slot;  // handles[k] is mapped at chunk slot k
+    for (size_t k = 0; k < cnt; ++k) {
+        e = hipMemMap((char *)m.va + k * chunk, chunk, 0, m.handles[k], 0);
+        if (e != hipSuccess) {
+            for (size_t j = k; j < cnt; ++j) (void)hipMemRelease(m.handles[j]);
+            m.handles.resize(k);
+            return undo(e, "hipMemMap");
+        }
+    }
+    hipMemAccessDesc acc = {};
+    acc.location = prop.location;
+    acc.flags = hipMemAccessFlagsProtReadWrite;
+    e = hipMemSetAccess(m.va, total, &acc, 1);
+    if (e != hipSuccess) return undo(e, "hipMemSetAccess");
+    maps.push_back(m);
+    bytes += (int64_t)total;
+    *p = m.va;
+    return SPMV_SUCCESS;
+}
+
+static void vmm_release(const VmmMap &m) {
+    (void)hipDeviceSynchronize();
+    for (size_t k = 0; k < m.handles.size(); ++k) {
+        (void)hipMemUnmap((char *)m.va + k * m.chunk, m.chunk);
+        (void)hipMemRelease(m.handles[k]);
+    }
+    (void)hipMemAddressFree(m.va, m.bytes);
+}
+
 void DevArena::free(void *p) {
+    for (size_t i = 0; i < maps.size(); ++i)
+        if (maps[i].va == p) {
+            vmm_release(maps[i]);
+            bytes -= (int64_t)maps[i].bytes;
+            maps.erase(maps.begin() + (long)i);
+            return;
+        }
     for (size_t i = 0; i < ptrs.size(); ++i)
         if (ptrs[i] == p) {
             size_t n = 0;
@@ -45,6 +127,8 @@ void DevArena::free(void *p) {
 }
 
 void DevArena::release() {
+    for (const VmmMap &m : maps) vmm_release(m);
+    maps.clear();
     for (void *q : ptrs) (void)hipFree(q);
     ptrs.clear();
     bytes = 0;
@@ -186,7 +270,7 @@ int build_csr(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
     CsrDev &c = p->csr;
     // 64-bit row pointers from 2^31 entries on; SPMV_CSR_FORCE_RP64 (internal)
     // exercises that kernel instance on small matrices in the tests
-    c.rp64 = A.nnz >= (int64_t)std::numeric_limits<int32_t>::max() - 64 || std::getenv("SPMV_CSR_FORCE_RP64");
+    c.rp64 = A.nnz >= (int64_t)std::numeric_limits<int32_t>::max() - 64 || o.csr_row_ptr64 != 0 || probe_env("SPMV_CSR_FORCE_RP64");
     if (c.rp64) {
         SPMV_RETURN_IF(upload(p, (int64_t **)&c.row_ptr, A.row_ptr, A.m + 1));
     } else {
@@ -207,7 +291,7 @@ int build_csr(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
 // order (JDS): slice row i is matrix row order[i]; nullptr = identity.
 int build_ell(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &, int cap, const int32_t *order) {
     EllDev &e = p->ell;
-    if (const char *u = std::getenv("SPMV_ELL_UNROLL")) e.unroll = std::atoi(u);
+    if (const char *u = probe_env("SPMV_ELL_UNROLL")) e.unroll = std::atoi(u);
     auto src = [&](int64_t r) -> int64_t { return order ? (int64_t)order[r] : r; };
     e.n_slices = (A.m + 63) / 64;
     std::vector<int64_t> off((size_t)e.n_slices + 1, 0);
@@ -487,10 +571,27 @@ static bool dia_offsets(const HostCsr &A, int max_diags, double max_fill, std::v
 // profiles/round1/probe/dia_placement.jsonl).  Copies of the values in up to
 // 8 allocations spread over the free device memory are timed with one
 // launch each over a zero x; the fastest is kept.
-static int dia_placement(spmv_plan_s *p, int64_t m, int64_t n, size_t bytes) {
+static int dia_placement(spmv_plan_s *p, int64_t m, int64_t n, size_t bytes, const spmv_options_t &o) {
     DiaDev &d = p->dia;
-    int K = bytes >= ((size_t)256 << 20) ? 8 : 1;
-    if (const char *e = std::getenv("SPMV_DIA_PLACEMENT")) K = std::max(1, std::min(8, std::atoi(e)));
+    int mode = o.placement;
+    SPMV_CHECK_ARG(mode >= SPMV_PLACEMENT_AUTO && mode <= SPMV_PLACEMENT_VMM, "unknown placement mode");
+    if (const char *e = probe_env("SPMV_PLACEMENT_MODE")) mode = std::atoi(e);
+    if (mode == SPMV_PLACEMENT_AUTO) mode = SPMV_PLACEMENT_PLAIN;  // the search is opt-in, as BIN's
+    if (mode == SPMV_PLACEMENT_SEARCH && bytes < ((size_t)256 << 20)) mode = SPMV_PLACEMENT_PLAIN;
+    d.placement = mode;
+    if (mode == SPMV_PLACEMENT_PLAIN) return SPMV_SUCCESS;
+    if (mode == SPMV_PLACEMENT_VMM) {  // move the values into a VMM mapping
+        size_t chunk = (size_t)2 << 20;
+        if (const char *e = probe_env("SPMV_VMM_CHUNK_MB")) chunk = (size_t)std::max(1, std::atoi(e)) << 20;
+        void *q = nullptr;
+        SPMV_RETURN_IF(p->arena.alloc_vmm(&q, bytes, chunk, p->device));
+        SPMV_HIP_TRY(hipMemcpy(q, d.val, bytes, hipMemcpyDeviceToDevice));
+        p->arena.free(d.val);
+        d.val = (double *)q;
+        return SPMV_SUCCESS;
+    }
+    int K = 8;
+    if (const char *e = probe_env("SPMV_DIA_PLACEMENT")) K = std::max(1, std::min(8, std::atoi(e)));
     if (K <= 1) return SPMV_SUCCESS;
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) {
@@ -556,6 +657,7 @@ static int dia_placement(spmv_plan_s *p, int64_t m, int64_t n, size_t bytes) {
     for (size_t k = 0; k < cand.size(); ++k)
         if (k != best) p->arena.free(cand[k]);
     d.val = cand[best];
+    d.placement_ms = t;
     if (d.dbg & 16) {
         std::fprintf(stderr, "[dia] placement ms:");
         for (float tt : t) std::fprintf(stderr, " %.4f", tt);
@@ -592,10 +694,10 @@ int build_dia(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
             val[(size_t)at] += A.val[j];  // duplicates are summed
         }
     SPMV_RETURN_IF(upload(p, &d.off, offs.data(), d.n_diags));
-    if (const char *e = std::getenv("SPMV_DIA_DEBUG")) d.dbg = std::atoi(e);
+    if (const char *e = probe_env("SPMV_DIA_DEBUG")) d.dbg = std::atoi(e);
     SPMV_RETURN_IF(upload(p, &d.val, val.data(), slots));
     p->stored_slots = slots;
-    SPMV_RETURN_IF(dia_placement(p, A.m, A.n, (size_t)slots * sizeof(double)));
+    SPMV_RETURN_IF(dia_placement(p, A.m, A.n, (size_t)slots * sizeof(double), o));
     p->algo_bytes = 8 * A.nnz + 4 * (int64_t)d.n_diags + 8 * A.n + 8 * A.m;
     p->n_kernels = 1;
     p->kernel_name = "dia_kernel";
@@ -626,7 +728,7 @@ int build_css(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
     int ncu = 0;
     SPMV_HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, p->device));
     c.nwg = ncu > 0 ? ncu : 256;
-    if (const char *e = std::getenv("SPMV_CSS_WGS")) {  // experiment: a subset of the CUs
+    if (const char *e = probe_env("SPMV_CSS_WGS")) {  // experiment: a subset of the CUs
         const int k = std::atoi(e);
         if (k >= 8 && k < c.nwg) c.nwg = k;
     }
@@ -651,7 +753,7 @@ int build_css(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
     std::vector<int32_t> rmap;          // block rows in slot order
     int64_t piece_cap = 0;
     int piece_div = 2;
-    if (const char *d = std::getenv("SPMV_CSS_PIECE_DIV")) piece_div = std::max(1, std::atoi(d));
+    if (const char *d = probe_env("SPMV_CSS_PIECE_DIV")) piece_div = std::max(1, std::atoi(d));
     bool fitted = false;
     for (c.P = P_min; c.P <= P_min + 1024 && !fitted; ++c.P) {
         const int64_t nb = (int64_t)c.P * c.nwg;
@@ -801,7 +903,7 @@ int build_css(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
     for (int64_t b = 0; b < nblocks; ++b) moff[b + 1] += moff[b];
     const int64_t lists_per_pass = (int64_t)c.nwg * W;
     c.interleaved = true;
-    if (const char *e = std::getenv("SPMV_CSS_LAYOUT")) c.interleaved = std::atoi(e) != 0;
+    if (const char *e = probe_env("SPMV_CSS_LAYOUT")) c.interleaved = std::atoi(e) != 0;
     int64_t total = 0;
     if (c.interleaved) {
         for (int pp = 0; pp < c.P; ++pp) {
@@ -863,7 +965,7 @@ int build_css(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
     std::vector<uint64_t> zeros(8 * 16, 0);
     SPMV_RETURN_IF(upload(p, &c.prog, zeros.data(), (int64_t)zeros.size()));
     c.launches = 0;
-    if (const char *d = std::getenv("SPMV_CSS_DEBUG")) c.dbg = std::atoi(d);
+    if (const char *d = probe_env("SPMV_CSS_DEBUG")) c.dbg = std::atoi(d);
     if (c.dbg & 32) SPMV_RETURN_IF(dev_alloc(p, &c.tstamp, (int64_t)c.P * c.nwg * (kCssWorkers + 2)));
     p->stored_slots = total;
     p->algo_bytes = 12 * A.nnz + 8 * A.n + 8 * A.m;

@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 #include <string>
 #include <vector>
 
@@ -42,11 +43,37 @@ const char *last_error();
         if (s_ != SPMV_SUCCESS) return s_;                                      \
     } while (0)
 
+// ---- experiment switches ------------------------------------------------
+// The probe build (`make probes`, -DSPMV_PROBES, probes_build/) reads the
+// SPMV_<FORMAT>_* tuning and ablation variables the tools/ scripts set; the
+// product library ignores them all, so no stray environment variable can
+// change what spmv_execute computes or how fast it runs.
+inline const char *probe_env(const char *name) {
+#ifdef SPMV_PROBES
+    return std::getenv(name);
+#else
+    (void)name;
+    return nullptr;
+#endif
+}
+
 // ---- device memory owned by a plan --------------------------------------
+// Plain hipMalloc allocations, plus buffers mapped through the HIP virtual
+// memory API (hipMemCreate + hipMemMap: the BIN product buffer, see
+// build_bin.cpp, placement).
+struct VmmMap {
+    void *va = nullptr;
+    size_t bytes = 0;
+    std::vector<hipMemGenericAllocationHandle_t> handles;  // one per mapped chunk
+    size_t chunk = 0;
+};
 struct DevArena {
     std::vector<void *> ptrs;
+    std::vector<VmmMap> maps;
     int64_t bytes = 0;
     int alloc(void **p, size_t n);  // hipMalloc, zero-size safe
+    // n bytes of physical memory in `chunk`-byte handles mapped at one VA range
+    int alloc_vmm(void **p, size_t n, size_t chunk, int device);
     void free(void *p);             // hipFree one allocation of this arena
     void release();
 };
@@ -147,6 +174,8 @@ struct DiaDev {
     double *val = nullptr;   // [n_diags * mp]
     int64_t mp = 0;          // m rounded up to kDiaBlockRows
     int dbg = 0;             // SPMV_DIA_DEBUG (internal): 1 = x from global memory, no LDS window
+    int placement = 0;       // SPMV_PLACEMENT_* used for val
+    std::vector<float> placement_ms;
 };
 
 // Column-slab sweep (CSS, k_css.hip).  Per (pass p, workgroup b, worker wave
@@ -237,7 +266,9 @@ struct BinDev {
     int32_t *bin_row0 = nullptr;  // [n_bins + 1]
     double *prod = nullptr;       // product buffer (largest group)
     int64_t prod_cap = 0;
-    int dbg = 0;  // SPMV_BIN_DEBUG (internal)
+    int placement = 0;            // how prod was allocated (spmv_options_t.placement, resolved)
+    bool mul_perm = false;        // Mul visits a strip's bins in scrambled order (build_bin.cpp)
+    int dbg = 0;  // SPMV_BIN_DEBUG (probe build only)
     std::vector<float> placement_ms;  // Mul ms of each product-buffer candidate
 };
 

@@ -251,8 +251,12 @@ static void launch_mul_t(const spmv_plan_s *p, int g, const double *x) {
 
 template <int PL>
 static void launch_mul_p(const spmv_plan_s *p, int g, const double *x) {
-    // SPMV_BIN_DEBUG bits 0-1 -> Mul MODE; default: nontemporal stores
-    // (measured 0.81 -> 0.71 ms at config 2, profiles/round1/probe/bin_probe_c2.jsonl)
+    // default: nontemporal stores (measured 0.81 -> 0.71 ms at config 2,
+    // profiles/round1/probe/bin_probe_c2.jsonl).  The ablation MODEs exist
+    // only in the probe build (SPMV_BIN_DEBUG bits 0-1, -DSPMV_PROBES).
+#ifndef SPMV_PROBES
+    launch_mul_t<1, PL>(p, g, x);
+#else
     switch (p->bin.dbg & 3) {
         case 1: launch_mul_t<0, PL>(p, g, x); break;
         case 2: launch_mul_t<2, PL>(p, g, x); break;
@@ -262,6 +266,7 @@ static void launch_mul_p(const spmv_plan_s *p, int g, const double *x) {
             break;
         default: launch_mul_t<1, PL>(p, g, x);
     }
+#endif
 }
 
 static void launch_mul(const spmv_plan_s *p, int g, const double *x) {
@@ -282,7 +287,12 @@ static void launch_sum_t(const spmv_plan_s *p, int g, double *y) {
 
 template <int W2, int U>
 static void launch_sum_w(const spmv_plan_s *p, int g, double *y) {
-    // SPMV_BIN_DEBUG bits 2-3 -> Sum MODE
+#ifndef SPMV_PROBES
+    // nontemporal product loads (config 2 Sum 0.308 -> 0.298 ms, neutral at
+    // config 3 and the N = 8 shape, profiles/round1/probe/bin_sum_nt_loads.jsonl)
+    launch_sum_t<W2, U, 1>(p, g, y);
+#else
+    // probe build: SPMV_BIN_DEBUG bits 2-3 -> Sum MODE
     if (p->bin.dbg & 512) {  // ablation: no slot loads
         launch_sum_t<W2, U, 4>(p, g, y);
         return;
@@ -299,6 +309,7 @@ static void launch_sum_w(const spmv_plan_s *p, int g, double *y) {
         case 2: launch_sum_t<W2, U, 2>(p, g, y); break;
         default: launch_sum_t<W2, U, 1>(p, g, y);
     }
+#endif
 }
 
 int bin_time_mul(const spmv_plan_s *p, const double *x, float *ms) {

@@ -219,7 +219,7 @@ int build_csr_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, 
                      const spmv_options_t &o, double mean_row) {
     CsrDev &c = p->csr;
     const hipStream_t st = p->stream;
-    c.rp64 = p->nnz >= (int64_t)INT32_MAX - 64 || std::getenv("SPMV_CSR_FORCE_RP64");
+    c.rp64 = p->nnz >= (int64_t)INT32_MAX - 64 || o.csr_row_ptr64 != 0 || probe_env("SPMV_CSR_FORCE_RP64");
     void *q;
     SPMV_RETURN_IF(p->arena.alloc(&q, (c.rp64 ? 8 : 4) * (size_t)(p->m + 1)));
     c.row_ptr = q;

@@ -281,8 +281,12 @@ int launch_css(const spmv_plan_s *p, const double *x, double *y) {
     }
     spmv_plan_s *mp = const_cast<spmv_plan_s *>(p);
     const uint64_t seq = mp->css.launches++;
-    // ablations (SPMV_CSS_DEBUG, internal): 1 no gathers, 2 no LDS atomics,
-    // 8 default cache policy on the matrix stream, 16 all gathers in 1 MiB
+#ifndef SPMV_PROBES
+    (void)c;
+    launch_css_t<true, 0>(p, x, y, seq);
+#else
+    // ablations (SPMV_CSS_DEBUG, probe build only): 1 no gathers, 2 no LDS
+    // atomics, 8 default cache policy on the matrix stream, 16 all gathers in 1 MiB
     switch (c.dbg & 19) {
         case 18: launch_css_t<true, 18>(p, x, y, seq); break;
         case 3: launch_css_t<true, 3>(p, x, y, seq); break;
@@ -293,6 +297,7 @@ int launch_css(const spmv_plan_s *p, const double *x, double *y) {
             if (c.dbg & 8) launch_css_t<false, 0>(p, x, y, seq);
             else launch_css_t<true, 0>(p, x, y, seq);
     }
+#endif
     SPMV_HIP_TRY(hipGetLastError());
     return SPMV_SUCCESS;
 }

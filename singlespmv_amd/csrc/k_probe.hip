@@ -1,6 +1,8 @@
 // k_probe.hip -- the measured STREAM-read ceiling SURVEY §8(d) asks bench.py
 // to report beside the 8 TB/s spec: a nontemporal 16-byte-per-lane read of
 // a buffer far larger than the 256 MB MALL, timed with HIP events.
+#include <numeric>
+
 #include "device.hpp"
 #include "internal.hpp"
 
@@ -67,6 +69,40 @@ __global__ __launch_bounds__(256) void gather_rate_kernel(const int32_t *__restr
         for (int u = 0; u < 8; ++u) acc += g[u];
     }
     if (acc == 12345.678) *sink = acc;
+}
+
+// Scattered-line write probe (placement experiments, tools/placement_probe.py):
+// every 128-byte line of a window is written once, 16 lanes per line with
+// nontemporal stores (the BIN Mul's product-write shape), lines visited in
+// the order i * P mod nlines (P odd) so consecutive lanes groups hit lines
+// far apart.
+__global__ __launch_bounds__(256) void line_write_kernel(double *__restrict__ buf, int64_t nlines, int64_t P) {
+    const int64_t g = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4;
+    const int64_t G = ((int64_t)gridDim.x * blockDim.x) >> 4;
+    const int sub = threadIdx.x & 15;
+    for (int64_t i = g; i < nlines; i += G) {
+        const int64_t line = (int64_t)(((__uint128_t)i * (uint64_t)P) % (uint64_t)nlines);
+        __builtin_nontemporal_store((double)i, buf + line * 16 + sub);
+    }
+}
+
+// The exactness guard of BIN and CSS (k_bin.hip, k_css.hip): one wave issues
+// ONE atomicAdd on LDS doubles -- compiled, as in bin_sum_kernel and
+// css_sweep_kernel, to a single ds_add_f64 under -munsafe-fp-atomics -- with
+// lane l adding val[l] to slot slot[l].  The claim the bit-exact BIN / CSS
+// sums rest on is that lanes hitting the same slot are applied in lane
+// order; tests/test_gpu_parity.py::test_lds_add_lane_order checks it on
+// order-sensitive values.
+__global__ __launch_bounds__(64) void lds_order_kernel(const int32_t *__restrict__ slot,
+                                                       const double *__restrict__ val, int32_t rounds,
+                                                       double *__restrict__ out) {
+    __shared__ double ys[64];
+    const int lane = threadIdx.x;
+    ys[lane] = 0.0;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    for (int r = 0; r < rounds; ++r) atomicAdd(&ys[slot[r * 64 + lane]], val[r * 64 + lane]);
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    out[lane] = ys[lane];
 }
 
 }  // namespace
@@ -178,5 +214,69 @@ extern "C" int spmv_stream_probe(int32_t device, int64_t bytes, int32_t iters, d
         return SPMV_ERROR_HIP;
     }
     *read_gbs = (double)n2 * 16 * iters / (ms * 1e-3) / 1e9;
+    return SPMV_SUCCESS;
+}
+
+// rounds x 64 (slot, value) pairs, one ds_add_f64 per round; out = the 64
+// LDS slots afterwards (see lds_order_kernel)
+extern "C" int spmv_lds_order_probe(int32_t device, int32_t rounds, const int32_t *slot, const double *val,
+                                    double *out) {
+    using namespace spmv;
+    SPMV_CHECK_ARG(rounds > 0 && rounds <= 1024 && slot && val && out, "bad arguments");
+    for (int64_t i = 0; i < (int64_t)rounds * 64; ++i) SPMV_CHECK_ARG(slot[i] >= 0 && slot[i] < 64, "slot outside [0, 64)");
+    SPMV_HIP_TRY(hipSetDevice(device));
+    int32_t *ds = nullptr;
+    double *dv = nullptr, *dout = nullptr;
+    const size_t n = (size_t)rounds * 64;
+    SPMV_HIP_TRY(hipMalloc(&ds, 4 * n));
+    SPMV_HIP_TRY(hipMalloc(&dv, 8 * n));
+    SPMV_HIP_TRY(hipMalloc(&dout, 8 * 64));
+    int st = SPMV_SUCCESS;
+    if (hipMemcpy(ds, slot, 4 * n, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(dv, val, 8 * n, hipMemcpyHostToDevice) != hipSuccess) {
+        set_error("spmv_lds_order_probe: upload failed");
+        st = SPMV_ERROR_HIP;
+    }
+    if (st == SPMV_SUCCESS) {
+        hipLaunchKernelGGL(lds_order_kernel, dim3(1), dim3(64), 0, nullptr, ds, dv, rounds, dout);
+        if (hipGetLastError() != hipSuccess || hipMemcpy(out, dout, 8 * 64, hipMemcpyDeviceToHost) != hipSuccess) {
+            set_error("spmv_lds_order_probe: launch or download failed");
+            st = SPMV_ERROR_HIP;
+        }
+    }
+    (void)hipFree(ds);
+    (void)hipFree(dv);
+    (void)hipFree(dout);
+    return st;
+}
+
+// internal (placement experiments): GB/s of the scattered-line write probe
+// over consecutive windows of `window` bytes of [buf, buf + bytes)
+extern "C" int spmv_line_write_probe(int32_t device, void *buf, int64_t bytes, int64_t window, int32_t reps,
+                                     double *gbs, int32_t max_windows, int32_t *n_windows) {
+    using namespace spmv;
+    SPMV_CHECK_ARG(buf && bytes > 0 && window >= 4096 && reps > 0 && gbs && n_windows, "bad arguments");
+    SPMV_HIP_TRY(hipSetDevice(device));
+    hipEvent_t a, b;
+    SPMV_HIP_TRY(hipEventCreate(&a));
+    SPMV_HIP_TRY(hipEventCreate(&b));
+    int nw = 0;
+    for (int64_t off = 0; off + window <= bytes && nw < max_windows; off += window, ++nw) {
+        const int64_t nlines = window / 128;
+        int64_t P = (nlines / 3) | 1;
+        while (std::gcd(P, nlines) != 1) P += 2;
+        double *w = (double *)((char *)buf + off);
+        hipLaunchKernelGGL(line_write_kernel, dim3(2048), dim3(256), 0, nullptr, w, nlines, P);
+        SPMV_HIP_TRY(hipEventRecord(a, nullptr));
+        for (int r = 0; r < reps; ++r) hipLaunchKernelGGL(line_write_kernel, dim3(2048), dim3(256), 0, nullptr, w, nlines, P);
+        SPMV_HIP_TRY(hipEventRecord(b, nullptr));
+        SPMV_HIP_TRY(hipEventSynchronize(b));
+        float ms = 0;
+        SPMV_HIP_TRY(hipEventElapsedTime(&ms, a, b));
+        gbs[nw] = (double)window * reps / (ms * 1e-3) / 1e9;
+    }
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    *n_windows = nw;
     return SPMV_SUCCESS;
 }

@@ -11,6 +11,8 @@
 #include <cstring>
 #include <strings.h>
 
+#include <vector>
+
 static int opt_hip_format() {
     int f = SPMV_FORMAT_AUTO;
 #if defined(OPT_HIP_CRS)
@@ -61,18 +63,49 @@ void OptimizeProblem(const SpMat &A, const Vec &x, SpMatOpt &A_opt, VecOpt &x_op
     spmv_options_t o;
     spmv_options_default(&o);
     o.format = opt_hip_format();
+    // SPMV_HIP_PLACEMENT=search: the build-time placement search for the BIN
+    // product buffer / DIA values (spmv_hip.h SPMV_PLACEMENT_SEARCH)
+    if (const char *pl = std::getenv("SPMV_HIP_PLACEMENT")) {
+        if (!strcasecmp(pl, "search")) o.placement = SPMV_PLACEMENT_SEARCH;
+        else if (!strcasecmp(pl, "vmm")) o.placement = SPMV_PLACEMENT_VMM;
+        else if (!strcasecmp(pl, "plain")) o.placement = SPMV_PLACEMENT_PLAIN;
+    }
+    A_opt.nRow = A.nRow;
+    A_opt.nCol = A.nCol;
+    A_opt.nNnz = A.nNnz;
+    A_opt.plan = nullptr;
+    A_opt.dist = nullptr;
+    A_opt.d_x = nullptr;
+    A_opt.x_uploaded = 0;
+    A_opt.n_gpus = 1;
+    const char *gpus = std::getenv("SPMV_HIP_GPUS");
+    if (gpus && *gpus) A_opt.n_gpus = std::atoi(gpus) > 1 ? std::atoi(gpus) : 1;
+    if (gpus && *gpus) {  // set (even to 1): the multi-GPU plan
+        // the rows over n_gpus devices: COO -> CSR row pointers, one dist plan
+        std::vector<int64_t> rp((size_t)A.nRow + 1);
+        int st = spmv_coo_to_csr(A.nRow, A.nNnz, A.row_idx, rp.data());
+        if (st != SPMV_SUCCESS) opt_hip_die("OptimizeProblem", st);
+        st = spmv_dist_create_csr(A_opt.n_gpus, nullptr, A.nRow, A.nCol, A.nNnz, rp.data(), A.col_idx, A.val, &o,
+                                  &A_opt.dist);
+        if (st != SPMV_SUCCESS) opt_hip_die("OptimizeProblem (SPMV_HIP_GPUS)", st);
+        spmv_plan_t p0 = nullptr;
+        int32_t nd = 0;
+        spmv_dist_info(A_opt.dist, &nd, nullptr, nullptr);
+        std::vector<spmv_plan_t> plans((size_t)nd);
+        spmv_dist_info(A_opt.dist, &nd, nullptr, plans.data());
+        p0 = plans[0];
+        spmv_plan_info_t info;
+        spmv_plan_info(p0, &info);
+        A_opt.format = info.format;
+        return;
+    }
     spmv_plan_t plan = nullptr;
     const int st = spmv_plan_create_coo(A.nRow, A.nCol, A.nNnz, A.row_idx, A.col_idx, A.val, &o, &plan);
     if (st != SPMV_SUCCESS) opt_hip_die("OptimizeProblem", st);
     spmv_plan_info_t info;
     spmv_plan_info(plan, &info);
-    A_opt.nRow = A.nRow;
-    A_opt.nCol = A.nCol;
-    A_opt.nNnz = A.nNnz;
     A_opt.plan = plan;
     A_opt.format = info.format;
-    A_opt.d_x = nullptr;
-    A_opt.x_uploaded = 0;
 }
 
 extern "C" {
@@ -85,7 +118,11 @@ void SpMV(const SpMatOpt &A, const VecOpt &x, Vec &y) {
     }
     SpMatOpt &a = const_cast<SpMatOpt &>(A);  // the reference passes const& too
     int st;
-    if (!resident) {
+    if (a.dist) {  // SPMV_HIP_GPUS: H2D x, RCCL broadcast, local SpMVs, RCCL all-gather, D2H y
+        st = spmv_dist_execute(a.dist, (resident && a.x_uploaded) ? nullptr : x.val, y.val,
+                               (resident && a.x_uploaded) ? SPMV_X_STAGED : 0u);
+        a.x_uploaded = 1;
+    } else if (!resident) {
         st = spmv_execute(a.plan, x.val, y.val, 0u);  // H2D x, kernels, D2H y
     } else {
         if (!a.x_uploaded) {
@@ -100,7 +137,9 @@ void SpMV(const SpMatOpt &A, const VecOpt &x, Vec &y) {
 
 void SpMVRelease(SpMatOpt &A) {
     spmv_plan_destroy(A.plan);
+    spmv_dist_destroy(A.dist);
     A.plan = nullptr;
+    A.dist = nullptr;
 }
 
 }  // extern "C"

@@ -81,6 +81,17 @@ def max_over_ranks(values, device):
     return [float(v) for v in t.tolist()]
 
 
+def sum_over_ranks(values, device):
+    """Element-wise sum of a short list of floats over all ranks."""
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor(values, dtype=torch.float64,
+                     device="cpu" if _CPU_COLLECTIVES else device)
+    if _dist_on():
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return [float(v) for v in t.tolist()]
+
+
 def gather_y(y_local, rows_per_rank: int):
     """All-gather equal, padded y slices into the full y (length
     world * rows_per_rank; the caller trims the padding)."""

@@ -52,6 +52,7 @@ int main() {
                     B.sum_u = B.sum_waves == 8 ? 8 : 32;
                     B.pad_log = pl;
                     B.nwg1 = B.nwg2 = 256;
+                    B.mul_perm = (si + wi + pl) % 2 == 0;  // both Mul bin orders
                     spmv_options_t o;
                     std::memset(&o, 0, sizeof(o));
                     BinLayout L;
@@ -77,11 +78,20 @@ int main() {
                         }
                     }
                     if (cur != E) return fail("E", cur, E);
-                    // Mul order: strip-major, same padded sizes
+                    // Mul order: strip-major, the bins of a strip in L.mul_bins
+                    // order (a permutation of the bins), same padded sizes
+                    {
+                        std::vector<char> hit((size_t)NB, 0);
+                        for (int64_t i = 0; i < NB; ++i) {
+                            const int64_t b = L.mul_bins[(size_t)i];
+                            if (b < 0 || b >= NB || hit[(size_t)b]++) return fail("mul_bins permutation", i, b);
+                        }
+                    }
                     cur = 0;
                     for (int64_t t = 0; t < S; ++t) {
                         if (L.strip_start[(size_t)t] != cur) return fail("strip_start", t, cur);
-                        for (int64_t b = 0; b < NB; ++b) {
+                        for (int64_t i = 0; i < NB; ++i) {
+                            const int64_t b = L.mul_bins[(size_t)i];
                             if (L.off1[(size_t)(b * S + t)] != cur) return fail("off1", b * S + t, cur);
                             cur += L.rpad(L.cnt[(size_t)(b * S + t)]);
                         }

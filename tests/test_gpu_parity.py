@@ -287,12 +287,16 @@ def test_device_pointers_and_streams():
         assert ms > 0
 
 
-@pytest.mark.parametrize("fmt", ["", "bin", "css"])
-def test_dropin_optimizeproblem_spmv(fmt, monkeypatch):
+@pytest.mark.parametrize("fmt,gpus", [("", ""), ("bin", ""), ("css", ""), ("bin", "1"), ("", "1")])
+def test_dropin_optimizeproblem_spmv(fmt, gpus, monkeypatch):
     """The reference-signature drop-in (include/opt_hip.h) via libopt_hip.so
-    (format from SPMV_HIP_FORMAT, as the -DOPT_HIP_<FMT> build would fix it)."""
+    (format from SPMV_HIP_FORMAT, as the -DOPT_HIP_<FMT> build would fix it);
+    SPMV_HIP_GPUS routes it through the multi-GPU plan (spmv_dist_*, here
+    over the box's one device)."""
     if fmt:
         monkeypatch.setenv("SPMV_HIP_FORMAT", fmt)
+    if gpus:
+        monkeypatch.setenv("SPMV_HIP_GPUS", gpus)
     class SpMatC(C.Structure):
         _fields_ = [("nRow", C.c_int), ("nCol", C.c_int), ("nNnz", C.c_int),
                     ("row_idx", C.c_void_p), ("col_idx", C.c_void_p), ("val", C.c_void_p)]
@@ -302,7 +306,8 @@ def test_dropin_optimizeproblem_spmv(fmt, monkeypatch):
 
     class SpMatOptC(C.Structure):
         _fields_ = [("nRow", C.c_int), ("nCol", C.c_int), ("nNnz", C.c_int), ("plan", C.c_void_p),
-                    ("format", C.c_int), ("d_x", C.c_void_p), ("x_uploaded", C.c_int)]
+                    ("format", C.c_int), ("d_x", C.c_void_p), ("x_uploaded", C.c_int), ("dist", C.c_void_p),
+                    ("n_gpus", C.c_int)]
 
     sp.lib()
     L = C.CDLL(sp.OPT_LIB_PATH)
@@ -321,6 +326,7 @@ def test_dropin_optimizeproblem_spmv(fmt, monkeypatch):
         L.SpMV(C.byref(Ao), C.byref(xo), C.byref(yv))
         assert sp.verify_result(sp.SpMat(m, n, row, col, val), x, y)
     check_close(y, g["y_crs"])
+    assert bool(Ao.dist) == bool(gpus) and bool(Ao.plan) != bool(gpus)
     L.SpMVRelease(C.byref(Ao))
 
 
@@ -450,20 +456,20 @@ def test_execute_alpha():
 
 
 @pytest.mark.parametrize("lanes", [1, 4, 32])
-def test_csr_64bit_row_pointers(monkeypatch, lanes):
+def test_csr_64bit_row_pointers(lanes):
     """The int64 row-pointer kernel instance (used from 2^31 nnz on), forced
-    on a small matrix: same y as the int32 instance, host and device builds."""
+    on a small matrix (option csr_row_ptr64): same y as the int32 instance,
+    host and device builds."""
     import torch
     m = 40000
     rp, col, val = sp.generate_csr(sp.gen_spec("powerlaw", m, max_len=1200, seed=91))
     x = sp.generate_vector(m, seed=93)
     y32 = run_plan(sp.Plan.from_csr(m, m, rp, col, val, "csr", csr_lanes=lanes), x, m)
-    monkeypatch.setenv("SPMV_CSR_FORCE_RP64", "1")
-    p64 = sp.Plan.from_csr(m, m, rp, col, val, "csr", csr_lanes=lanes)
+    p64 = sp.Plan.from_csr(m, m, rp, col, val, "csr", csr_lanes=lanes, csr_row_ptr64=True)
     assert p64.info()["row_ptr_bytes"] == 8
     assert np.array_equal(run_plan(p64, x, m), y32)
     pd = sp.Plan.from_device_csr(m, m, torch.from_numpy(rp).cuda(), torch.from_numpy(col).cuda(),
-                                 torch.from_numpy(val).cuda(), "csr", csr_lanes=lanes)
+                                 torch.from_numpy(val).cuda(), "csr", csr_lanes=lanes, csr_row_ptr64=True)
     assert pd.info()["row_ptr_bytes"] == 8
     assert np.array_equal(run_plan(pd, x, m), y32)
 
@@ -522,19 +528,130 @@ def test_bin_bit_exact(shape, kind, opts):
     assert np.array_equal(y, oracle_y(rp, col, val, x)), f"bin {shape} {kind} {opts}"
 
 
-@pytest.mark.parametrize("env", [{"SPMV_BIN_PADLOG": "3"}, {"SPMV_BIN_PADLOG": "5"}, {"SPMV_BIN_SUMWAVES": "2"},
-                                 {"SPMV_BIN_SUMWAVES": "8"}, {"SPMV_BIN_REUSE": "1"},
-                                 {"SPMV_BIN_DEBUG": "1"}])
-def test_bin_layout_knobs(env, monkeypatch):
-    """The internal layout knobs (product-line padding, Sum waves / bin rows,
-    a product buffer re-used per row group, plain stores) change speed only."""
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
+@pytest.mark.parametrize("opts", [{"bin_pad": 8}, {"bin_pad": 16}, {"bin_pad": 32}, {"bin_sum_waves": 2},
+                                  {"bin_sum_waves": 4}, {"bin_sum_waves": 8}, {"placement": "plain"},
+                                  {"placement": "vmm"}, {"placement": "search"}])
+def test_bin_layout_options(opts):
+    """The layout options (product-line padding, Sum waves / bin rows) and the
+    product-buffer placements change speed only."""
     m = 120_000
     rp, col, val = _bin_matrix("powerlaw", m, m, seed=41)
     x = sp.generate_vector(m, seed=43)
-    plan = sp.Plan.from_csr(m, m, rp, col, val, "bin", bin_groups=2)
-    assert np.array_equal(run_plan(plan, x, m), oracle_y(rp, col, val, x)), env
+    plan = sp.Plan.from_csr(m, m, rp, col, val, "bin", bin_groups=2, **opts)
+    info = plan.info()
+    if "bin_pad" in opts:
+        assert info["bin_pad"] == opts["bin_pad"]
+    if "bin_sum_waves" in opts:
+        assert info["bin_sum_waves"] == opts["bin_sum_waves"]
+    assert np.array_equal(run_plan(plan, x, m), oracle_y(rp, col, val, x)), opts
+
+
+def _create_peak_drop(make):
+    """(plan, peak drop of free device memory while `make()` runs): a thread
+    polls hipMemGetInfo (torch.cuda.mem_get_info) during the create call."""
+    import threading
+    import torch
+    torch.cuda.synchronize()
+    base = torch.cuda.mem_get_info()[0]
+    low = [base]
+    stop = threading.Event()
+
+    def poll():
+        while not stop.is_set():
+            low[0] = min(low[0], torch.cuda.mem_get_info()[0])
+
+    t = threading.Thread(target=poll)
+    t.start()
+    try:
+        plan = make()
+    finally:
+        stop.set()
+        t.join()
+    low[0] = min(low[0], torch.cuda.mem_get_info()[0])
+    return plan, base - low[0]
+
+
+@pytest.mark.parametrize("fmt,kind", [("bin", "uniform"), ("dia", "banded")])
+def test_plan_create_holds_only_the_plan(fmt, kind):
+    """AUTO placement: while a large BIN / DIA plan is created, free device
+    memory never drops by more than the plan's own bytes (+128 MB of runtime
+    slack); ten plans built in a row behave the same.  The opt-in SEARCH
+    placement times several candidates (and reports them in plan info)."""
+    m = 4_000_000
+    spec = sp.gen_spec(kind, m, per_row=16, band_lo=-20, band_hi=20, seed=21)
+    rp, col, val = sp.generate_csr(spec)
+    for i in range(10 if fmt == "bin" else 2):
+        plan, drop = _create_peak_drop(lambda: sp.Plan.from_csr(m, m, rp, col, val, fmt))
+        info = plan.info()
+        assert info["format"] == fmt and info["placement"] == "plain"
+        assert drop <= info["device_bytes"] + (128 << 20), (i, drop, info["device_bytes"])
+        plan.destroy()
+    plan = sp.Plan.from_csr(m, m, rp, col, val, fmt, placement="search")
+    info = plan.info()
+    assert info["placement"] == "search" and info["placement_candidates"] >= 2
+    assert 0 < info["placement_best_ms"] <= info["placement_worst_ms"]
+
+
+def test_experiment_switches_do_not_reach_the_product_library(monkeypatch):
+    """Every ablation / tuning variable of the probe build, set to a value that
+    (in the probe build) skips stores, drops LDS adds or re-lays the data:
+    the product library ignores them -- y stays bit-exact."""
+    bad = {"SPMV_BIN_DEBUG": "6", "SPMV_BIN_PADLOG": "5", "SPMV_BIN_SUMWAVES": "8", "SPMV_BIN_SLOT_LINEAR": "1",
+           "SPMV_BIN_REUSE": "1", "SPMV_BIN_SB": "2", "SPMV_BIN_CUS": "3", "SPMV_BIN_PLACEMENT": "3",
+           "SPMV_BIN_HOST_BUILD": "1", "SPMV_CSS_DEBUG": "3", "SPMV_CSS_LAYOUT": "0", "SPMV_CSS_PIECE_DIV": "7",
+           "SPMV_CSS_WGS": "5", "SPMV_DIA_DEBUG": "1", "SPMV_DIA_PLACEMENT": "2", "SPMV_ELL_UNROLL": "3",
+           "SPMV_CSR_FORCE_RP64": "1", "SPMV_PLACEMENT_MODE": "9", "SPMV_VMM_CHUNK_MB": "1"}
+    for k, v in bad.items():
+        monkeypatch.setenv(k, v)
+    m = 60_000
+    for kind, fmts in (("powerlaw", ["bin", "css", "csr", "ell"]), ("banded", ["dia", "bin"])):
+        spec = sp.gen_spec(kind, m, max_len=900, band_lo=-5, band_hi=9, seed=12)
+        rp, col, val = sp.generate_csr(spec)
+        x = sp.generate_vector(m, seed=13)
+        yo = oracle_y(rp, col, val, x)
+        for fmt in fmts:
+            plan = sp.Plan.from_csr(m, m, rp, col, val, fmt)
+            info = plan.info()
+            assert info["n_kernels"] >= 1 and info["row_ptr_bytes"] == 4
+            y = run_plan(plan, x, m)
+            if fmt in ("bin", "dia", "ell"):
+                assert np.array_equal(y, yo), (kind, fmt)
+            else:
+                check_close(y, yo, what=f"{kind} {fmt} with switches set")
+
+
+def test_lds_add_lane_order():
+    """The named guard of BIN's and CSS's exactness (k_bin.hip, k_css.hip):
+    lanes of ONE ds_add_f64 that hit the same LDS slot are applied in lane
+    order.  Values are chosen so that any other order (reverse, pairwise
+    tree, or a different lane permutation) rounds differently."""
+    rng = np.random.default_rng(5)
+
+    def lane_order(slots, vals):
+        out = np.zeros(64)
+        for r in range(len(slots) // 64):
+            for lane in range(64):
+                k = slots[r * 64 + lane]
+                out[k] = out[k] + vals[r * 64 + lane]
+        return out
+
+    # 1) all 64 lanes on one slot: 1e16, 31 small values, -1e16, 31 small values
+    v = np.concatenate([[1e16], 1.0 + rng.integers(0, 4, 31) * 0.25, [-1e16], 1.0 + rng.integers(0, 4, 31) * 0.25])
+    s = np.zeros(64, np.int32)
+    want = lane_order(s, v)
+    rev = 0.0
+    for t in v[::-1]:
+        rev = rev + t
+    assert want[0] != rev, "test values are not order-sensitive"
+    assert np.array_equal(sp.lds_order_probe(s, v), want)
+    # 2) k-major-like patterns: 4 slots interleaved, magnitudes spread, 16 rounds
+    s = np.tile(np.arange(64, dtype=np.int32) % 4, 16)
+    v = rng.choice([1e16, -1e16, 3.0, 0.1, 1e-3, 7e15], size=s.size) * rng.random(s.size)
+    assert np.array_equal(sp.lds_order_probe(s, v), lane_order(s, v))
+    # 3) random slots, runs of equal slots within one instruction
+    s = np.sort(rng.integers(0, 64, size=64 * 32).reshape(32, 64), axis=1).astype(np.int32).ravel()
+    v = rng.standard_normal(s.size) * 10.0 ** rng.integers(-8, 17, s.size)
+    assert np.array_equal(sp.lds_order_probe(s, v), lane_order(s, v))
 
 
 def test_bin_edge_cases():
@@ -637,6 +754,58 @@ def test_full_size_headline_bit_exact(config):
     assert np.all(lin <= 1e-12 * np.abs(outs[2]) + 1e-300)
     plan.destroy()
 
+
+
+def test_full_size_c5_rank_shape():
+    """Rank 0 of BASELINE config 5 (80 M x 80 M, 16 nnz/row, row-partitioned
+    over 8 GPUs): its 10 M rows over all 80 M columns with the 640 MB x, the
+    AUTO plan (BIN with 2 Sum waves), bit for bit against the oracle's opt_crs
+    restatement, plus linearity A(x1 + x2) = A x1 + A x2."""
+    import torch
+    world, rows = 8, 10_000_000
+    spec = sp.gen_spec("uniform", world * rows, per_row=16, seed=42)
+    rp, col, val = sp.generate_csr(spec, 0, rows)
+    n = world * rows
+    plan = sp.Plan.from_csr(rows, n, rp, col, val, "auto")
+    info = plan.info()
+    assert info["format"] == "bin" and info["n"] == n and info["nnz"] == 16 * rows
+    x1 = sp.generate_vector(n, seed=43)
+    x2 = sp.generate_vector(n, seed=44)
+    y = torch.empty(rows, dtype=torch.float64, device="cuda")
+    outs = []
+    for xv in (x1, x2, x1 + x2):
+        plan.execute(torch.from_numpy(xv).cuda(), y)
+        outs.append(y.cpu().numpy().copy())
+    assert np.array_equal(outs[0], oracle_y(rp, col, val, x1))
+    lin = np.abs(outs[2] - (outs[0] + outs[1]))
+    assert np.all(lin <= 1e-12 * np.abs(outs[2]) + 1e-300)
+    plan.destroy()
+
+
+def test_full_size_c4_banded():
+    """BASELINE config 4 at full size: 20 M rows, diagonals -32..+31 (64),
+    1.28 G entries -- the largest index range in the product.  The DIA plan
+    bit for bit and the CSR plan (16 lanes per row) to 1e-12 against the
+    oracle's opt_crs restatement."""
+    import torch
+    m = 20_000_000
+    spec = sp.gen_spec("banded", m, band_lo=-32, band_hi=31, seed=42)
+    rp, col, val = sp.generate_csr(spec)
+    assert int(rp[-1]) == 64 * m - 1024  # rows 0..31 and the last 31 rows are clipped
+    x = sp.generate_vector(m, seed=43)
+    yo = oracle_y(rp, col, val, x)
+    xd = torch.from_numpy(x).cuda()
+    y = torch.empty(m, dtype=torch.float64, device="cuda")
+    plan = sp.Plan.from_csr(m, m, rp, col, val, "dia")
+    assert plan.info()["n_diags"] == 64
+    plan.execute(xd, y)
+    assert np.array_equal(y.cpu().numpy(), yo)
+    plan.destroy()
+    del plan
+    plan = sp.Plan.from_csr(m, m, rp, col, val, "csr")
+    plan.execute(xd, y)
+    check_close(y.cpu().numpy(), yo, what="c4 csr")
+    plan.destroy()
 
 
 def test_bin_refuses_huge_sparse_grid_and_auto_avoids_it():

@@ -263,3 +263,23 @@ def test_mtx2bin_cli(tmp_path):
     g = load_golden("mtx_random")
     m, n, rp, col, val = sp.load_csr_bin(out)
     assert np.array_equal(rp, sp.coo_to_csr(int(g["m"]), g["row"])) and np.array_equal(val, g["val"])
+
+
+def test_dist_layout_cuts_and_slices():
+    """The row cut of the C-ABI multi-GPU plan (spmv_dist_layout): nnz-
+    balanced cuts, monotone, covering [0, m], and the padded
+    slice = the longest range; N = 1..8 over uniform, power-law and
+    all-empty matrices."""
+    for kind in ("uniform", "powerlaw"):
+        spec = sp.gen_spec(kind, 100_003, per_row=7, max_len=5000, seed=4)
+        rp, _, _ = sp.generate_csr(spec)
+        nnz = int(rp[-1])
+        for parts in range(1, 9):
+            cuts, sl = sp.dist_layout(rp, parts)
+            assert cuts[0] == 0 and cuts[-1] == len(rp) - 1 and np.all(np.diff(cuts) >= 0)
+            assert sl == max(1, int(np.max(np.diff(cuts))))
+            share = np.diff(rp[cuts])
+            # no part exceeds its nnz share by more than one row's entries
+            assert share.max() <= nnz / parts + np.diff(rp).max()
+    cuts, sl = sp.dist_layout(np.zeros(11, np.int64), 4)
+    assert cuts[0] == 0 and cuts[-1] == 10 and sl >= 1

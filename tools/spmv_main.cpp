@@ -8,29 +8,93 @@
 // with GPU additions: AchievedGB/s against the plan's algorithmic bytes and
 // the MI355X 8 TB/s HBM roofline.
 //
-// Usage: spmv <matrix.mtx> [--format crs|ell|ss|dia|hyb|css|coo|jds|bin|auto] [--resident]
+// Usage: spmv <matrix.mtx | gen:uniform:ROWS:PER | gen:banded:ROWS:HALF | gen:powerlaw:ROWS:MAXLEN>
+//             [--format crs|ell|ss|dia|hyb|css|coo|jds|bin|auto] [--resident] [--gpus N]
+//             [--placement plain|search|vmm]
+//
+// --gpus N spans N devices of the node through the drop-in's multi-GPU plan
+// (SPMV_HIP_GPUS, spmv_dist_*: nnz-balanced row ranges, RCCL broadcast of x,
+// RCCL all-gather of y); gen: builds the seeded synthetic matrix of the
+// BASELINE configs in memory (seed 42) instead of parsing text -- config 5 is
+// `gen:uniform:80000000:16 --gpus 8 --resident`.
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <iostream>
 #include <string>
+#include <vector>
 
 #include "opt_hip.h"
+
+// gen:<kind>:<rows>:<p> -> sorted COO (the SpMat LoadSparseMatrix returns)
+static bool GenerateMatrix(SpMat &A, const std::string &what) {
+    char kind[32] = {0};
+    long long rows = 0, p = 0;
+    if (std::sscanf(what.c_str(), "gen:%31[a-z]:%lld:%lld", kind, &rows, &p) != 3 || rows <= 0 || p <= 0) return false;
+    spmv_gen_spec_t g = {};
+    g.m = g.n = rows;
+    g.seed = 42;
+    g.per_row = 16;
+    g.max_len = 10000;
+    g.alpha = 2.0;
+    g.band_lo = -32;
+    g.band_hi = 31;
+    if (!std::strcmp(kind, "uniform")) {
+        g.kind = SPMV_GEN_UNIFORM;
+        g.per_row = (int)p;
+    } else if (!std::strcmp(kind, "banded")) {
+        g.kind = SPMV_GEN_BANDED;
+        g.band_lo = -(int)p;
+        g.band_hi = (int)p - 1;
+    } else if (!std::strcmp(kind, "powerlaw")) {
+        g.kind = SPMV_GEN_POWERLAW;
+        g.max_len = (int)p;
+    } else {
+        return false;
+    }
+    int64_t nnz = 0;
+    if (spmv_gen_count(&g, 0, rows, &nnz) != SPMV_SUCCESS || nnz >= 2147483647LL) return false;
+    std::vector<int64_t> rp((size_t)rows + 1);
+    A.nRow = A.nCol = (int)rows;
+    A.nNnz = (int)nnz;
+    A.row_idx = (int *)std::malloc(sizeof(int) * (size_t)std::max<int64_t>(nnz, 1));
+    A.col_idx = (int *)std::malloc(sizeof(int) * (size_t)std::max<int64_t>(nnz, 1));
+    A.val = (double *)std::malloc(sizeof(double) * (size_t)std::max<int64_t>(nnz, 1));
+    if (!A.row_idx || !A.col_idx || !A.val) return false;
+    if (spmv_gen_fill(&g, 0, rows, rp.data(), A.col_idx, A.val) != SPMV_SUCCESS) return false;
+#pragma omp parallel for schedule(static)
+    for (long long r = 0; r < rows; ++r)
+        for (int64_t j = rp[(size_t)r]; j < rp[(size_t)r + 1]; ++j) A.row_idx[j] = (int)r;
+    return true;
+}
 
 int main(int argc, char **argv) {
     srand(3);  // src/main.cpp:18
     if (argc < 2) {
-        std::printf("Usage: %s <matrix> [--format crs|ell|ss|dia|hyb|css|coo|jds|bin|auto] [--resident]\n", argv[0]);
+        std::printf("Usage: %s <matrix | gen:uniform:ROWS:PER | gen:banded:ROWS:HALF | gen:powerlaw:ROWS:MAXLEN> "
+                    "[--format crs|ell|ss|dia|hyb|css|coo|jds|bin|auto] [--resident] [--gpus N] [--placement plain|search|vmm]\n", argv[0]);
         return 1;
     }
     const std::string matFile = argv[1];
     for (int i = 2; i < argc; ++i) {
         if (!std::strcmp(argv[i], "--format") && i + 1 < argc) setenv("SPMV_HIP_FORMAT", argv[++i], 1);
         else if (!std::strcmp(argv[i], "--resident")) setenv("SPMV_HIP_X_RESIDENT", "1", 1);
+        else if (!std::strcmp(argv[i], "--placement") && i + 1 < argc) setenv("SPMV_HIP_PLACEMENT", argv[++i], 1);
+        else if (!std::strcmp(argv[i], "--gpus") && i + 1 < argc) {
+            setenv("SPMV_HIP_GPUS", argv[++i], 1);
+        }
     }
     SpMat A;
-    std::cerr << "Loading sparse matrix " << matFile << " ... ";
-    LoadSparseMatrix(A, matFile);
+    if (matFile.rfind("gen:", 0) == 0) {
+        std::cerr << "Generating " << matFile << " ... ";
+        if (!GenerateMatrix(A, matFile)) {
+            std::printf("*** bad generator spec %s ***\n", matFile.c_str());
+            return 1;
+        }
+    } else {
+        std::cerr << "Loading sparse matrix " << matFile << " ... ";
+        LoadSparseMatrix(A, matFile);
+    }
     std::cerr << "done." << std::endl;
     Vec x = CreateRandomVector(A.nCol);
     Vec y = CreateRandomVector(A.nRow);
@@ -67,10 +131,24 @@ int main(int argc, char **argv) {
     std::cerr << "done." << std::endl;
 
     spmv_plan_info_t info;
-    spmv_plan_info(A_opt.plan, &info);
+    int64_t algo_bytes = 0;
+    if (A_opt.dist) {  // algorithmic bytes of the whole job: every device's plan
+        int32_t nd = 0;
+        spmv_dist_info(A_opt.dist, &nd, nullptr, nullptr);
+        std::vector<spmv_plan_t> plans((size_t)nd);
+        spmv_dist_info(A_opt.dist, &nd, nullptr, plans.data());
+        for (spmv_plan_t p : plans) {
+            spmv_plan_info(p, &info);
+            algo_bytes += info.algo_bytes;
+        }
+        spmv_plan_info(plans[0], &info);
+    } else {
+        spmv_plan_info(A_opt.plan, &info);
+        algo_bytes = info.algo_bytes;
+    }
     static const char *names[] = {"AUTO", "CRS", "ELL", "SS", "DIA", "HYB", "CSS", "COO", "JDS", "BIN"};
     const double gflops = (double)A.nNnz * 2.0 / best / 1e9;
-    const double gbs = (double)info.algo_bytes / best / 1e9;
+    const double gbs = (double)algo_bytes / best / 1e9;
     std::printf("++++++++++++++++++++++++++++++++++++++++\n");
     std::printf("%25s\t%s\n", "Architecture", "GPU");
     std::printf("%25s\t%s\n", "MatrixFormat", names[info.format]);
@@ -79,11 +157,11 @@ int main(int argc, char **argv) {
     std::printf("%25s\t%s\n", "MatrixPath", matFile.c_str());
     std::printf("%25s\t%lf\n", "Performance(GFLOPS)", gflops);
     std::printf("%25s\t%lf\n", "AchievedGB/s", gbs);
-    std::printf("%25s\t%lf\n", "RooflineFrac", gbs / 8000.0);
+    std::printf("%25s\t%lf\n", "RooflineFrac", gbs / (8000.0 * A_opt.n_gpus));
     std::printf("%25s\t%d\n", "nRow", A.nRow);
     std::printf("%25s\t%d\n", "nCol", A.nCol);
     std::printf("%25s\t%d\n", "nNnz", A.nNnz);
-    std::printf("%25s\t%d\n", "nGPU", 1);
+    std::printf("%25s\t%d\n", "nGPU", A_opt.n_gpus);
     std::printf("%25s\t%s\n", "XResident", getenv("SPMV_HIP_X_RESIDENT") ? "1" : "0");
     std::printf("----------------------------------------\n");
     SpMVRelease(A_opt);
