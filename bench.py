@@ -56,9 +56,25 @@ def streamed_bytes(info) -> dict:
     once, plus one re-load per workgroup range boundary) and writes 8 B
     products; Sum reads products 8 + row slot 2 B and writes y."""
     E = info["stored_slots"]
-    mul = E * (8 + 2 + 8) + E // max(1, info["bin_pad"]) * 4 + 8 * info["n"]
-    summ = E * (8 + 2) + 8 * info["m"]
-    return {"mul": mul, "sum": summ, "total": mul + summ}
+    mul_read = E * (8 + 2) + E // max(1, info["bin_pad"]) * 4 + 8 * info["n"]
+    mul_write = 8 * E
+    sum_read = E * (8 + 2)
+    sum_write = 8 * info["m"]
+    return {"mul": mul_read + mul_write, "sum": sum_read + sum_write,
+            "total": mul_read + mul_write + sum_read + sum_write,
+            "mul_read": mul_read, "mul_write": mul_write, "sum_read": sum_read, "sum_write": sum_write}
+
+
+def bin_ceiling(model: dict, read_gbs: float, write_gbs: float, nnz: int) -> dict:
+    """BIN's own floor: its streamed bytes (not the 12 B/nnz roofline) moved at
+    the measured STREAM read / write ceilings of this GPU, Mul then Sum."""
+    ms = model["total"] / read_gbs / 1e6
+    ms_rw = ((model["mul_read"] + model["sum_read"]) / read_gbs + (model["mul_write"] + model["sum_write"]) / write_gbs) / 1e6
+    return {"model": "BIN streamed bytes (Mul 8+2+0.25 B read + 8 B write, Sum 8+2 B read per stored entry, "
+                     "x strips, y), all moved at the measured STREAM-read ceiling",
+            "bytes": model["total"], "read_gbs": read_gbs, "write_gbs": write_gbs,
+            "implied_ms": ms, "implied_gflops": 2.0 * nnz / (ms * 1e-3) / 1e9,
+            "implied_ms_separate_write": ms_rw}
 
 
 def cpu_model() -> str:
@@ -385,6 +401,7 @@ def main():
     achieved = r["achieved_gbs"]
     # measured STREAM-read ceiling of this GPU (reported beside the spec peak)
     stream_gbs = sp.stream_probe(local, 2 << 30, 10)
+    stream_write_gbs = sp.stream_write_probe(local, 2 << 30, 10)
     # and the measured ceiling of random 8-byte x gathers that hit L2: every
     # format here issues one x gather per nnz, so this bounds the gather side
     gather_gps = sp.gather_probe(local, 64 << 20, 1 << 20)
@@ -421,10 +438,17 @@ def main():
                      "kernel": r["kernel"], "algo_bytes_per_launch": r["algo_bytes"],
                      "launch_ms": r["event_ms_per_launch"],
                      "stream_ceiling_gbs": stream_gbs, "frac_of_stream": achieved / stream_gbs,
+                     "stream_write_gbs": stream_write_gbs,
                      **gather_fields,
                      "csr5_model_gbs": csr5_bytes / (r["event_ms_per_launch"] * 1e-3) / 1e9},
         "cpu_baseline": cpu,
         "streamed_bytes_model": streamed_bytes(info) if info["format"] == "bin" else None,
+        # BIN's own byte floor: what this format could do on this GPU at best;
+        # the headline's launch time over it is how close the kernels are
+        "ceiling": (dict(bin_ceiling(streamed_bytes(info), stream_gbs, stream_write_gbs, nnz_local),
+                         frac_of_ceiling=bin_ceiling(streamed_bytes(info), stream_gbs, stream_write_gbs,
+                                                     nnz_local)["implied_ms"] / r["event_ms_per_launch"])
+                    if info["format"] == "bin" else None),
         "formats": results,
         "gen_s": round(t_gen, 2),
         "x_broadcast_ms": round(t_bcast * 1e3, 3) if distributed else None,

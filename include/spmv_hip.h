@@ -177,6 +177,10 @@ const char *spmv_phase_name(spmv_plan_t plan, int32_t k);
  * of a `bytes` buffer (use >> 256 MB), `iters` launches timed with events. */
 int spmv_stream_probe(int32_t device, int64_t bytes, int32_t iters, double *read_gbs);
 
+/* Measured STREAM-write ceiling of `device` (GB/s): nontemporal 16-byte
+ * stores over a `bytes` buffer, `iters` launches timed with events. */
+int spmv_stream_write_probe(int32_t device, int64_t bytes, int32_t iters, double *write_gbs);
+
 /* Measured ceiling of random 8-byte gathers (gathers/s): n streamed int32
  * indices into a `table_bytes` table (1 MB: L2-resident, the best case of a
  * gather-bound SpMV), 8 gathers in flight per lane, best of 5 launches. */

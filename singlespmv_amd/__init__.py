@@ -99,7 +99,7 @@ EXPORTS = [
     "spmv_srand", "spmv_rand_vector", "spmv_verify_coo", "spmv_coo_to_csr", "spmv_gen_count",
     "spmv_gen_fill", "spmv_gen_vector", "spmv_partition_rows", "spmv_save_csr_bin",
     "spmv_load_csr_bin", "spmv_lds_order_probe", "spmv_dist_layout", "spmv_dist_create_csr",
-    "spmv_dist_execute", "spmv_dist_time", "spmv_dist_info", "spmv_dist_destroy",
+    "spmv_dist_execute", "spmv_dist_time", "spmv_dist_info", "spmv_dist_destroy", "spmv_stream_write_probe",
 ]
 
 _lib = None
@@ -129,6 +129,7 @@ def lib():
     L.spmv_time.argtypes = [vp, vp, vp, i32, C.POINTER(f64)]
     L.spmv_profile.argtypes = [vp, vp, vp, i32, C.POINTER(f64), i32, C.POINTER(i32)]
     L.spmv_stream_probe.argtypes = [i32, i64, i32, C.POINTER(f64)]
+    L.spmv_stream_write_probe.argtypes = [i32, i64, i32, C.POINTER(f64)]
     L.spmv_gather_probe.argtypes = [i32, i64, i64, C.POINTER(f64)]
     L.spmv_lds_order_probe.argtypes = [i32, i32, _I32P, _F64P, _F64P]
     L.spmv_dist_layout.argtypes = [_I64P, i64, i32, _I64P, C.POINTER(i64)]
@@ -294,6 +295,13 @@ def stream_probe(device: int = 0, bytes_: int = 2 << 30, iters: int = 10) -> flo
     """Measured STREAM-read GB/s of the device (the practical HBM ceiling)."""
     g = C.c_double()
     _check(lib().spmv_stream_probe(device, bytes_, iters, C.byref(g)), "spmv_stream_probe")
+    return g.value
+
+
+def stream_write_probe(device: int = 0, bytes_: int = 2 << 30, iters: int = 10) -> float:
+    """Measured STREAM-write GB/s of the device (nontemporal 16-B stores)."""
+    g = C.c_double()
+    _check(lib().spmv_stream_write_probe(device, bytes_, iters, C.byref(g)), "spmv_stream_write_probe")
     return g.value
 
 

@@ -71,6 +71,14 @@ __global__ __launch_bounds__(256) void gather_rate_kernel(const int32_t *__restr
     if (acc == 12345.678) *sink = acc;
 }
 
+// STREAM-write ceiling: nontemporal 16-byte stores, one per thread per step
+// (the BIN Mul's product stores are nontemporal 8-byte lanes on 128-B lines)
+__global__ __launch_bounds__(256) void stream_write_kernel(f64x2 *__restrict__ a, int64_t n2) {
+    const int64_t G = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n2; i += G)
+        __builtin_nontemporal_store(f64x2{1.0, (double)i}, a + i);
+}
+
 // Scattered-line write probe (placement experiments, tools/placement_probe.py):
 // every 128-byte line of a window is written once, 16 lanes per line with
 // nontemporal stores (the BIN Mul's product-write shape), lines visited in
@@ -278,5 +286,41 @@ extern "C" int spmv_line_write_probe(int32_t device, void *buf, int64_t bytes, i
     (void)hipEventDestroy(a);
     (void)hipEventDestroy(b);
     *n_windows = nw;
+    return SPMV_SUCCESS;
+}
+
+extern "C" int spmv_stream_write_probe(int32_t device, int64_t bytes, int32_t iters, double *write_gbs) {
+    using namespace spmv;
+    SPMV_CHECK_ARG(write_gbs != nullptr && bytes >= (1 << 20) && iters > 0, "bad arguments");
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count == 0) {
+        (void)hipGetLastError();
+        set_error("no HIP device visible");
+        return SPMV_ERROR_NO_DEVICE;
+    }
+    SPMV_CHECK_ARG(device >= 0 && device < count, "device ordinal out of range");
+    SPMV_HIP_TRY(hipSetDevice(device));
+    const int64_t n2 = bytes / 16;
+    f64x2 *a = nullptr;
+    SPMV_HIP_TRY(hipMalloc(&a, (size_t)n2 * 16));
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    const unsigned blocks = 256 * 16;
+    hipLaunchKernelGGL(stream_write_kernel, dim3(blocks), dim3(256), 0, 0, a, n2);  // warm-up
+    (void)hipEventRecord(e0, 0);
+    for (int i = 0; i < iters; ++i) hipLaunchKernelGGL(stream_write_kernel, dim3(blocks), dim3(256), 0, 0, a, n2);
+    (void)hipEventRecord(e1, 0);
+    const hipError_t e = hipEventSynchronize(e1);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    (void)hipFree(a);
+    if (e != hipSuccess) {
+        set_error(std::string("stream write probe: ") + hipGetErrorString(e));
+        return SPMV_ERROR_HIP;
+    }
+    *write_gbs = (double)n2 * 16 * iters / (ms * 1e-3) / 1e9;
     return SPMV_SUCCESS;
 }
