@@ -28,8 +28,11 @@
 // Determinism / exactness: a bin is owned by one wave, which adds its
 // products in Sum order = column order within each row (strips ascending,
 // columns ascending within a segment); lanes of one ds_add_f64 that hit the
-// same slot are applied in lane order (as k_css.hip relies on, checked bit for
-// bit by the tests); slots start at +0.0 and products are rounded multiplies,
+// same slot are applied in lane order (as k_css.hip relies on) -- the named
+// guard of that hardware behaviour is tests/test_gpu_parity.py::
+// test_lds_add_lane_order (one ds_add_f64 on order-sensitive values), and
+// tests/test_guards.py checks that these adds compile to ds_add_f64 with no
+// CAS loop; slots start at +0.0 and products are rounded multiplies,
 // so every row is the sequential opt_crs sum (src/opt_crs.cpp:61-66) bit for
 // bit, and repeated calls are identical.
 #include "device.hpp"

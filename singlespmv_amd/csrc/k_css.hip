@@ -27,7 +27,9 @@
 // Determinism / exactness: a row (or row piece) is owned by one wave, which
 // adds its entries in ascending column order (ds_add_f64 in program order;
 // lanes of one instruction that hit the same slot are applied in lane = list
-// order by the LDS unit -- observed, and checked bit for bit by the tests);
+// order by the LDS unit -- observed; the named guard is tests/test_gpu_parity.py::
+// test_lds_add_lane_order, and tests/test_guards.py checks the adds compile to
+// ds_add_f64);
 // the slot starts at +0.0.  An unsplit row is therefore the sequential
 // opt_crs sum (src/opt_crs.cpp:61-66) bit for bit; a row longer than half a
 // wave's share is split into pieces whose sums are added in piece order at
