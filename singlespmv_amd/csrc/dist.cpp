@@ -69,7 +69,7 @@ static void dist_free(spmv_dist_s *d) {
 
 // broadcast d_x[0] to every device, on each device's stream
 static int dist_bcast_x(spmv_dist_s *d) {
-    if (d->nd == 1 || d->n == 0) return SPMV_SUCCESS;
+    if (d->n == 0) return SPMV_SUCCESS;  // (N = 1 too: an in-place RCCL broadcast on one rank)
     SPMV_NCCL_TRY(ncclGroupStart());
     for (int k = 0; k < d->nd; ++k) {
         const ncclResult_t r = ncclBroadcast(d->d_x[0], d->d_x[k], (size_t)d->n, ncclDouble, 0, d->comms[k],
@@ -91,7 +91,6 @@ static int dist_local_spmv(spmv_dist_s *d) {
 }
 
 static int dist_gather_y(spmv_dist_s *d) {
-    if (d->nd == 1) return SPMV_SUCCESS;  // d_yfull[0] aliases d_yloc[0]
     SPMV_NCCL_TRY(ncclGroupStart());
     for (int k = 0; k < d->nd; ++k) {
         const ncclResult_t r = ncclAllGather(d->d_yloc[k], d->d_yfull[k], (size_t)d->slice, ncclDouble, d->comms[k],
@@ -194,23 +193,24 @@ int spmv_dist_create_csr(int32_t n_devices, const int32_t *devices, int64_t m, i
         d->plans.push_back(p);
         spmv_set_stream(p, s);
         double *q = nullptr;
-        const bool one = n_devices == 1;
         if (hipMalloc(&q, 8 * (size_t)std::max<int64_t>(n, 1)) != hipSuccess) st = SPMV_ERROR_OUT_OF_MEMORY;
         d->d_x.push_back(q);
         q = nullptr;
         if (st == SPMV_SUCCESS && hipMalloc(&q, 8 * (size_t)d->slice) != hipSuccess) st = SPMV_ERROR_OUT_OF_MEMORY;
         if (q) (void)hipMemset(q, 0, 8 * (size_t)d->slice);
         d->d_yloc.push_back(q);
-        double *f = one ? q : nullptr;
-        if (st == SPMV_SUCCESS && !one && hipMalloc(&f, 8 * (size_t)d->slice * n_devices) != hipSuccess)
+        double *f = nullptr;
+        if (st == SPMV_SUCCESS && hipMalloc(&f, 8 * (size_t)d->slice * n_devices) != hipSuccess)
             st = SPMV_ERROR_OUT_OF_MEMORY;
-        d->d_yfull.push_back(one ? nullptr : f);
+        d->d_yfull.push_back(f);
         if (st != SPMV_SUCCESS) {
             (void)hipGetLastError();
             set_error("spmv_dist_create_csr: device allocation failed on device " + std::to_string(dev));
         }
     }
-    if (st == SPMV_SUCCESS && n_devices > 1) {
+    // RCCL communicators at every N, N = 1 included, so the single-GPU box
+    // runs the same broadcast / all-gather path as an 8-GPU node
+    if (st == SPMV_SUCCESS) {
         d->comms.assign((size_t)n_devices, nullptr);
         const ncclResult_t r = ncclCommInitAll(d->comms.data(), n_devices, d->devs.data());
         if (r != ncclSuccess) {
@@ -243,7 +243,7 @@ int spmv_dist_execute(spmv_dist_t d, const double *x, double *y, uint32_t flags)
     SPMV_RETURN_IF(dist_gather_y(d));
     if (y) {
         SPMV_HIP_TRY(hipSetDevice(d->devs[0]));
-        const double *full = d->nd == 1 ? d->d_yloc[0] : d->d_yfull[0];
+        const double *full = d->d_yfull[0];
         for (int k = 0; k < d->nd; ++k) {
             const int64_t rows = d->cuts[k + 1] - d->cuts[k];
             if (rows)
