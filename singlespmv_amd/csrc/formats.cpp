@@ -64,11 +64,21 @@ int DevArena::alloc_vmm(void **p, size_t n, size_t chunk, int device) {
     // all handles first, then mapped -- in creation order, or (probe build,
     // SPMV_VMM_SHUFFLE) handle k at chunk slot k * P mod count
     const size_t cnt = total / chunk;
-    for (size_t k = 0; k < cnt; ++k) {
+    // probe build, SPMV_VMM_STRIDE=K: create K times the handles and keep
+    // every K-th (the others are released once the kept ones are mapped), so
+    // physically consecutive blocks do not back consecutive chunks
+    size_t K = 1;
+    if (const char *st = probe_env("SPMV_VMM_STRIDE")) K = (size_t)std::max(1, std::min(8, std::atoi(st)));
+    std::vector<hipMemGenericAllocationHandle_t> spare;
+    for (size_t k = 0; k < cnt * K; ++k) {
         hipMemGenericAllocationHandle_t h;
         e = hipMemCreate(&h, chunk, &prop, 0);
-        if (e != hipSuccess) return undo(e, "hipMemCreate");
-        m.handles.push_back(h);
+        if (e != hipSuccess) {
+            for (auto hs : spare) (void)hipMemRelease(hs);
+            return undo(e, "hipMemCreate");
+        }
+        if (k % K == 0) m.handles.push_back(h);
+        else spare.push_back(h);
     }
     size_t P = 1;
     if (const char *sh = probe_env("SPMV_VMM_SHUFFLE"))
@@ -83,10 +93,12 @@ int DevArena::alloc_vmm(void **p, size_t n, size_t chunk, int device) {
         e = hipMemMap((char *)m.va + k * chunk, chunk, 0, m.handles[k], 0);
         if (e != hipSuccess) {
             for (size_t j = k; j < cnt; ++j) (void)hipMemRelease(m.handles[j]);
+            for (auto hs : spare) (void)hipMemRelease(hs);
             m.handles.resize(k);
             return undo(e, "hipMemMap");
         }
     }
+    for (auto hs : spare) (void)hipMemRelease(hs);
     hipMemAccessDesc acc = {};
     acc.location = prop.location;
     acc.flags = hipMemAccessFlagsProtReadWrite;

@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--cols", type=int, default=0)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--window-mb", type=int, default=64)
+    ap.add_argument("--hold-gb", type=float, default=0.0,
+                    help="allocate (and keep) this much device memory before the plans")
     ap.add_argument("--churn-gb", type=float, default=0.0,
                     help="allocate and free this much torch memory between plans")
     a = ap.parse_args()
@@ -37,6 +39,9 @@ def main():
     L.spmv_bin_prod.argtypes = [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_int64)]
     L.spmv_line_write_probe.argtypes = [C.c_int32, C.c_void_p, C.c_int64, C.c_int64, C.c_int32,
                                         C.POINTER(C.c_double), C.c_int32, C.POINTER(C.c_int32)]
+    hold = None
+    if a.hold_gb > 0:
+        hold = torch.empty(int(a.hold_gb * 2**30) // 8, dtype=torch.float64, device="cuda")
     m = a.rows
     n = a.cols or m
     spec = sp.gen_spec("uniform", n, n, per_row=16, seed=42)
@@ -76,7 +81,7 @@ def main():
                 win = [round(gbs[k]) for k in range(nw.value)]
                 plan.time(x, y, 3)
                 ph2 = plan.profile(x, y, a.iters)
-            print(json.dumps({"mode": mode, "env": env, "plan": i, "mul_ms": round(ph["mul"], 4), "sum_ms": round(ph["sum"], 4),
+            print(json.dumps({"mode": mode, "env": env, "plan": i, "hold_gb": a.hold_gb, "mul_ms": round(ph["mul"], 4), "sum_ms": round(ph["sum"], 4),
                               "mul_ms_after": round(ph2["mul"], 4) if win else None,
                               "build_s": round(tb, 2), "plan_gb": round(info["device_bytes"] / 2**30, 3),
                               "free_drop_gb": round((free0 - free1) / 2**30, 3), "y_same": same,
