@@ -236,11 +236,13 @@ extern "C" int spmv_lds_order_probe(int32_t device, int32_t rounds, const int32_
     int32_t *ds = nullptr;
     double *dv = nullptr, *dout = nullptr;
     const size_t n = (size_t)rounds * 64;
-    SPMV_HIP_TRY(hipMalloc(&ds, 4 * n));
-    SPMV_HIP_TRY(hipMalloc(&dv, 8 * n));
-    SPMV_HIP_TRY(hipMalloc(&dout, 8 * 64));
     int st = SPMV_SUCCESS;
-    if (hipMemcpy(ds, slot, 4 * n, hipMemcpyHostToDevice) != hipSuccess ||
+    if (hipMalloc(&ds, 4 * n) != hipSuccess || hipMalloc(&dv, 8 * n) != hipSuccess ||
+        hipMalloc(&dout, 8 * 64) != hipSuccess) {
+        (void)hipGetLastError();
+        set_error("spmv_lds_order_probe: device allocation failed");
+        st = SPMV_ERROR_OUT_OF_MEMORY;
+    } else if (hipMemcpy(ds, slot, 4 * n, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(dv, val, 8 * n, hipMemcpyHostToDevice) != hipSuccess) {
         set_error("spmv_lds_order_probe: upload failed");
         st = SPMV_ERROR_HIP;
