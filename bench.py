@@ -55,10 +55,12 @@ def streamed_bytes(info) -> dict:
     entry, one int32 destination per padded group, the x strips (each strip
     once, plus one re-load per workgroup range boundary) and writes 8 B
     products; Sum reads products 8 + row slot 2 B and writes y."""
-    E = info["stored_slots"]
-    mul_read = E * (8 + 2) + E // max(1, info["bin_pad"]) * 4 + 8 * info["n"]
-    mul_write = 8 * E
-    sum_read = E * (8 + 2)
+    E = info["stored_slots"]  # Mul entries (segments, voids, long blocks)
+    EL = info.get("bin_long_entries", 0)  # long blocks: 4 B lcode instead of a destination per group
+    P = info.get("bin_products") or E  # products + run partials (+ the trash line)
+    mul_read = E * (8 + 2) + (E - EL) // max(1, info["bin_pad"]) * 4 + 4 * EL + 8 * info["n"]
+    mul_write = 8 * P
+    sum_read = P * (8 + 2)
     sum_write = 8 * info["m"]
     return {"mul": mul_read + mul_write, "sum": sum_read + sum_write,
             "total": mul_read + mul_write + sum_read + sum_write,
@@ -276,7 +278,8 @@ def main():
                                             info["placement_candidates"]]
         relevant = {"csr": ("csr_lanes",), "ss": ("ss_sigma",), "ell": ("ell_width",),
                     "hyb": ("ell_width",), "dia": ("n_diags",), "css": ("css_passes", "css_slabs"),
-                    "bin": ("bin_bins", "bin_strips", "bin_strip_cols", "bin_pad", "bin_sum_waves")}
+                    "bin": ("bin_bins", "bin_strips", "bin_strip_cols", "bin_pad", "bin_sum_waves",
+                            "bin_long_len", "bin_long_rows", "bin_long_pieces", "bin_products")}
         if info["format"] == "bin" and fi != 0:
             r["phases_ms"] = plan.profile(x, y, 10)  # Mul / Sum split (opt_ss MulPerf / SumPerf)
         for k in relevant.get(info["format"], ()):

@@ -101,7 +101,12 @@ typedef struct spmv_options {
     int32_t bin_pad;         /* BIN: segment padding 8 | 16 | 32 entries (0 = auto) */
     int32_t csr_row_ptr64;   /* CSR: 1 = 64-bit row pointers below 2^31 nnz too */
     int32_t placement;       /* BIN product buffer / DIA values, see SPMV_PLACEMENT_* */
-    int32_t reserved[4];
+    int32_t bin_long_len;    /* BIN: rows with >= this many entries are reduced per
+                                strip run in the Mul (partial sums, <= 1e-12 from
+                                the sequential sum); 0 = auto (max(128, strips)
+                                when such rows hold >= 5 % of nnz), -1 = never
+                                (every row bit-exact)                         */
+    int32_t reserved[3];
 } spmv_options_t;
 
 /* Placement of the large scratch/value buffer of BIN and DIA plans (the BIN
@@ -110,7 +115,7 @@ typedef struct spmv_options {
 #define SPMV_PLACEMENT_AUTO 0   /* = PLAIN                                           */
 #define SPMV_PLACEMENT_PLAIN 1  /* one hipMalloc, nothing timed: create holds no
                                    device memory beyond the plan's own            */
-#define SPMV_PLACEMENT_SEARCH 2 /* buffers >= 256 MB: up to 8 candidates spread
+#define SPMV_PLACEMENT_SEARCH 2 /* BIN products >= 32 MB, DIA values >= 256 MB: up to 8 candidates spread
                                    over all free HBM, each timed with one launch
                                    over a zero x, the fastest kept -- create
                                    briefly holds most of the free device memory;
@@ -252,6 +257,12 @@ typedef struct spmv_plan_info {
     int32_t placement_candidates; /* SEARCH: candidates timed                  */
     float placement_best_ms;  /* SEARCH: fastest / slowest candidate launch    */
     float placement_worst_ms;
+    int32_t bin_long_len;     /* BIN: long-row threshold in use (0 = none)      */
+    int32_t bin_reserved;
+    int64_t bin_long_rows;    /* BIN: rows on the run path, their run pieces    */
+    int64_t bin_long_pieces;
+    int64_t bin_products;     /* BIN: products + partials the Sum reads         */
+    int64_t bin_long_entries; /* BIN: Mul entries in long blocks (with padding) */
 } spmv_plan_info_t;
 
 int spmv_plan_info(spmv_plan_t plan, spmv_plan_info_t *info);

@@ -57,7 +57,7 @@ class Options(C.Structure):
                 ("dia_max_fill", C.c_double), ("css_slab_shift", C.c_int32), ("css_lag", C.c_int32),
                 ("css_pace", C.c_int32), ("bin_strip_cols", C.c_int32), ("bin_groups", C.c_int32),
                 ("bin_sum_waves", C.c_int32), ("bin_pad", C.c_int32), ("csr_row_ptr64", C.c_int32),
-                ("placement", C.c_int32), ("reserved", C.c_int32 * 4)]
+                ("placement", C.c_int32), ("bin_long_len", C.c_int32), ("reserved", C.c_int32 * 3)]
 
 
 PLACEMENTS = {"auto": 0, "plain": 1, "search": 2, "vmm": 3}
@@ -73,7 +73,10 @@ class PlanInfo(C.Structure):
                 ("bin_bins", C.c_int64), ("bin_strips", C.c_int64), ("bin_strip_cols", C.c_int32),
                 ("bin_pad", C.c_int32), ("bin_sum_waves", C.c_int32), ("bin_groups", C.c_int32),
                 ("placement", C.c_int32), ("placement_candidates", C.c_int32),
-                ("placement_best_ms", C.c_float), ("placement_worst_ms", C.c_float)]
+                ("placement_best_ms", C.c_float), ("placement_worst_ms", C.c_float),
+                ("bin_long_len", C.c_int32), ("bin_reserved", C.c_int32), ("bin_long_rows", C.c_int64),
+                ("bin_long_pieces", C.c_int64), ("bin_products", C.c_int64),
+                ("bin_long_entries", C.c_int64)]
 
     def as_dict(self):
         d = {k: getattr(self, k) for k, _ in self._fields_}
@@ -337,7 +340,8 @@ def make_options(fmt="auto", device: int = -1, csr_lanes: int = 0, ell_width: in
                  ss_sigma: int = 0, dia_max_diags: int = 0, dia_max_fill: float = 0.0,
                  css_slab_shift: int = 0, css_lag: int = 0, css_pace: int = 0,
                  bin_strip_cols: int = 0, bin_groups: int = 0, bin_sum_waves: int = 0,
-                 bin_pad: int = 0, csr_row_ptr64: bool = False, placement="auto") -> Options:
+                 bin_pad: int = 0, csr_row_ptr64: bool = False, placement="auto",
+                 bin_long_len: int = 0) -> Options:
     o = Options()
     lib().spmv_options_default(C.byref(o))
     o.format = FORMATS[fmt] if isinstance(fmt, str) else int(fmt)
@@ -347,6 +351,7 @@ def make_options(fmt="auto", device: int = -1, csr_lanes: int = 0, ell_width: in
     o.bin_strip_cols, o.bin_groups = bin_strip_cols, bin_groups
     o.bin_sum_waves, o.bin_pad, o.csr_row_ptr64 = bin_sum_waves, bin_pad, 1 if csr_row_ptr64 else 0
     o.placement = PLACEMENTS[placement] if isinstance(placement, str) else int(placement)
+    o.bin_long_len = bin_long_len
     return o
 
 

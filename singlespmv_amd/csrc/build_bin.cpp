@@ -41,7 +41,19 @@ struct BinLayout {
     int64_t ES = 0, SB = 1;             // slot entries; strips per block
     std::vector<int64_t> strip_start;   // [G * (S + 1)] Mul-order start of (group, strip)
     std::vector<int64_t> mul_bins;      // [NB] bins in Mul visiting order within each strip (per group)
+    // long rows (internal.hpp BinDev, the run path); LL = 0: none
+    int64_t LL = 0, NP = 0, E1 = 0, TRASH = 0;
+    std::vector<int64_t> eff_rp;        // [m + 1] cumulative Sum entries per row (bin cut)
+    std::vector<int64_t> lb_off;        // [S + 1] long entries of strip t in lb_j / lb_row
+    std::vector<int64_t> lb_j;          // entry index, ordered [strip][row][CSR order]
+    std::vector<int32_t> lb_row;
+    std::vector<int32_t> lpc;           // [NB * S] run pieces of (bin, strip)
+    std::vector<int64_t> lpoff;         // [NB * S] product position of (bin, strip)'s first piece
+    std::vector<int64_t> lpad;          // [S] long entries of strip t, padded to 64
+    std::vector<int64_t> lstart;        // [S] Mul position of strip t's first long block
+    std::vector<int64_t> lcode_off;     // [S] lcode index of the same
     int64_t rpad(int64_t v) const { return (v + PAD - 1) & ~(PAD - 1); }
+    bool is_long(const int64_t *rp, int64_t r) const { return LL > 0 && rp[r + 1] - rp[r] >= LL; }
 };
 
 // ---- parameters (strip width, workgroups, padding, Sum waves) -----------
@@ -117,9 +129,93 @@ static int bin_params(spmv_plan_s *p, const spmv_options_t &o, int64_t m, int64_
     return SPMV_SUCCESS;
 }
 
+// ---- long rows: the threshold, and the Sum entries each row will need
+// (its nnz; a long row: its run pieces, about one per strip it touches)
+static int64_t bin_long_threshold(const spmv_options_t &o, const int64_t *rp, int64_t m, int64_t nnz, int64_t S) {
+    if (o.bin_long_len < 0 || o.bin_groups > 1 || nnz == 0) return 0;
+    if (nnz + nnz / 2 + ((int64_t)S << 6) >= ((int64_t)1 << 31)) return 0;  // product positions are int31
+    const int64_t LL = o.bin_long_len > 0 ? o.bin_long_len : std::max<int64_t>(128, S);
+    int64_t lnnz = 0;
+#pragma omp parallel for schedule(static) reduction(+ : lnnz)
+    for (int64_t r = 0; r < m; ++r) {
+        const int64_t l = rp[r + 1] - rp[r];
+        if (l >= LL) lnnz += l;
+    }
+    if (lnnz == 0) return 0;
+    // auto: only when long rows carry a real share of the entries (config 3:
+    // rows >= 245 entries hold 38 %)
+    if (o.bin_long_len == 0 && lnnz * 20 < nnz) return 0;
+    return LL;
+}
+
+// Sum entries per row for the bin cut, and the long entries bucketed by
+// strip ([strip][row][CSR order], rows ascending).
+static void bin_long_prep(const HostCsr &A, int64_t C, BinLayout &L) {
+    const int64_t m = A.m, S = L.S;
+    std::vector<int64_t> w((size_t)m);
+#pragma omp parallel
+    {
+        std::vector<int32_t> ts;
+#pragma omp for schedule(dynamic, 4096)
+        for (int64_t r = 0; r < m; ++r) {
+            const int64_t l = A.row_ptr[r + 1] - A.row_ptr[r];
+            if (!L.is_long(A.row_ptr, r)) {
+                w[(size_t)r] = l;
+                continue;
+            }
+            ts.clear();
+            for (int64_t j = A.row_ptr[r]; j < A.row_ptr[r + 1]; ++j) ts.push_back(A.col[j] / (int32_t)C);
+            std::sort(ts.begin(), ts.end());
+            w[(size_t)r] = (int64_t)(std::unique(ts.begin(), ts.end()) - ts.begin()) + l / 64;
+        }
+    }
+    L.eff_rp.assign((size_t)m + 1, 0);
+    for (int64_t r = 0; r < m; ++r) L.eff_rp[(size_t)r + 1] = L.eff_rp[(size_t)r] + w[(size_t)r];
+    L.lb_off.assign((size_t)S + 1, 0);
+    for (int64_t r = 0; r < m; ++r)
+        if (L.is_long(A.row_ptr, r))
+            for (int64_t j = A.row_ptr[r]; j < A.row_ptr[r + 1]; ++j) ++L.lb_off[(size_t)(A.col[j] / C) + 1];
+    for (int64_t t = 0; t < S; ++t) L.lb_off[(size_t)t + 1] += L.lb_off[(size_t)t];
+    std::vector<int64_t> cur(L.lb_off.begin(), L.lb_off.end() - 1);
+    L.lb_j.resize((size_t)L.lb_off[(size_t)S]);
+    L.lb_row.resize(L.lb_j.size());
+    for (int64_t r = 0; r < m; ++r)
+        if (L.is_long(A.row_ptr, r))
+            for (int64_t j = A.row_ptr[r]; j < A.row_ptr[r + 1]; ++j) {
+                const int64_t k = cur[(size_t)(A.col[j] / C)]++;
+                L.lb_j[(size_t)k] = j;
+                L.lb_row[(size_t)k] = (int32_t)r;
+            }
+}
+
+// a long entry starts a piece at its row's first entry in the strip and at
+// every 64-entry block boundary
+static inline bool long_starts(const BinLayout &L, int64_t b0, int64_t p) {
+    return p == 0 || (p & 63) == 0 || L.lb_row[(size_t)(b0 + p)] != L.lb_row[(size_t)(b0 + p - 1)];
+}
+
+// run pieces per (bin, strip) and each strip's padded long length
+static void bin_long_count(BinLayout &L) {
+    const int64_t S = L.S, NB = L.NB;
+    L.lpc.assign((size_t)(NB * S), 0);
+    L.lpad.assign((size_t)S, 0);
+#pragma omp parallel for schedule(dynamic, 4)
+    for (int64_t t = 0; t < S; ++t) {
+        const int64_t b0 = L.lb_off[(size_t)t], nt = L.lb_off[(size_t)t + 1] - b0;
+        int64_t b = 0;
+        for (int64_t p = 0; p < nt; ++p) {
+            if (!long_starts(L, b0, p)) continue;
+            const int32_t r = L.lb_row[(size_t)(b0 + p)];
+            while (L.row0[(size_t)b + 1] <= r) ++b;
+            ++L.lpc[(size_t)(b * S + t)];
+        }
+        L.lpad[(size_t)t] = (nt + 63) & ~(int64_t)63;
+    }
+}
+
 // ---- row bins: <= max_rows rows, cut at cumulative nnz targets; a multiple
 // of the Sum kernel's wave count when there are enough rows
-static int bin_rows(spmv_plan_s *p, const int64_t *row_ptr, int64_t m, int64_t n, int64_t nnz, BinLayout &L) {
+static int bin_rows(spmv_plan_s *p, const int64_t *row_ptr, int64_t m, int64_t n, BinLayout &L) {
     BinDev &B = p->bin;
     const int max_rows = B.max_rows;
     L.S = std::max<int64_t>(1, (n + B.strip - 1) / B.strip);
@@ -128,6 +224,9 @@ static int bin_rows(spmv_plan_s *p, const int64_t *row_ptr, int64_t m, int64_t n
     const int64_t waves = (int64_t)B.nwg2 * B.sum_waves;
     int64_t nb = std::max<int64_t>(1, (m + max_rows - 1) / max_rows);
     if (nb * 2 >= waves) nb = (nb + waves - 1) / waves * waves;
+    // cut on the Sum entries per row (long rows: their run pieces)
+    const int64_t *cum = L.LL > 0 ? L.eff_rp.data() : row_ptr;
+    const int64_t total = cum[m];
     L.row0.assign(1, 0);
     for (int64_t r = 0; r < m;) {
         const int64_t b = (int64_t)L.row0.size() - 1;
@@ -135,8 +234,8 @@ static int bin_rows(spmv_plan_s *p, const int64_t *row_ptr, int64_t m, int64_t n
         if (b >= nb - 1) {
             r1 = std::min<int64_t>(m, r + max_rows);
         } else {
-            const int64_t tgt = (int64_t)((__int128)nnz * (b + 1) / nb);
-            r1 = std::lower_bound(row_ptr + r + 1, row_ptr + m + 1, tgt) - row_ptr;
+            const int64_t tgt = (int64_t)((__int128)total * (b + 1) / nb);
+            r1 = std::lower_bound(cum + r + 1, cum + m + 1, tgt) - cum;
             r1 = std::max<int64_t>(r + 1, std::min<int64_t>(r1, r + max_rows));
         }
         L.row0.push_back((int32_t)r1);
@@ -202,10 +301,12 @@ static void bin_offsets(spmv_plan_s *p, const spmv_options_t &o, BinLayout &L) {
     if (const char *e = probe_env("SPMV_BIN_SB")) SB = std::max<int64_t>(1, std::atoll(e));
     if (B.reuse || SB > S) SB = S;
     const int64_t NBK = (S + SB - 1) / SB;
-    B.n_blocks = NBK;
+    // long rows: one more run per bin (its run pieces, [strip][row][piece])
+    const int64_t NR = NBK + (L.LL > 0 ? 1 : 0);
+    B.n_blocks = NR;
     L.off2.assign((size_t)(NB * S), 0);
     L.off1.assign((size_t)(NB * S), 0);
-    L.run_off.assign((size_t)(NBK * NB + 1), 0);
+    L.run_off.assign((size_t)(NR * NB + 1), 0);
     {
         int64_t cur = 0;
         for (int64_t k = 0; k < NBK; ++k)
@@ -216,7 +317,20 @@ static void bin_offsets(spmv_plan_s *p, const spmv_options_t &o, BinLayout &L) {
                     cur += L.rpad(L.cnt[(size_t)(b * S + t)]);
                 }
             }
-        L.run_off[(size_t)(NBK * NB)] = cur;
+        if (L.LL > 0) {
+            L.lpoff.assign((size_t)(NB * S), 0);
+            for (int64_t b = 0; b < NB; ++b) {
+                L.run_off[(size_t)(NBK * NB + b)] = cur;
+                for (int64_t t = 0; t < S; ++t) {
+                    L.lpoff[(size_t)(b * S + t)] = cur;
+                    cur += L.lpc[(size_t)(b * S + t)];
+                }
+            }
+            L.NP = cur - E;
+            // padding lanes and voids write to a trash line past the Sum's runs
+            L.TRASH = L.rpad(cur);
+        }
+        L.run_off[(size_t)(NR * NB)] = cur;
     }
     // slot runs: the same runs, each padded to whole Sum batches
     {
@@ -249,6 +363,7 @@ static void bin_offsets(spmv_plan_s *p, const spmv_options_t &o, BinLayout &L) {
         for (int64_t i = 0; i < nbg; ++i) L.mul_bins[(size_t)(g0 + i)] = g0 + (int64_t)(((__int128)i * P) % nbg);
     }
     L.strip_start.assign((size_t)G * (S + 1), 0);
+    if (L.LL > 0) L.lstart.assign((size_t)S, 0);
     for (int g = 0; g < G; ++g) {
         int64_t cur = B.g_prod[(size_t)g];
         for (int64_t t = 0; t < S; ++t) {
@@ -258,8 +373,18 @@ static void bin_offsets(spmv_plan_s *p, const spmv_options_t &o, BinLayout &L) {
                 L.off1[(size_t)(b * S + t)] = cur;
                 cur += L.rpad(L.cnt[(size_t)(b * S + t)]);
             }
+            if (L.LL > 0) {  // G == 1: void up to a 64-entry boundary, then the long blocks
+                cur = (cur + 63) & ~(int64_t)63;
+                L.lstart[(size_t)t] = cur;
+                cur += L.lpad[(size_t)t];
+            }
         }
         L.strip_start[(size_t)(g * (S + 1) + S)] = cur;
+    }
+    L.E1 = L.strip_start.back();
+    if (L.LL > 0) {
+        L.lcode_off.assign((size_t)S, 0);
+        for (int64_t t = 1; t < S; ++t) L.lcode_off[(size_t)t] = L.lcode_off[(size_t)t - 1] + L.lpad[(size_t)t - 1];
     }
 }
 
@@ -269,13 +394,27 @@ static void bin_offsets(spmv_plan_s *p, const spmv_options_t &o, BinLayout &L) {
 // (the sequential opt_crs order), but consecutive lanes of one ds_add_f64 hit
 // different rows instead of all landing on one slot (a banded or long row
 // otherwise serialises the LDS atomics 64 ways).
-static int bin_fill_host(spmv_plan_s *p, const HostCsr &A, const BinLayout &L) {
-    BinDev &B = p->bin;
-    const int64_t S = L.S, NB = L.NB, E = L.E, C = B.strip, PAD = L.PAD;
+// The entry arrays as the host builder lays them out (uploaded by
+// bin_fill_host; tests/bin_layout_check.cpp emulates the kernels on them).
+struct BinHostArrays {
+    std::vector<double> val1;
+    std::vector<uint16_t> cs1, slot2;
+    std::vector<int32_t> dst1, lcode;
+    std::vector<int64_t> lshift;
+};
+
+static void bin_fill_arrays(const BinDev &B, const HostCsr &A, const BinLayout &L, BinHostArrays &H) {
+    const int64_t S = L.S, NB = L.NB, E1 = L.E1, C = B.strip, PAD = L.PAD;
     const int max_rows = B.max_rows;
-    std::vector<double> val1((size_t)E);
-    std::vector<uint16_t> cs1((size_t)E), slot2((size_t)L.ES, (uint16_t)max_rows);
-    std::vector<int32_t> dst1((size_t)(E >> B.pad_log));
+    // voids between a strip's segments and its long blocks stay zero; their
+    // destination groups (and the long blocks') point at the trash line
+    std::vector<double> &val1 = H.val1;
+    std::vector<uint16_t> &cs1 = H.cs1, &slot2 = H.slot2;
+    std::vector<int32_t> &dst1 = H.dst1;
+    val1.assign((size_t)E1, 0.0);
+    cs1.assign((size_t)E1, 0);
+    slot2.assign((size_t)L.ES, (uint16_t)max_rows);
+    dst1.assign((size_t)(E1 >> B.pad_log), (int32_t)(L.TRASH >> B.pad_log));
     std::vector<int> gof((size_t)NB);
     for (int g = 0; g < B.G; ++g)
         for (int64_t b = B.g_bin[(size_t)g]; b < B.g_bin[(size_t)g + 1]; ++b) gof[(size_t)b] = g;
@@ -297,6 +436,7 @@ static int bin_fill_host(spmv_plan_s *p, const HostCsr &A, const BinLayout &L) {
             kpos.assign((size_t)segbase[(size_t)S], 0);
             // pass 1: per segment, how many rows have a k-th entry
             for (int64_t r = row0[b]; r < row0[b + 1]; ++r) {
+                if (L.is_long(A.row_ptr, r)) continue;  // run path
                 for (int64_t j = A.row_ptr[r]; j < A.row_ptr[r + 1]; ++j) {
                     const int64_t t = A.col[j] / C;
                     ++kpos[(size_t)(segbase[(size_t)t] + rowk[(size_t)t]++)];
@@ -314,6 +454,7 @@ static int bin_fill_host(spmv_plan_s *p, const HostCsr &A, const BinLayout &L) {
             }
             // pass 2: place every entry
             for (int64_t r = row0[b]; r < row0[b + 1]; ++r) {
+                if (L.is_long(A.row_ptr, r)) continue;
                 const uint16_t slot = (uint16_t)(r - row0[b]);
                 for (int64_t j = A.row_ptr[r]; j < A.row_ptr[r + 1]; ++j) {
                     const int32_t c = A.col[j];
@@ -338,10 +479,60 @@ static int bin_fill_host(spmv_plan_s *p, const HostCsr &A, const BinLayout &L) {
             }
         }
     }
-    SPMV_RETURN_IF(upload_vec(p, &B.val1, val1));
-    SPMV_RETURN_IF(upload_vec(p, &B.cs1, cs1));
-    SPMV_RETURN_IF(upload_vec(p, &B.dst1, dst1));
-    SPMV_RETURN_IF(upload_vec(p, &B.slot2, slot2));
+    if (L.LL > 0) {
+        // long blocks of every strip: entries in [row][CSR order], each lane's
+        // lcode = piece start bit | (last entry of its piece ? the piece's
+        // product position : 0x7FFFFFFF); the piece's slot in the bin's long run
+        std::vector<int32_t> &lcode = H.lcode;
+        lcode.assign((size_t)(L.lcode_off.back() + L.lpad.back()), 0);
+        const int64_t NBK = B.n_blocks - 1;
+#pragma omp parallel for schedule(dynamic, 4)
+        for (int64_t t = 0; t < S; ++t) {
+            const int64_t b0 = L.lb_off[(size_t)t], nt = L.lb_off[(size_t)t + 1] - b0;
+            const int64_t ms = L.lstart[(size_t)t], cs = L.lcode_off[(size_t)t];
+            int64_t b = 0, pos = -1, lastb = -1;
+            for (int64_t p2 = 0; p2 < nt; ++p2) {
+                const int32_t r = L.lb_row[(size_t)(b0 + p2)];
+                const int64_t j = L.lb_j[(size_t)(b0 + p2)];
+                const bool start = long_starts(L, b0, p2);
+                if (start) {
+                    while (L.row0[(size_t)b + 1] <= r) ++b;
+                    if (b != lastb) {
+                        pos = L.lpoff[(size_t)(b * S + t)];
+                        lastb = b;
+                    } else {
+                        ++pos;
+                    }
+                    const size_t run = (size_t)(NBK * NB + b);
+                    slot2[(size_t)bin_slot_index(pos, L.run_off[run], L.srun_off[run], B.slot_linear ? 0 : B.sum_u)] =
+                        (uint16_t)(r - L.row0[(size_t)b]);
+                }
+                const bool end = p2 + 1 == nt || long_starts(L, b0, p2 + 1);
+                val1[(size_t)(ms + p2)] = A.val[j];
+                cs1[(size_t)(ms + p2)] = (uint16_t)(A.col[j] - t * C);
+                lcode[(size_t)(cs + p2)] = (int32_t)((start ? 0x80000000u : 0u) | (end ? (uint32_t)pos : 0x7FFFFFFFu));
+            }
+            for (int64_t p2 = nt; p2 < L.lpad[(size_t)t]; ++p2)  // padding lanes: own piece, to the trash line
+                lcode[(size_t)(cs + p2)] = (int32_t)(0x80000000u | (uint32_t)L.TRASH);
+        }
+        H.lshift.resize((size_t)S);
+        for (int64_t t = 0; t < S; ++t) H.lshift[(size_t)t] = L.lcode_off[(size_t)t] - L.lstart[(size_t)t];
+    }
+}
+
+static int bin_fill_host(spmv_plan_s *p, const HostCsr &A, const BinLayout &L) {
+    BinDev &B = p->bin;
+    BinHostArrays H;
+    bin_fill_arrays(B, A, L, H);
+    if (L.LL > 0) {
+        SPMV_RETURN_IF(upload_vec(p, &B.lcode, H.lcode));
+        SPMV_RETURN_IF(upload_vec(p, &B.lstart, L.lstart));
+        SPMV_RETURN_IF(upload_vec(p, &B.lshift, H.lshift));
+    }
+    SPMV_RETURN_IF(upload_vec(p, &B.val1, H.val1));
+    SPMV_RETURN_IF(upload_vec(p, &B.cs1, H.cs1));
+    SPMV_RETURN_IF(upload_vec(p, &B.dst1, H.dst1));
+    SPMV_RETURN_IF(upload_vec(p, &B.slot2, H.slot2));
     return SPMV_SUCCESS;
 }
 
@@ -462,7 +653,9 @@ static int bin_place_prod(spmv_plan_s *p, int64_t n, size_t prod_bytes, const sp
     // free HBM; VMM 2-MB handles were fast on some boxes and not on others
     // (profiles/round2/placement/, DESIGN §4a "Placement").
     if (mode == SPMV_PLACEMENT_AUTO) mode = SPMV_PLACEMENT_PLAIN;
-    if (mode == SPMV_PLACEMENT_SEARCH && prod_bytes < ((size_t)256 << 20)) mode = SPMV_PLACEMENT_PLAIN;
+    // the Mul of a 184 MB product buffer (config 3 with long rows) varies 0.118-0.151 ms
+    // by placement as much as config 2's does: search from 32 MB
+    if (mode == SPMV_PLACEMENT_SEARCH && prod_bytes < ((size_t)32 << 20)) mode = SPMV_PLACEMENT_PLAIN;
     B.placement = mode;
     if (mode == SPMV_PLACEMENT_SEARCH) return bin_place_search(p, n, prod_bytes);
     if (mode == SPMV_PLACEMENT_VMM) {
@@ -477,15 +670,18 @@ static int bin_place_prod(spmv_plan_s *p, int64_t n, size_t prod_bytes, const sp
 }
 
 // ---- Mul pieces, small tables, product buffer -----------------------------
-static int bin_finish(spmv_plan_s *p, int64_t n, const BinLayout &L, const spmv_options_t &o) {
-    BinDev &B = p->bin;
-    const int64_t S = L.S, E = L.E;
-    // Mul pieces: each workgroup takes an nnz-balanced range of its group's
-    // Mul-ordered entries (cut at 64-entry multiples), split at strips
-    std::vector<int64_t> piece_off{0}, pbeg, pend;
-    std::vector<int32_t> pstrip;
+// Mul pieces: each workgroup takes an nnz-balanced range of its group's
+// Mul-ordered entries (cut at 64-entry multiples), split at strips
+struct BinPieces {
+    std::vector<int64_t> off{0}, beg, end;
+    std::vector<int32_t> strip;
+};
+static void bin_pieces(const BinDev &B, const BinLayout &L, BinPieces &P) {
+    const int64_t S = L.S;
     for (int g = 0; g < B.G; ++g) {
-        const int64_t g0 = B.g_prod[(size_t)g], g1 = B.g_prod[(size_t)g + 1];
+        // Mul-order range of the group (with long rows, G == 1: segments,
+        // voids and long blocks)
+        const int64_t g0 = B.g_prod[(size_t)g], g1 = L.LL > 0 ? L.E1 : B.g_prod[(size_t)g + 1];
         const int64_t *ss = L.strip_start.data() + (size_t)g * (S + 1);
         int64_t s = 0;
         for (int k = 0; k < B.nwg1; ++k) {
@@ -495,15 +691,24 @@ static int bin_finish(spmv_plan_s *p, int64_t n, const BinLayout &L, const spmv_
             for (int64_t t = s; t < S && ss[t] < z; ++t) {
                 const int64_t lo = std::max(a, ss[t]), hi = std::min(z, ss[t + 1]);
                 if (lo < hi) {
-                    pstrip.push_back((int32_t)t);
-                    pbeg.push_back(lo);
-                    pend.push_back(hi);
+                    P.strip.push_back((int32_t)t);
+                    P.beg.push_back(lo);
+                    P.end.push_back(hi);
                 }
             }
-            piece_off.push_back((int64_t)pstrip.size());
+            P.off.push_back((int64_t)P.strip.size());
         }
     }
-    B.prod_cap = B.reuse ? 0 : E;
+}
+
+static int bin_finish(spmv_plan_s *p, int64_t n, const BinLayout &L, const spmv_options_t &o) {
+    BinDev &B = p->bin;
+    const int64_t E = L.E;
+    BinPieces P;
+    bin_pieces(B, L, P);
+    std::vector<int64_t> &piece_off = P.off, &pbeg = P.beg, &pend = P.end;
+    std::vector<int32_t> &pstrip = P.strip;
+    B.prod_cap = B.reuse ? 0 : (L.LL > 0 ? L.TRASH + L.PAD : E);
     if (B.reuse)
         for (int g = 0; g < B.G; ++g) B.prod_cap = std::max(B.prod_cap, B.g_prod[(size_t)g + 1] - B.g_prod[(size_t)g]);
     const size_t prod_bytes = sizeof(double) * (size_t)std::max<int64_t>(B.prod_cap, 1);
@@ -521,7 +726,12 @@ static int bin_finish(spmv_plan_s *p, int64_t n, const BinLayout &L, const spmv_
         for (float tt : B.placement_ms) std::fprintf(stderr, " %.4f", tt);
         std::fprintf(stderr, "\n");
     }
-    p->stored_slots = E;
+    p->stored_slots = L.E1;
+    B.mul_entries = L.E1;
+    B.long_len = L.LL;
+    B.long_pieces = L.NP;
+    B.long_entries = 0;
+    for (int64_t v : L.lpad) B.long_entries += v;
     p->n_kernels = B.reuse ? 2 * B.G : B.G + 1;
     return SPMV_SUCCESS;
 }
@@ -534,15 +744,25 @@ int build_bin(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
         return SPMV_SUCCESS;
     }
     BinLayout L;
-    SPMV_RETURN_IF(bin_rows(p, A.row_ptr, A.m, A.n, A.nnz, L));
-    // segment sizes (bin b, strip s)
+    L.S = std::max<int64_t>(1, (A.n + B.strip - 1) / B.strip);
+    L.LL = bin_long_threshold(o, A.row_ptr, A.m, A.nnz, L.S);
+    if (L.LL > 0) {
+        bin_long_prep(A, B.strip, L);
+        for (int64_t r = 0; r < A.m; ++r) B.long_rows += L.is_long(A.row_ptr, r) ? 1 : 0;
+    }
+    SPMV_RETURN_IF(bin_rows(p, A.row_ptr, A.m, A.n, L));
+    // segment sizes (bin b, strip s); long rows are not in the segments
     const int64_t S = L.S, NB = L.NB, C = B.strip;
     L.cnt.assign((size_t)(NB * S), 0);
 #pragma omp parallel for schedule(dynamic, 16)
     for (int64_t b = 0; b < NB; ++b) {
         int32_t *cb = L.cnt.data() + b * S;
-        for (int64_t j = A.row_ptr[L.row0[(size_t)b]]; j < A.row_ptr[L.row0[(size_t)b + 1]]; ++j) ++cb[A.col[j] / C];
+        for (int64_t r = L.row0[(size_t)b]; r < L.row0[(size_t)b + 1]; ++r) {
+            if (L.is_long(A.row_ptr, r)) continue;
+            for (int64_t j = A.row_ptr[r]; j < A.row_ptr[r + 1]; ++j) ++cb[A.col[j] / C];
+        }
     }
+    if (L.LL > 0) bin_long_count(L);
     bin_offsets(p, o, L);
     SPMV_RETURN_IF(bin_fill_host(p, A, L));
     return bin_finish(p, A.n, L, o);
@@ -558,8 +778,11 @@ int build_bin_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, 
     }
     std::vector<int64_t> rp((size_t)p->m + 1);
     SPMV_HIP_TRY(hipMemcpy(rp.data(), d_rp, 8 * (size_t)(p->m + 1), hipMemcpyDeviceToHost));
+    // long rows take the host builder (the run path is laid out on the host)
+    if (bin_long_threshold(o, rp.data(), p->m, p->nnz, std::max<int64_t>(1, (p->n + B.strip - 1) / B.strip)) > 0)
+        return kBinNeedHostBuild;
     BinLayout L;
-    SPMV_RETURN_IF(bin_rows(p, rp.data(), p->m, p->n, p->nnz, L));
+    SPMV_RETURN_IF(bin_rows(p, rp.data(), p->m, p->n, L));
     std::vector<int64_t> bstart((size_t)L.NB + 1);
     for (int64_t b = 0; b <= L.NB; ++b) bstart[(size_t)b] = rp[(size_t)L.row0[(size_t)b]];
     std::vector<int64_t>().swap(rp);

@@ -220,6 +220,18 @@ struct CssDev {
 // ds_add_f64 and writes y -> deterministic, and an unsplit row's sum is the
 // sequential opt_crs sum (column order) bit for bit.  Row groups bound the
 // product buffer (re-used by every group: it can stay in the Infinity Cache).
+//
+// Long rows (>= long_len entries; power-law rows with many entries per
+// strip) leave the segments: each strip's Mul range ends with their runs in
+// the strip, packed in 64-entry blocks (the strip's range is 64-aligned, a
+// void of zero entries after the segments).  The Mul reduces a block's runs
+// with a segmented wave scan and writes one partial per run piece (a run
+// cut at a block boundary is two pieces) to the piece's place in the bin's
+// long run, which the Sum adds after the bin's segments (one more run per
+// bin).  lcode per long entry: bit 31 = first entry of a piece, bits 0-30 =
+// the piece's product position on its last entry, else 0x7FFFFFFF.  A long
+// row is the sum of its pieces in (strip, piece) order -- deterministic, not
+// the sequential order (<= 1e-12 relative), like CSS's split rows.
 constexpr int kBinLdsDoubles = 20480;  // Sum: 160 KB of LDS y slices per workgroup
 constexpr int kBinMulThreads = 1024;
 constexpr int kBinMaxStrip = 20480;  // Mul: x strip of 160 KB of LDS
@@ -268,6 +280,12 @@ struct BinDev {
     int64_t prod_cap = 0;
     int placement = 0;            // how prod was allocated (spmv_options_t.placement, resolved)
     bool mul_perm = false;        // Mul visits a strip's bins in scrambled order (build_bin.cpp)
+    int64_t long_len = 0;         // rows with >= long_len entries take the run path (0: none)
+    int64_t long_rows = 0, long_pieces = 0, long_entries = 0;
+    int64_t mul_entries = 0;      // Mul-order length (segments + voids + long blocks)
+    int64_t *lstart = nullptr;    // [n_strips]: Mul position where the strip's long blocks start
+    int64_t *lshift = nullptr;    // [n_strips]: lcode index - Mul position in those blocks
+    int32_t *lcode = nullptr;     // per long-block entry: piece start bit | product position
     int dbg = 0;  // SPMV_BIN_DEBUG (probe build only)
     std::vector<float> placement_ms;  // Mul ms of each product-buffer candidate
 };

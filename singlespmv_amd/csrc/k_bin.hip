@@ -52,27 +52,85 @@ struct MulBatch {
     int32_t d[U];
 };
 
-template <int U, int PL, int MODE>
+// LONG: blocks at or past `ls` (the strip's long blocks, 64-aligned) load
+// their lcode word instead of the segment destination.
+template <int U, int PL, int MODE, bool LONG>
 __device__ __forceinline__ void mul_load(MulBatch<U> &B, int64_t base, int64_t e0, int64_t e1, int lane,
                                          const double *__restrict__ val1, const uint16_t *__restrict__ cs1,
-                                         const int32_t *__restrict__ dst1) {
+                                         const int32_t *__restrict__ dst1, int64_t ls, int64_t lsh,
+                                         const int32_t *__restrict__ lcode) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const int64_t e = base + u * 64 + lane;
         const int64_t ee = e < e1 ? e : e0;
         B.v[u] = ld_stream(val1 + ee);
         B.c[u] = (MODE & 8) ? (uint32_t)((ee * 2654435761u) & 16383) : (uint32_t)__builtin_nontemporal_load(cs1 + ee);
-        B.d[u] = ld_stream(dst1 + (ee >> PL));
+        // a lane past the piece (e >= e1, masked at the store) reads word 0:
+        // its clamped e0 may lie in the segments, before the long blocks
+        if (LONG && base + u * 64 >= ls) B.d[u] = ld_stream(lcode + (e < e1 ? e + lsh : 0));
+        else B.d[u] = ld_stream(dst1 + (ee >> PL));
     }
 }
 
-template <int U, int MODE, int PL>
+// 64-bit DPP move (two 32-bit v_mov_dpp): lanes the control does not feed
+// (or rows outside ROWMASK) read 0
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ double dpp_f64(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, ROWMASK, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, ROWMASK, 0xF, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+// One 64-entry long block: inclusive segmented scan of the products over the
+// lanes (pieces start where lcode's bit 31 is set), then the last lane of
+// every piece writes its partial.  The scan is a fixed DPP tree -- row_shr
+// 1/2/4/8 inside each 16-lane row, then row_bcast15 (rows 1, 3) and
+// row_bcast31 (rows 2, 3) -- so a partial is deterministic; a lane adds a
+// source only from its own piece (source lane >= the piece's first lane).
+template <int MODE>
+__device__ __forceinline__ void mul_long_block(double pr, int32_t code, bool ok, int lane,
+                                               double *__restrict__ prod) {
+    const bool start = code < 0 || !ok;
+    const uint64_t starts = __ballot(start);
+    const uint64_t upto = starts & (~0ull >> (63 - lane));
+    const int seg = 63 - __clzll((long long)upto);
+    const int r16 = lane & 15, row = lane >> 4;
+    double v = ok ? pr : 0.0, t;
+    t = dpp_f64<0x111, 0xF>(v);  // row_shr:1
+    if (r16 >= 1 && lane - 1 >= seg) v = __dadd_rn(t, v);
+    t = dpp_f64<0x112, 0xF>(v);  // row_shr:2
+    if (r16 >= 2 && lane - 2 >= seg) v = __dadd_rn(t, v);
+    t = dpp_f64<0x114, 0xF>(v);  // row_shr:4
+    if (r16 >= 4 && lane - 4 >= seg) v = __dadd_rn(t, v);
+    t = dpp_f64<0x118, 0xF>(v);  // row_shr:8
+    if (r16 >= 8 && lane - 8 >= seg) v = __dadd_rn(t, v);
+    t = dpp_f64<0x142, 0xA>(v);  // row_bcast:15 -> rows 1 and 3
+    if ((row & 1) && seg <= row * 16 - 1) v = __dadd_rn(t, v);
+    t = dpp_f64<0x143, 0xC>(v);  // row_bcast:31 -> rows 2 and 3
+    if (row >= 2 && seg <= 31) v = __dadd_rn(t, v);
+    const int32_t pos = code & 0x7FFFFFFF;
+    // Plain stores: a piece's 8-byte partial shares its 128-B line with the
+    // neighbouring pieces of its (bin, strip), written by the next lanes or
+    // the next block -- kept in L2 they merge into whole lines.  Nontemporal
+    // partial stores cost the Mul that follows a Sum 0.111 -> 0.137 ms at
+    // config 3 (profiles/round2/probe/c3_long_store.jsonl).  MODE 16 / 32
+    // (probe ablations): nontemporal partial stores / none (wrong sums).
+    if ((MODE & 32) == 0 && ok && pos != 0x7FFFFFFF) {
+        if (MODE & 16) __builtin_nontemporal_store(v, prod + pos);
+        else prod[pos] = v;
+    }
+}
+
+template <int U, int MODE, int PL, bool LONG>
 __device__ __forceinline__ void mul_store(const MulBatch<U> &B, int64_t base, int64_t e1, int lane,
-                                          const double *xs, double *__restrict__ prod) {
+                                          const double *xs, double *__restrict__ prod, int64_t ls) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const int64_t e = base + u * 64 + lane;
-        if (e < e1) {
+        if (LONG && base + u * 64 >= ls) {
+            mul_long_block<MODE>(__dmul_rn(B.v[u], xs[B.c[u]]), B.d[u], e < e1, lane, prod);
+        } else if (e < e1) {
             const double pr = __dmul_rn(B.v[u], xs[B.c[u]]);
             // MODE 4 (ablation): write in Mul order (sequential) instead of Sum order
             double *dp = (MODE & 4) ? prod + e : prod + ((int64_t)B.d[u] << PL) + (e & ((1 << PL) - 1));
@@ -90,12 +148,13 @@ __device__ __forceinline__ void mul_store(const MulBatch<U> &B, int64_t base, in
 // MODE (SPMV_BIN_DEBUG, internal ablations): 1 nontemporal product stores,
 // 2 no product stores (value kept alive), 4 products written in Mul order
 // (sequential; wrong results -- measures the cost of the scattered layout).  PL: segments padded to 2^PL entries.
-template <int U, int MODE, int PL>
+template <int U, int MODE, int PL, bool LONG>
 __global__ __launch_bounds__(kBinMulThreads) void bin_mul_kernel(
     const int64_t *__restrict__ piece_off, int64_t q_base, const int32_t *__restrict__ piece_strip,
     const int64_t *__restrict__ piece_begin, const int64_t *__restrict__ piece_end,
     const double *__restrict__ val1, const uint16_t *__restrict__ cs1, const int32_t *__restrict__ dst1,
-    const double *__restrict__ x, int64_t n, int32_t strip, double *__restrict__ prod) {
+    const double *__restrict__ x, int64_t n, int32_t strip, double *__restrict__ prod,
+    const int64_t *__restrict__ lstart, const int64_t *__restrict__ lshift, const int32_t *__restrict__ lcode) {
     __shared__ double xs[kBinMaxStrip];
     constexpr int NW = kBinMulThreads / 64;
     constexpr int64_t STEP = (int64_t)NW * 64 * U;
@@ -104,8 +163,10 @@ __global__ __launch_bounds__(kBinMulThreads) void bin_mul_kernel(
     const int64_t q0 = piece_off[q_base + blockIdx.x], q1 = piece_off[q_base + blockIdx.x + 1];
     for (int64_t q = q0; q < q1; ++q) {
         // consecutive pieces of a workgroup are consecutive strips: stage x
-        const int64_t c0 = (int64_t)piece_strip[q] * strip;
+        const int32_t st = piece_strip[q];
+        const int64_t c0 = (int64_t)st * strip;
         const int64_t e0 = piece_begin[q], e1 = piece_end[q];
+        const int64_t ls = LONG ? lstart[st] : INT64_MAX, lsh = LONG ? lshift[st] : 0;
         const int cw = (int)(n - c0 < strip ? n - c0 : strip);
         __syncthreads();  // the previous strip's readers are done
         for (int i = threadIdx.x; i < cw; i += kBinMulThreads) xs[i] = x[c0 + i];
@@ -113,14 +174,15 @@ __global__ __launch_bounds__(kBinMulThreads) void bin_mul_kernel(
         const int64_t first = e0 + (int64_t)w * 64 * U;
         const int64_t nit = first < e1 ? (e1 - first + STEP - 1) / STEP : 0;
         MulBatch<U> A, B;
-        if (nit > 0) mul_load<U, PL, MODE>(A, first, e0, e1, lane, val1, cs1, dst1);
+        if (nit > 0) mul_load<U, PL, MODE, LONG>(A, first, e0, e1, lane, val1, cs1, dst1, ls, lsh, lcode);
         for (int64_t it = 0; it < nit; it += 2) {
             const int64_t ba = first + it * STEP, bb = ba + STEP;
-            if (it + 1 < nit) mul_load<U, PL, MODE>(B, bb, e0, e1, lane, val1, cs1, dst1);
-            mul_store<U, MODE, PL>(A, ba, e1, lane, xs, prod);
+            if (it + 1 < nit) mul_load<U, PL, MODE, LONG>(B, bb, e0, e1, lane, val1, cs1, dst1, ls, lsh, lcode);
+            mul_store<U, MODE, PL, LONG>(A, ba, e1, lane, xs, prod, ls);
             if (it + 1 < nit) {
-                if (it + 2 < nit) mul_load<U, PL, MODE>(A, bb + STEP, e0, e1, lane, val1, cs1, dst1);
-                mul_store<U, MODE, PL>(B, bb, e1, lane, xs, prod);
+                if (it + 2 < nit)
+                    mul_load<U, PL, MODE, LONG>(A, bb + STEP, e0, e1, lane, val1, cs1, dst1, ls, lsh, lcode);
+                mul_store<U, MODE, PL, LONG>(B, bb, e1, lane, xs, prod, ls);
             }
         }
     }
@@ -162,11 +224,24 @@ __device__ __forceinline__ void sum_load(SumBatch<U, MODE> &B, int64_t base, int
 #pragma unroll
         for (int h = 0; h < 4; ++h) B.w[4 * q + h] = w[h];
     }
+    if constexpr ((MODE & 16) != 0) {
+        // ablation (wrong sums): the same bytes as 16-byte loads, lane l
+        // reading products 2l, 2l+1 of each 128-entry block
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-        const int64_t e = base + u * 64 + lane;
-        const int64_t ee = e < p1 ? e : p0;
-        B.v[u] = (MODE & 1) ? ld_stream(prod + (ee - pbase)) : prod[ee - pbase];
+        for (int u = 0; u < U; u += 2) {
+            const int64_t e = base + (u / 2) * 128 + 2 * lane;
+            const int64_t ee = e + 1 < p1 ? e : p0;
+            const f64x2 v = ld_stream2(prod + (ee - pbase));
+            B.v[u] = v.x;
+            B.v[u + 1] = v.y;
+        }
+    } else {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t e = base + u * 64 + lane;
+            const int64_t ee = e < p1 ? e : p0;
+            B.v[u] = (MODE & 1) ? ld_stream(prod + (ee - pbase)) : prod[ee - pbase];
+        }
     }
     if ((MODE & 12) == 4) {
 #pragma unroll
@@ -247,9 +322,14 @@ __global__ __launch_bounds__(64 * W2) void bin_sum_kernel(
 template <int MODE, int PL>
 static void launch_mul_t(const spmv_plan_s *p, int g, const double *x) {
     const BinDev &B = p->bin;
-    hipLaunchKernelGGL((bin_mul_kernel<8, MODE, PL>), dim3((unsigned)B.nwg1), dim3(kBinMulThreads), 0,
-                       p->stream, B.piece_off, (int64_t)g * B.nwg1, B.piece_strip, B.piece_begin, B.piece_end,
-                       B.val1, B.cs1, B.dst1, x, p->n, (int32_t)B.strip, B.prod);
+    if (B.long_len > 0)
+        hipLaunchKernelGGL((bin_mul_kernel<8, MODE, PL, true>), dim3((unsigned)B.nwg1), dim3(kBinMulThreads), 0,
+                           p->stream, B.piece_off, (int64_t)g * B.nwg1, B.piece_strip, B.piece_begin, B.piece_end,
+                           B.val1, B.cs1, B.dst1, x, p->n, (int32_t)B.strip, B.prod, B.lstart, B.lshift, B.lcode);
+    else
+        hipLaunchKernelGGL((bin_mul_kernel<8, MODE, PL, false>), dim3((unsigned)B.nwg1), dim3(kBinMulThreads), 0,
+                           p->stream, B.piece_off, (int64_t)g * B.nwg1, B.piece_strip, B.piece_begin, B.piece_end,
+                           B.val1, B.cs1, B.dst1, x, p->n, (int32_t)B.strip, B.prod, nullptr, nullptr, nullptr);
 }
 
 template <int PL>
@@ -267,7 +347,11 @@ static void launch_mul_p(const spmv_plan_s *p, int g, const double *x) {
             if (p->bin.dbg & 256) launch_mul_t<13, PL>(p, g, x);
             else launch_mul_t<5, PL>(p, g, x);
             break;
-        default: launch_mul_t<1, PL>(p, g, x);
+        default:
+            // long-block partial stores: 2048 nontemporal, 4096 none (ablations)
+            if (p->bin.dbg & 2048) launch_mul_t<17, PL>(p, g, x);
+            else if (p->bin.dbg & 4096) launch_mul_t<33, PL>(p, g, x);
+            else launch_mul_t<1, PL>(p, g, x);
     }
 #endif
 }
@@ -298,6 +382,10 @@ static void launch_sum_w(const spmv_plan_s *p, int g, double *y) {
     // probe build: SPMV_BIN_DEBUG bits 2-3 -> Sum MODE
     if (p->bin.dbg & 512) {  // ablation: no slot loads
         launch_sum_t<W2, U, 4>(p, g, y);
+        return;
+    }
+    if (p->bin.dbg & 1024) {  // ablation: 16-byte product loads (wrong sums)
+        launch_sum_t<W2, U, 17>(p, g, y);
         return;
     }
     // default: nontemporal product loads (config 2 Sum 0.308 -> 0.298 ms,

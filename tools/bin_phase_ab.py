@@ -1,0 +1,84 @@
+#!/usr/bin/env python3
+"""In-process A/B of BIN plan variants, Mul and Sum timed separately.
+
+Each variant is a set of probe-build environment switches read at plan build
+(SPMV_BIN_*; run with SPMV_HIP_LIBRARY=probes_build/libspmv_hip.so); every
+plan of the process is built from the same CSR, then the plans are profiled
+in interleaved rounds (cdna_hip_programming.md rule 24).  One JSON line per
+(round, variant).
+
+  SPMV_HIP_LIBRARY=probes_build/libspmv_hip.so python tools/bin_phase_ab.py \
+      --variants 'base:;ld16:SPMV_BIN_DEBUG=1024' --rows 10000000
+"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--variants", required=True,
+                    help="name:VAR=v,opt=v;name:... (UPPER-case keys: probe environment; lower-case: plan options)")
+    ap.add_argument("--kind", default="uniform")
+    ap.add_argument("--rows", type=int, default=10_000_000)
+    ap.add_argument("--ncols", type=int, default=0)
+    ap.add_argument("--per-row", type=int, default=16)
+    ap.add_argument("--max-len", type=int, default=10000)
+    ap.add_argument("--rounds", type=int, default=4)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--placement", default="search")
+    ap.add_argument("--check", action="store_true", help="bit-equality of each variant's y vs the first")
+    a = ap.parse_args()
+    import torch
+    import singlespmv_amd as sp
+    m = a.rows
+    n = a.ncols or m
+    spec = sp.gen_spec(a.kind, n, n, per_row=a.per_row, max_len=a.max_len, seed=42)
+    rp, col, val = sp.generate_csr(spec, 0, m)
+    x = torch.from_numpy(sp.generate_vector(n, seed=43)).cuda()
+    y = torch.empty(m, dtype=torch.float64, device="cuda")
+    plans = []
+    for part in filter(None, a.variants.split(";")):
+        name, _, envs = part.partition(":")
+        saved, opts = {}, {}
+        for kv in filter(None, envs.split(",")):
+            k, v = kv.split("=")
+            if k.islower():
+                opts[k] = int(v)
+                continue
+            saved[k] = os.environ.get(k)
+            os.environ[k] = v
+        p = sp.Plan.from_csr(m, n, rp, col, val, "bin", placement=a.placement, **opts)
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+        info = p.info()
+        plans.append((name, p, info))
+    yref = None
+    if a.check:
+        for name, p, _ in plans:
+            p.execute(x, y)
+            torch.cuda.synchronize()
+            if yref is None:
+                yref = y.clone()
+            print(json.dumps({"variant": name, "bit_equal_to_first": bool(torch.equal(y, yref))}), flush=True)
+    for r in range(a.rounds):
+        for name, p, info in plans:
+            ph = p.profile(x, y, a.iters)
+            tot = p.time(x, y, a.iters) / a.iters
+            print(json.dumps({"round": r, "variant": name, "ms": round(tot, 4),
+                              "long_rows": info.get("bin_long_rows"), "pieces": info.get("bin_long_pieces"),
+                              "products": info.get("bin_products"), "stored": info.get("stored_slots"),
+                              **{k: round(v, 4) for k, v in ph.items()},
+                              "placement_ms": [round(info.get("placement_best_ms", 0), 4),
+                                               round(info.get("placement_worst_ms", 0), 4)],
+                              "m": m, "n": n}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
