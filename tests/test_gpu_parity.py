@@ -262,8 +262,11 @@ def test_integer_exact_all_formats():
     rp, col, val = sp.generate_csr(spec)
     x = sp.generate_vector(m, seed=43, integer_values=True)
     yo = oracle_y(rp, col, val, x)
-    for fmt in ["csr", "ell", "ss", "hyb", "css", "coo", "jds"]:
-        y = run_plan(sp.Plan.from_csr(m, m, rp, col, val, fmt), x, m)
+    for fmt in ["csr", "ell", "ss", "hyb", "css", "coo", "jds", "bin"]:
+        plan = sp.Plan.from_csr(m, m, rp, col, val, fmt)
+        if fmt == "bin":  # small integers: the long rows' run partials are exact too
+            assert plan.info()["bin_long_rows"] > 0
+        y = run_plan(plan, x, m)
         assert np.array_equal(y, yo), fmt
 
 
