@@ -719,6 +719,8 @@ static int bin_finish(spmv_plan_s *p, int64_t n, const BinLayout &L, const spmv_
     SPMV_RETURN_IF(upload_vec(p, &B.run_off, L.run_off));
     SPMV_RETURN_IF(upload_vec(p, &B.srun_off, L.srun_off));
     SPMV_RETURN_IF(upload_vec(p, &B.bin_row0, L.row0));
+    // the run path is part of the launch the placement search times
+    B.long_len = L.LL;
     SPMV_RETURN_IF(bin_place_prod(p, n, prod_bytes, o));
     if (B.dbg & 16) {
         std::fprintf(stderr, "[bin] val1 %p cs1 %p dst1 %p slot2 %p prod %p (E %lld) placement ms:", (void *)B.val1,
@@ -728,7 +730,6 @@ static int bin_finish(spmv_plan_s *p, int64_t n, const BinLayout &L, const spmv_
     }
     p->stored_slots = L.E1;
     B.mul_entries = L.E1;
-    B.long_len = L.LL;
     B.long_pieces = L.NP;
     B.long_entries = 0;
     for (int64_t v : L.lpad) B.long_entries += v;

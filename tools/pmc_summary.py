@@ -72,11 +72,11 @@ def main(src, tag, config_key_prefix):
                 parts = kern.split("+")
                 tot, found = 0.0, 0
                 for part in parts:
-                    for k, s in summary.items():
-                        if part in k.split("(")[0]:
-                            tot += s[field]
-                            found += 1
-                            break
+                    # the instantiation the timed loop ran: most launches
+                    cands = [s for k, s in summary.items() if part in k.split("(")[0]]
+                    if cands:
+                        tot += max(cands, key=lambda s: s["launches"])[field]
+                        found += 1
                 if found == len(parts):
                     traffic[f"{config_key_prefix}:{kern}"] = (
                         tot if field == "traffic_raw" else
