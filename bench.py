@@ -408,11 +408,25 @@ def main():
     # and the measured ceiling of random 8-byte x gathers that hit L2: every
     # format here issues one x gather per nnz, so this bounds the gather side
     gather_gps = sp.gather_probe(local, 64 << 20, 1 << 20)
+    # ... and from a table of x's own size (beyond L2 once x > 4 MB): the
+    # ceiling of the row-parallel formats, whose gathers go wherever x is
+    gather_x_gps = sp.gather_probe(local, 64 << 20, min(max(8 * n_glob, 1 << 20), 2 << 30))
     gathers_gps = nnz_local / (r["event_ms_per_launch"] * 1e-3)
     gather_fields = {}
     if r["format"] not in ("dia", "bin"):  # DIA and BIN read x from LDS, not by gathers
         gather_fields = {"x_gathers_per_s": gathers_gps, "gather_ceiling_per_s": gather_gps,
                          "frac_of_gather_ceiling": gathers_gps / gather_gps}
+    # per format: x gathers/s against the ceiling of where its gathers land
+    # (CSS: an L2-resident slab; CSR/ELL/SS/COO/JDS/HYB: an x-sized table)
+    for fr in results.values():
+        if "event_ms_per_launch" not in fr or fr["format"] in ("dia", "bin"):
+            continue
+        g = nnz_local / (fr["event_ms_per_launch"] * 1e-3)
+        ceil = gather_gps if fr["format"] == "css" else gather_x_gps
+        fr["x_gathers_per_s"] = g
+        fr["gather_ceiling_per_s"] = ceil
+        fr["gather_ceiling_table"] = "1 MB (L2)" if fr["format"] == "css" else f"{8 * n_glob >> 20} MB (x)"
+        fr["frac_of_gather_ceiling"] = g / ceil
     # the reference's CSR5 byte model (CSR5_cuda/detail/utils.h:10-14), which
     # charges x per nnz -- for comparability with published CSR5 numbers only
     csr5_bytes = (rows + 1 + nnz_local) * 4 + (2 * nnz_local + rows) * 8

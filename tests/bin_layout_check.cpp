@@ -272,12 +272,16 @@ int main() {
                         if (emulate(B, A0, L, H0, x)) return fail("emulation (exact layout)", trial, si);
                         ++cases;
                     }
-                    if (kind != 1 || si == 0) continue;
-                    // ---- the same CSR with long rows on the run path
+                    if (kind == 0 || (kind == 2 && !emu) || si == 0) continue;
+                    // ---- the same CSR with long rows on the run path: the
+                    // auto threshold (long-row CSRs), or 6 entries (many short
+                    // long rows, pieces cut at block boundaries)
                     HostCsr A{m, n, nnz, rp.data(), col.data(), val.data()};
                     BinLayout K;
                     K.S = std::max<int64_t>(1, (n + C - 1) / C);
+                    o.bin_long_len = kind == 1 ? 0 : 6;
                     K.LL = bin_long_threshold(o, rp.data(), m, nnz, K.S);
+                    o.bin_long_len = 0;
                     if (K.LL == 0) continue;  // too few long entries for auto
                     bin_long_prep(A, C, K);
                     if (bin_rows(&p, rp.data(), m, n, K) != SPMV_SUCCESS) return fail("long bin_rows");

@@ -557,6 +557,36 @@ def test_bin_bit_exact(shape, kind, opts):
         assert np.array_equal(run_plan(plan, x, m), oracle_y(rp, col, val, x)), f"bin exact {shape} {opts}"
 
 
+@pytest.mark.parametrize("long_len,opts", [(6, {}), (64, {}), (1000, {}), (64, {"bin_strip_cols": 3001}),
+                                           (200, {"bin_sum_waves": 2, "bin_pad": 8}), (64, {"bin_sum_waves": 8})])
+def test_bin_long_rows_run_path(long_len, opts):
+    """The run path at explicit thresholds: rows with >=
+    long_len entries are reduced per strip run in the Mul (pieces cut at
+    64-entry blocks -- rows of 5000 entries over 2-17 strips give runs far
+    longer than a block), the rest stay bit-exact; two plans agree bit for
+    bit; plan info counts the long rows and at least one piece per run."""
+    m, n = 60_000, 50_000
+    rp, col, val = _bin_matrix("powerlaw", m, n, seed=long_len)
+    x = sp.generate_vector(n, seed=3)
+    plan = sp.Plan.from_csr(m, n, rp, col, val, "bin", bin_long_len=long_len, **opts)
+    info = plan.info()
+    lens = np.diff(rp)
+    assert info["bin_long_len"] == long_len
+    assert info["bin_long_rows"] == int(np.sum(lens >= long_len)) > 0
+    C = opts.get("bin_strip_cols", 20480)
+    runs = sum(len(np.unique(col[rp[r]:rp[r + 1]] // C)) for r in np.flatnonzero(lens >= long_len))
+    assert info["bin_long_pieces"] >= runs
+    y = run_plan(plan, x, m)
+    assert_bin_rows(plan, y, rp, col, val, x, what=f"long_len {long_len} {opts}")
+    again = sp.Plan.from_csr(m, n, rp, col, val, "bin", bin_long_len=long_len, **opts)
+    assert np.array_equal(run_plan(again, x, m), y)
+    # signed values: the partials still meet the 1e-12 bound of sum |a x|
+    sval = val * np.where(np.arange(len(val)) % 3 == 0, -1.0, 1.0)
+    xs = x - 0.5
+    ps = sp.Plan.from_csr(m, n, rp, col, sval, "bin", bin_long_len=long_len, **opts)
+    assert_bin_rows(ps, run_plan(ps, xs, m), rp, col, sval, xs, what=f"signed long_len {long_len}")
+
+
 @pytest.mark.parametrize("opts", [{"bin_pad": 8}, {"bin_pad": 16}, {"bin_pad": 32}, {"bin_sum_waves": 2},
                                   {"bin_sum_waves": 4}, {"bin_sum_waves": 8}, {"placement": "plain"},
                                   {"placement": "vmm"}, {"placement": "search"}])
