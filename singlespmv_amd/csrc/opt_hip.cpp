@@ -70,6 +70,10 @@ void OptimizeProblem(const SpMat &A, const Vec &x, SpMatOpt &A_opt, VecOpt &x_op
         else if (!strcasecmp(pl, "vmm")) o.placement = SPMV_PLACEMENT_VMM;
         else if (!strcasecmp(pl, "plain")) o.placement = SPMV_PLACEMENT_PLAIN;
     }
+    // SPMV_HIP_EXACT=1: every row the sequential opt_crs sum bit for bit --
+    // BIN keeps long power-law rows off its run path (spmv_hip.h bin_long_len)
+    if (const char *ex = std::getenv("SPMV_HIP_EXACT"))
+        if (std::atoi(ex) != 0) o.bin_long_len = -1;
     A_opt.nRow = A.nRow;
     A_opt.nCol = A.nCol;
     A_opt.nNnz = A.nNnz;

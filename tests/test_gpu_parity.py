@@ -354,6 +354,53 @@ def test_dropin_optimizeproblem_spmv(fmt, gpus, monkeypatch):
     L.SpMVRelease(C.byref(Ao))
 
 
+@pytest.mark.parametrize("exact", ["", "1"])
+def test_dropin_exact_switch(exact, monkeypatch):
+    """SPMV_HIP_EXACT=1 keeps the drop-in's BIN plan off the run path: a
+    power-law matrix's long rows are then the sequential opt_crs sum bit for
+    bit; without it they are within 1e-12."""
+    monkeypatch.setenv("SPMV_HIP_FORMAT", "bin")
+    if exact:
+        monkeypatch.setenv("SPMV_HIP_EXACT", exact)
+
+    class SpMatC(C.Structure):
+        _fields_ = [("nRow", C.c_int), ("nCol", C.c_int), ("nNnz", C.c_int),
+                    ("row_idx", C.c_void_p), ("col_idx", C.c_void_p), ("val", C.c_void_p)]
+
+    class VecC(C.Structure):
+        _fields_ = [("size", C.c_int), ("val", C.c_void_p)]
+
+    class SpMatOptC(C.Structure):
+        _fields_ = [("nRow", C.c_int), ("nCol", C.c_int), ("nNnz", C.c_int), ("plan", C.c_void_p),
+                    ("format", C.c_int), ("d_x", C.c_void_p), ("x_uploaded", C.c_int), ("dist", C.c_void_p),
+                    ("n_gpus", C.c_int)]
+
+    sp.lib()
+    L = C.CDLL(sp.OPT_LIB_PATH)
+    opt = getattr(L, "_Z15OptimizeProblemRK5SpMatRK3VecR8SpMatOptR6VecOpt")
+    m = 30_000
+    rp, col, val = sp.generate_csr(sp.gen_spec("powerlaw", m, max_len=3000, seed=29))
+    row = np.ascontiguousarray(np.repeat(np.arange(m, dtype=np.int32), np.diff(rp)))
+    col = np.ascontiguousarray(col)
+    x = sp.generate_vector(m, seed=31)
+    A = SpMatC(m, m, len(val), row.ctypes.data, col.ctypes.data, val.ctypes.data)
+    xv = VecC(m, x.ctypes.data)
+    y = np.full(m, 99.0)
+    yv = VecC(m, y.ctypes.data)
+    Ao, xo = SpMatOptC(), VecC()
+    opt(C.byref(A), C.byref(xv), C.byref(Ao), C.byref(xo))
+    L.SpMV(C.byref(Ao), C.byref(xo), C.byref(yv))
+    yo = oracle_y(rp, col, val, x)
+    long_rows = np.diff(rp) >= 128
+    assert long_rows.any()
+    if exact:
+        assert np.array_equal(y, yo)
+    else:
+        assert np.array_equal(y[~long_rows], yo[~long_rows])
+        check_close(y, yo, what="drop-in bin, run path")
+    L.SpMVRelease(C.byref(Ao))
+
+
 @pytest.mark.parametrize("fmt,name", [("ss", "SS"), ("css", "CSS"), ("jds", "JDS"), ("coo", "COO"), ("bin", "BIN")])
 def test_driver_binary_reports_block(fmt, name):
     import subprocess
