@@ -417,9 +417,15 @@ def main():
         gather_fields = {"x_gathers_per_s": gathers_gps, "gather_ceiling_per_s": gather_gps,
                          "frac_of_gather_ceiling": gathers_gps / gather_gps}
     # per format: x gathers/s against the ceiling of where its gathers land
-    # (CSS: an L2-resident slab; CSR/ELL/SS/COO/JDS/HYB: an x-sized table)
+    # (CSS: an L2-resident slab; CSR/ELL/SS/COO/JDS/HYB: an x-sized table of
+    # random gathers -- > 1 when the gathers are not random, as on a banded
+    # matrix, whose bound is then the stream)
     for fr in results.values():
-        if "event_ms_per_launch" not in fr or fr["format"] in ("dia", "bin"):
+        if "event_ms_per_launch" not in fr:
+            continue
+        # and its algorithmic bytes against the measured STREAM-read ceiling
+        fr["frac_of_stream"] = fr["achieved_gbs"] / stream_gbs
+        if fr["format"] in ("dia", "bin"):
             continue
         g = nnz_local / (fr["event_ms_per_launch"] * 1e-3)
         ceil = gather_gps if fr["format"] == "css" else gather_x_gps
