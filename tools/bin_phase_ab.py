@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--variants", required=True,
                     help="name:VAR=v,opt=v;name:... (UPPER-case keys: probe environment; lower-case: plan options)")
     ap.add_argument("--kind", default="uniform")
+    ap.add_argument("--fmt", default="bin")
     ap.add_argument("--rows", type=int, default=10_000_000)
     ap.add_argument("--ncols", type=int, default=0)
     ap.add_argument("--per-row", type=int, default=16)
@@ -51,7 +52,7 @@ def main():
                 continue
             saved[k] = os.environ.get(k)
             os.environ[k] = v
-        p = sp.Plan.from_csr(m, n, rp, col, val, "bin", placement=a.placement, **opts)
+        p = sp.Plan.from_csr(m, n, rp, col, val, a.fmt, placement=a.placement, **opts)
         for k, v in saved.items():
             if v is None:
                 os.environ.pop(k, None)
