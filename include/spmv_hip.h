@@ -106,11 +106,7 @@ typedef struct spmv_options {
                                 the sequential sum); 0 = auto (max(128, strips)
                                 when such rows hold >= 5 % of nnz), -1 = never
                                 (every row bit-exact)                         */
-    int32_t x_window;        /* CSR: stage the x a workgroup reads in an LDS window
-                                when its rows' columns span <= 2048 (banded /
-                                locality-ordered matrices): 0 = auto (on where
-                                any workgroup qualifies), -1 = never          */
-    int32_t reserved[2];
+    int32_t reserved[3];
 } spmv_options_t;
 
 /* Placement of the large scratch/value buffer of BIN and DIA plans (the BIN
@@ -267,9 +263,6 @@ typedef struct spmv_plan_info {
     int64_t bin_long_pieces;
     int64_t bin_products;     /* BIN: products + partials the Sum reads         */
     int64_t bin_long_entries; /* BIN: Mul entries in long blocks (with padding) */
-    int64_t x_window_wgs;     /* CSR: workgroups reading x from an LDS window   */
-    int32_t x_window_max;     /* CSR: the widest such window (doubles)          */
-    int32_t x_window_reserved;
 } spmv_plan_info_t;
 
 int spmv_plan_info(spmv_plan_t plan, spmv_plan_info_t *info);

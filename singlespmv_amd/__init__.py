@@ -57,8 +57,7 @@ class Options(C.Structure):
                 ("dia_max_fill", C.c_double), ("css_slab_shift", C.c_int32), ("css_lag", C.c_int32),
                 ("css_pace", C.c_int32), ("bin_strip_cols", C.c_int32), ("bin_groups", C.c_int32),
                 ("bin_sum_waves", C.c_int32), ("bin_pad", C.c_int32), ("csr_row_ptr64", C.c_int32),
-                ("placement", C.c_int32), ("bin_long_len", C.c_int32), ("x_window", C.c_int32),
-                ("reserved", C.c_int32 * 2)]
+                ("placement", C.c_int32), ("bin_long_len", C.c_int32), ("reserved", C.c_int32 * 3)]
 
 
 PLACEMENTS = {"auto": 0, "plain": 1, "search": 2, "vmm": 3}
@@ -77,8 +76,7 @@ class PlanInfo(C.Structure):
                 ("placement_best_ms", C.c_float), ("placement_worst_ms", C.c_float),
                 ("bin_long_len", C.c_int32), ("bin_reserved", C.c_int32), ("bin_long_rows", C.c_int64),
                 ("bin_long_pieces", C.c_int64), ("bin_products", C.c_int64),
-                ("bin_long_entries", C.c_int64), ("x_window_wgs", C.c_int64), ("x_window_max", C.c_int32),
-                ("x_window_reserved", C.c_int32)]
+                ("bin_long_entries", C.c_int64)]
 
     def as_dict(self):
         d = {k: getattr(self, k) for k, _ in self._fields_}
@@ -343,7 +341,7 @@ def make_options(fmt="auto", device: int = -1, csr_lanes: int = 0, ell_width: in
                  css_slab_shift: int = 0, css_lag: int = 0, css_pace: int = 0,
                  bin_strip_cols: int = 0, bin_groups: int = 0, bin_sum_waves: int = 0,
                  bin_pad: int = 0, csr_row_ptr64: bool = False, placement="auto",
-                 bin_long_len: int = 0, x_window: int = 0) -> Options:
+                 bin_long_len: int = 0) -> Options:
     o = Options()
     lib().spmv_options_default(C.byref(o))
     o.format = FORMATS[fmt] if isinstance(fmt, str) else int(fmt)
@@ -354,7 +352,6 @@ def make_options(fmt="auto", device: int = -1, csr_lanes: int = 0, ell_width: in
     o.bin_sum_waves, o.bin_pad, o.csr_row_ptr64 = bin_sum_waves, bin_pad, 1 if csr_row_ptr64 else 0
     o.placement = PLACEMENTS[placement] if isinstance(placement, str) else int(placement)
     o.bin_long_len = bin_long_len
-    o.x_window = x_window
     return o
 
 

@@ -494,9 +494,6 @@ int spmv_plan_info(spmv_plan_t p, spmv_plan_info_t *info) {
     info->empty_rows = p->empty_rows;
     info->css_split_rows = p->css.split_rows;
     std::strncpy(info->kernel, p->kernel_name.c_str(), sizeof(info->kernel) - 1);
-    const XWindow &xw = p->format == SPMV_FORMAT_CSR ? p->csr.xw : p->ell.xw;
-    info->x_window_wgs = xw.wgs;
-    info->x_window_max = xw.max;
     if (p->format == SPMV_FORMAT_BIN) {
         info->bin_bins = p->bin.n_bins;
         info->bin_strips = p->bin.n_strips;

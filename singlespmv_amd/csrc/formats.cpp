@@ -295,13 +295,13 @@ int build_csr(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
     SPMV_RETURN_IF(upload(p, &c.val, A.val, A.nnz, kPad));
     SPMV_RETURN_IF(csr_plan_lanes(p, A.row_ptr, A.m, o));
     csr_finish_info(p);
-    return csr_plan_window(p, o);
+    return SPMV_SUCCESS;
 }
 
 // ---------------------------------------------------------------- ELL
 // cap: maximum slots per row kept in the ELL part (HYB); INT32_MAX for ELL.
 // order (JDS): slice row i is matrix row order[i]; nullptr = identity.
-int build_ell(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o, int cap, const int32_t *order) {
+int build_ell(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &, int cap, const int32_t *order) {
     EllDev &e = p->ell;
     if (const char *u = probe_env("SPMV_ELL_UNROLL")) e.unroll = std::atoi(u);
     auto src = [&](int64_t r) -> int64_t { return order ? (int64_t)order[r] : r; };
@@ -355,7 +355,7 @@ int build_ell(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o, int cap
     p->algo_bytes = 12 * A.nnz + 8 * A.n + 8 * A.m;
     p->n_kernels = 1;
     p->kernel_name = "ell_slice_kernel";
-    return ell_plan_window(p, o);
+    return SPMV_SUCCESS;
 }
 
 // ---------------------------------------------------------------- JDS
@@ -484,7 +484,7 @@ int build_hyb(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
     p->algo_bytes = 12 * A.nnz + 8 * A.n + 8 * A.m + 12 * h.n_rows;
     p->n_kernels = h.n_rows ? 2 : 1;
     p->kernel_name = "ell_slice_kernel";
-    return ell_plan_window(p, o);
+    return SPMV_SUCCESS;
 }
 
 // ---------------------------------------------------------------- SS

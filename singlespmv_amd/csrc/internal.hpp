@@ -87,16 +87,6 @@ constexpr int kPad = 8;
 // Adaptive CSR (csr_lanes = AUTO on skewed rows): rows binned by length,
 // bin b summed by kCsrBinLanes[b] lanes per row (256 = one workgroup per row).
 constexpr int kCsrBins = 8;
-// LDS x window of a workgroup (CSR in row order, ELL): the plan records per
-// workgroup the first column and the span of the columns its entries read;
-// span -1 when wider than kCsrMaxWin (that workgroup gathers from global
-// memory).  Kept only when some workgroup qualifies (win != null).
-constexpr int kCsrMaxWin = 2048;  // doubles (16 KB of LDS)
-struct XWindow {
-    int32_t *win = nullptr;  // [2 * workgroups]: (lo, span)
-    int64_t wgs = 0;         // workgroups with a window
-    int max = 0;             // widest window = LDS doubles per workgroup
-};
 constexpr int kCsrBinLanes[kCsrBins] = {1, 2, 4, 8, 16, 32, 64, 256};
 struct CsrDev {
     void *row_ptr = nullptr;  // int32 or int64 [m+1]
@@ -106,7 +96,6 @@ struct CsrDev {
     int lanes = 4;            // lanes per row (1..64); 0 = adaptive (bins)
     int32_t *bin_rows = nullptr;        // rows of every bin, ascending within a bin
     int64_t bin_off[kCsrBins + 1] = {};  // host: bin b = bin_rows[bin_off[b], bin_off[b+1])
-    XWindow xw;                         // LDS x windows (rows in order, lanes > 0)
 };
 
 // Sliced ELL (opt_ell, src/opt_ell.cpp): slices of 64 consecutive rows (one
@@ -125,7 +114,6 @@ struct EllDev {
     int max_width = 0;
     int unroll = 2;  // quads per lane per iteration (SPMV_ELL_UNROLL, internal;
                      // 2 beat 4 by 28 % at config 4, 5 % at config 2)
-    XWindow xw;      // LDS x windows per workgroup of 4 slices
 };
 
 // HYB overflow: rows whose length exceeds K keep entries K.. in a CSR over
@@ -378,11 +366,6 @@ int build_ss_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, c
 int choose_format(const HostCsr &A, const spmv_options_t &o);
 int auto_csr_lanes(double mean_row);
 int csr_plan_lanes(spmv_plan_s *p, const int64_t *row_ptr, int64_t m, const spmv_options_t &o);
-int csr_plan_window(spmv_plan_s *p, const spmv_options_t &o);  // k_csr.hip, after the device upload
-int ell_plan_window(spmv_plan_s *p, const spmv_options_t &o);  // k_ell.hip
-// k_csr.hip: windows of workgroups covering bounds[w*stride .. (w+1)*stride]
-int plan_x_window(spmv_plan_s *p, int64_t nb, int stride, const void *bounds, bool bounds64, const int32_t *col,
-                  XWindow *out);
 void csr_finish_info(spmv_plan_s *p);
 int auto_ss_sigma(double mean_row);
 

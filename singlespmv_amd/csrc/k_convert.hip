@@ -242,7 +242,7 @@ int build_csr_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, 
     SPMV_HIP_TRY(hipMemcpy(hrp.data(), d_rp, 8 * (size_t)(p->m + 1), hipMemcpyDeviceToHost));
     SPMV_RETURN_IF(csr_plan_lanes(p, hrp.data(), p->m, o));
     csr_finish_info(p);
-    return csr_plan_window(p, o);
+    return SPMV_SUCCESS;
 }
 
 int build_ss_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, const double *d_val,

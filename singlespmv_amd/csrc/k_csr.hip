@@ -16,10 +16,6 @@
 #include "device.hpp"
 #include "internal.hpp"
 
-#include <algorithm>
-#include <climits>
-#include <vector>
-
 namespace spmv {
 
 // LIST: the rows come from a length bin (rows[]), not 0..m-1 (adaptive CSR)
@@ -54,194 +50,6 @@ __global__ __launch_bounds__(256) void csr_vec4_kernel(int64_t m, const int32_t 
     }
     acc = group_sum<L>(acc);
     if (lane == 0) y[row] = acc;
-}
-
-// csr_win<L, RP>: csr_vec4 with x staged through LDS (north star: "x[]
-// staged through LDS").  Workgroup w owns rows [w*256/L, (w+1)*256/L) and the
-// plan knows the column window [win[2w], win[2w] + win[2w+1]) they read
-// (csr_plan_window).  The lane's first chunk of col/val is loaded first, the
-// window is copied into LDS with coalesced loads while those are in flight,
-// and after one barrier every gather is a ds_read_b64 instead of an L1/L2
-// request.  A span of -1 (columns too spread) keeps the global gathers.  Each
-// lane sums the same entries in the same order and the group reduces with the
-// same butterfly as csr_vec4_kernel<L>: y is bit-identical to it.
-template <int L, typename RP>
-__global__ __launch_bounds__(256) void csr_win_kernel(int64_t m, const int32_t *__restrict__ win,
-                                                      const RP *__restrict__ rp, const int32_t *__restrict__ col,
-                                                      const double *__restrict__ val, const double *__restrict__ x,
-                                                      double *__restrict__ y) {
-    extern __shared__ double xs[];
-    const int64_t g = ((int64_t)blockIdx.x * 256 + threadIdx.x) / L;
-    const int lane = threadIdx.x & (L - 1);
-    const int32_t lo = win[2 * blockIdx.x], span = win[2 * blockIdx.x + 1];
-    const bool live = g < m;  // whole groups (L | 256); the barrier needs every thread
-    int64_t s = 0, e = 0;
-    if (live) {
-        s = rp[g];
-        e = rp[g + 1];
-    }
-    double acc = 0.0;
-    if (span < 0) {  // workgroup-uniform: global gathers
-        for (int64_t j = (s & ~(int64_t)3) + 4 * lane; j < e; j += 4 * L) {
-            const i32x4 c = ld_stream4(col + j);
-            const f64x2 v01 = ld_stream2(val + j);
-            const f64x2 v23 = ld_stream2(val + j + 2);
-            const double x0 = (j + 0 >= s && j + 0 < e) ? ld_x(x, c.x) : 0.0;
-            const double x1 = (j + 1 >= s && j + 1 < e) ? ld_x(x, c.y) : 0.0;
-            const double x2 = (j + 2 >= s && j + 2 < e) ? ld_x(x, c.z) : 0.0;
-            const double x3 = (j + 3 >= s && j + 3 < e) ? ld_x(x, c.w) : 0.0;
-            if (j + 0 >= s && j + 0 < e) acc = madd(v01.x, x0, acc);
-            if (j + 1 >= s && j + 1 < e) acc = madd(v01.y, x1, acc);
-            if (j + 2 >= s && j + 2 < e) acc = madd(v23.x, x2, acc);
-            if (j + 3 >= s && j + 3 < e) acc = madd(v23.y, x3, acc);
-        }
-    } else {
-        int64_t j = (s & ~(int64_t)3) + 4 * lane;
-        i32x4 c = {0, 0, 0, 0};
-        f64x2 v01 = {0.0, 0.0}, v23 = {0.0, 0.0};
-        if (j < e) {
-            c = ld_stream4(col + j);
-            v01 = ld_stream2(val + j);
-            v23 = ld_stream2(val + j + 2);
-        }
-        for (int i = threadIdx.x; i < span; i += 256) xs[i] = x[(int64_t)lo + i];
-        __syncthreads();
-        while (j < e) {
-            // entries outside [s, e) (the aligned start, the padding) are
-            // never read from the window: their columns may lie outside it
-            const double x0 = (j + 0 >= s && j + 0 < e) ? xs[c.x - lo] : 0.0;
-            const double x1 = (j + 1 >= s && j + 1 < e) ? xs[c.y - lo] : 0.0;
-            const double x2 = (j + 2 >= s && j + 2 < e) ? xs[c.z - lo] : 0.0;
-            const double x3 = (j + 3 >= s && j + 3 < e) ? xs[c.w - lo] : 0.0;
-            if (j + 0 >= s && j + 0 < e) acc = madd(v01.x, x0, acc);
-            if (j + 1 >= s && j + 1 < e) acc = madd(v01.y, x1, acc);
-            if (j + 2 >= s && j + 2 < e) acc = madd(v23.x, x2, acc);
-            if (j + 3 >= s && j + 3 < e) acc = madd(v23.y, x3, acc);
-            j += 4 * L;
-            if (j < e) {
-                c = ld_stream4(col + j);
-                v01 = ld_stream2(val + j);
-                v23 = ld_stream2(val + j + 2);
-            }
-        }
-    }
-    acc = group_sum<L>(acc);
-    if (live && lane == 0) y[g] = acc;
-}
-
-// Plan-time LDS x windows (csr_win_kernel, ell_slice_kernel<..., WIN>):
-// workgroup w covers the entries [bounds[w*stride], bounds[min((w+1)*stride,
-// nb)]) of `col` (CSR: row pointers, `stride` rows per workgroup; ELL: slice
-// offsets, 4 slices per workgroup); its window is the smallest and largest
-// column there, span = hi - lo + 1, or -1 beyond kCsrMaxWin.  One 256-thread
-// block per workgroup.
-template <typename B>
-__global__ __launch_bounds__(256) void window_scan(int64_t nb, int stride, const B *__restrict__ bounds,
-                                                   const int32_t *__restrict__ col, int32_t *__restrict__ win) {
-    __shared__ int32_t red[2][4];
-    const int64_t r0 = (int64_t)blockIdx.x * stride;
-    const int64_t r1 = r0 + stride < nb ? r0 + stride : nb;
-    const int64_t b = bounds[r0], e = bounds[r1];
-    int32_t lo = INT32_MAX, hi = -1;
-    for (int64_t j = b + threadIdx.x; j < e; j += 256) {
-        const int32_t c = col[j];
-        lo = c < lo ? c : lo;
-        hi = c > hi ? c : hi;
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const int32_t l2 = __shfl_xor(lo, o, 64), h2 = __shfl_xor(hi, o, 64);
-        lo = l2 < lo ? l2 : lo;
-        hi = h2 > hi ? h2 : hi;
-    }
-    if ((threadIdx.x & 63) == 0) {
-        red[0][threadIdx.x >> 6] = lo;
-        red[1][threadIdx.x >> 6] = hi;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        for (int w = 1; w < 4; ++w) {
-            lo = red[0][w] < lo ? red[0][w] : lo;
-            hi = red[1][w] > hi ? red[1][w] : hi;
-        }
-        if (hi < 0) {  // no entries
-            win[2 * blockIdx.x] = 0;
-            win[2 * blockIdx.x + 1] = 0;
-        } else {
-            const int64_t span = (int64_t)hi - lo + 1;
-            win[2 * blockIdx.x] = lo;
-            win[2 * blockIdx.x + 1] = span <= kCsrMaxWin ? (int32_t)span : -1;
-        }
-    }
-}
-
-int plan_x_window(spmv_plan_s *p, int64_t nb, int stride, const void *bounds, bool bounds64, const int32_t *col,
-                  XWindow *out) {
-    *out = XWindow{};
-    if (nb <= 0) return SPMV_SUCCESS;
-    const int64_t nwg = (nb + stride - 1) / stride;
-    void *q = nullptr;
-    SPMV_RETURN_IF(p->arena.alloc(&q, sizeof(int32_t) * 2 * (size_t)nwg));
-    int32_t *dwin = (int32_t *)q;
-    if (bounds64)
-        hipLaunchKernelGGL(window_scan<int64_t>, dim3((unsigned)nwg), dim3(256), 0, p->stream, nb, stride,
-                           (const int64_t *)bounds, col, dwin);
-    else
-        hipLaunchKernelGGL(window_scan<int32_t>, dim3((unsigned)nwg), dim3(256), 0, p->stream, nb, stride,
-                           (const int32_t *)bounds, col, dwin);
-    SPMV_HIP_TRY(hipGetLastError());
-    std::vector<int32_t> h(2 * (size_t)nwg);
-    SPMV_HIP_TRY(hipMemcpyAsync(h.data(), dwin, sizeof(int32_t) * h.size(), hipMemcpyDeviceToHost, p->stream));
-    SPMV_HIP_TRY(hipStreamSynchronize(p->stream));
-    int64_t wgs = 0;
-    int mx = 0;
-    for (int64_t w = 0; w < nwg; ++w)
-        if (h[2 * w + 1] >= 0) {
-            ++wgs;
-            mx = std::max(mx, h[2 * w + 1]);
-        }
-    if (wgs == 0) {
-        p->arena.free(dwin);
-        return SPMV_SUCCESS;
-    }
-    out->win = dwin;
-    out->wgs = wgs;
-    out->max = std::max(mx, 1);
-    return SPMV_SUCCESS;
-}
-
-// After the CSR is on the device (either build path): per-workgroup windows
-// for the in-order kernel (lanes > 0); x_window = -1 turns them off.
-int csr_plan_window(spmv_plan_s *p, const spmv_options_t &o) {
-    CsrDev &c = p->csr;
-    if (o.x_window < 0 || c.lanes <= 0 || p->m == 0) return SPMV_SUCCESS;
-    SPMV_RETURN_IF(plan_x_window(p, p->m, 256 / c.lanes, c.row_ptr, c.rp64, c.col, &c.xw));
-    if (c.xw.win) p->kernel_name = "csr_win_kernel<" + std::to_string(c.lanes) + ">";
-    return SPMV_SUCCESS;
-}
-
-template <int L, typename RP>
-static int launch_csr_win_t(const spmv_plan_s *p, const double *x, double *y) {
-    const int64_t blocks = (p->m * L + 255) / 256;
-    hipLaunchKernelGGL((csr_win_kernel<L, RP>), dim3((unsigned)blocks), dim3(256),
-                       sizeof(double) * (size_t)p->csr.xw.max, p->stream, p->m, p->csr.xw.win,
-                       (const RP *)p->csr.row_ptr, p->csr.col, p->csr.val, x, y);
-    SPMV_HIP_TRY(hipGetLastError());
-    return SPMV_SUCCESS;
-}
-
-template <typename RP>
-static int launch_csr_win(const spmv_plan_s *p, const double *x, double *y) {
-    switch (p->csr.lanes) {
-        case 1: return launch_csr_win_t<1, RP>(p, x, y);
-        case 2: return launch_csr_win_t<2, RP>(p, x, y);
-        case 4: return launch_csr_win_t<4, RP>(p, x, y);
-        case 8: return launch_csr_win_t<8, RP>(p, x, y);
-        case 16: return launch_csr_win_t<16, RP>(p, x, y);
-        case 32: return launch_csr_win_t<32, RP>(p, x, y);
-        case 64: return launch_csr_win_t<64, RP>(p, x, y);
-        default: set_error("csr lanes must be a power of two in [1,64]"); return SPMV_ERROR_INVALID_VALUE;
-    }
 }
 
 // One 256-thread workgroup per row (the longest-row bin of adaptive CSR):
@@ -437,7 +245,6 @@ static int launch_csr_lanes(const spmv_plan_s *p, int lanes, int64_t nrows, cons
 template <typename RP>
 static int launch_csr_rp(const spmv_plan_s *p, const double *x, double *y) {
     const CsrDev &c = p->csr;
-    if (c.xw.win) return launch_csr_win<RP>(p, x, y);
     if (!c.bin_rows) return launch_csr_lanes<RP>(p, c.lanes, p->m, nullptr, x, y);
     // adaptive: every bin in one launch (workgroup ranges per bin)
     return launch_adaptive<RP, false>(p, c.bin_off, c.bin_rows, (const RP *)c.row_ptr, c.col, c.val, x, y, nullptr);

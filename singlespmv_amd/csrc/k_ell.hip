@@ -17,13 +17,21 @@
 
 namespace spmv {
 
-// One slice's row sum for this lane: quads of 4 slots, UNROLL quads in
-// flight; LDSX: x read from the workgroup's LDS window (xs[c - lo]).
-template <int UNROLL, bool LDSX>
-__device__ __forceinline__ double ell_lane_sum(int64_t quads, const int32_t *__restrict__ cp,
-                                               const double *__restrict__ vp, const double *__restrict__ x,
-                                               const double *xs, int32_t lo) {
-    auto gx = [&](int32_t c) { return LDSX ? xs[c - lo] : ld_x(x, c); };
+template <int UNROLL, bool ADD, bool PERM>
+__global__ __launch_bounds__(256) void ell_slice_kernel(int64_t m, int64_t n_slices,
+                                                        const int32_t *__restrict__ perm,
+                                                        const int64_t *__restrict__ slice_off,
+                                                        const int32_t *__restrict__ col,
+                                                        const double *__restrict__ val,
+                                                        const double *__restrict__ x,
+                                                        double *__restrict__ y) {
+    const int64_t slice = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (slice >= n_slices) return;
+    const int64_t base = slice_off[slice];
+    const int64_t quads = (slice_off[slice + 1] - base) >> 8;  // (width/4)
+    const int32_t *cp = col + base + lane * 4;
+    const double *vp = val + base + lane * 4;
     double acc = 0.0;
     int64_t q = 0;
     for (; q + UNROLL <= quads; q += UNROLL) {
@@ -38,10 +46,10 @@ __device__ __forceinline__ double ell_lane_sum(int64_t quads, const int32_t *__r
         double g[UNROLL][4];
 #pragma unroll
         for (int u = 0; u < UNROLL; ++u) {
-            g[u][0] = gx(c[u].x);
-            g[u][1] = gx(c[u].y);
-            g[u][2] = gx(c[u].z);
-            g[u][3] = gx(c[u].w);
+            g[u][0] = ld_x(x, c[u].x);
+            g[u][1] = ld_x(x, c[u].y);
+            g[u][2] = ld_x(x, c[u].z);
+            g[u][3] = ld_x(x, c[u].w);
         }
 #pragma unroll
         for (int u = 0; u < UNROLL; ++u) {
@@ -55,49 +63,11 @@ __device__ __forceinline__ double ell_lane_sum(int64_t quads, const int32_t *__r
         const i32x4 c = ld_stream4(cp + q * 256);
         const f64x2 a = ld_stream2(vp + q * 256);
         const f64x2 b = ld_stream2(vp + q * 256 + 2);
-        const double g0 = gx(c.x), g1 = gx(c.y), g2 = gx(c.z), g3 = gx(c.w);
+        const double g0 = ld_x(x, c.x), g1 = ld_x(x, c.y), g2 = ld_x(x, c.z), g3 = ld_x(x, c.w);
         acc = madd(a.x, g0, acc);
         acc = madd(a.y, g1, acc);
         acc = madd(b.x, g2, acc);
         acc = madd(b.y, g3, acc);
-    }
-    return acc;
-}
-
-// WIN: the workgroup's 4 slices read x only inside [win[2b], win[2b] +
-// win[2b+1]) (plan-time, k_csr.hip window_scan); that window is copied to LDS
-// once and every gather is a ds_read_b64.  Span -1: global gathers.  The
-// arithmetic is the same either way (bit-identical y).
-template <int UNROLL, bool ADD, bool PERM, bool WIN>
-__global__ __launch_bounds__(256) void ell_slice_kernel(int64_t m, int64_t n_slices,
-                                                        const int32_t *__restrict__ perm,
-                                                        const int64_t *__restrict__ slice_off,
-                                                        const int32_t *__restrict__ col,
-                                                        const double *__restrict__ val,
-                                                        const double *__restrict__ x,
-                                                        double *__restrict__ y,
-                                                        const int32_t *__restrict__ win) {
-    extern __shared__ double xs[];
-    const int64_t slice = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    const bool live = slice < n_slices;
-    int64_t base = 0, quads = 0;
-    if (live) {
-        base = slice_off[slice];
-        quads = (slice_off[slice + 1] - base) >> 8;  // (width/4)
-    }
-    const int32_t *cp = col + base + lane * 4;
-    const double *vp = val + base + lane * 4;
-    double acc;
-    if (WIN && win[2 * blockIdx.x + 1] >= 0) {  // workgroup-uniform
-        const int32_t lo = win[2 * blockIdx.x], span = win[2 * blockIdx.x + 1];
-        for (int i = threadIdx.x; i < span; i += blockDim.x) xs[i] = x[(int64_t)lo + i];
-        __syncthreads();
-        if (!live) return;
-        acc = ell_lane_sum<UNROLL, true>(quads, cp, vp, x, xs, lo);
-    } else {
-        if (!live) return;
-        acc = ell_lane_sum<UNROLL, false>(quads, cp, vp, x, xs, 0);
     }
     const int64_t srow = slice * 64 + lane;
     if (srow < m) {
@@ -107,31 +77,16 @@ __global__ __launch_bounds__(256) void ell_slice_kernel(int64_t m, int64_t n_sli
     }
 }
 
-template <int U, bool WIN>
-static void launch_ell_uw(const spmv_plan_s *p, const double *x, double *y) {
-    const EllDev &e = p->ell;
-    const int64_t blocks = (e.n_slices + 3) / 4;
-    const size_t lds = WIN ? sizeof(double) * (size_t)e.xw.max : 0;
-    if (e.perm)
-        hipLaunchKernelGGL((ell_slice_kernel<U, false, true, WIN>), dim3((unsigned)blocks), dim3(256), lds,
-                           p->stream, p->m, e.n_slices, e.perm, e.slice_off, e.col, e.val, x, y, e.xw.win);
-    else
-        hipLaunchKernelGGL((ell_slice_kernel<U, false, false, WIN>), dim3((unsigned)blocks), dim3(256), lds,
-                           p->stream, p->m, e.n_slices, e.perm, e.slice_off, e.col, e.val, x, y, e.xw.win);
-}
-
 template <int U>
 static void launch_ell_u(const spmv_plan_s *p, const double *x, double *y) {
-    if (p->ell.xw.win) launch_ell_uw<U, true>(p, x, y);
-    else launch_ell_uw<U, false>(p, x, y);
-}
-
-// LDS x windows per workgroup (4 slices = 256 rows; their slots are one
-// contiguous range of col); x_window = -1 turns them off.
-int ell_plan_window(spmv_plan_s *p, const spmv_options_t &o) {
-    EllDev &e = p->ell;
-    if (o.x_window < 0 || e.n_slices == 0) return SPMV_SUCCESS;
-    return plan_x_window(p, e.n_slices, 4, e.slice_off, true, e.col, &e.xw);
+    const EllDev &e = p->ell;
+    const int64_t blocks = (e.n_slices + 3) / 4;
+    if (e.perm)
+        hipLaunchKernelGGL((ell_slice_kernel<U, false, true>), dim3((unsigned)blocks), dim3(256), 0, p->stream,
+                           p->m, e.n_slices, e.perm, e.slice_off, e.col, e.val, x, y);
+    else
+        hipLaunchKernelGGL((ell_slice_kernel<U, false, false>), dim3((unsigned)blocks), dim3(256), 0,
+                           p->stream, p->m, e.n_slices, e.perm, e.slice_off, e.col, e.val, x, y);
 }
 
 int launch_ell(const spmv_plan_s *p, const double *x, double *y) {

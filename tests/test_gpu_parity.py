@@ -121,97 +121,6 @@ def test_csr_lanes(lanes):
         assert np.array_equal(y, yo)
 
 
-def _banded_with_far_entries(m, every, seed):
-    """A banded CSR (diagonals -32..31) where every `every`-th row also has one
-    entry half the matrix away: the workgroups holding such a row read x
-    beyond an LDS window (0 = none)."""
-    rp, col, val = sp.generate_csr(sp.gen_spec("banded", m, band_lo=-32, band_hi=31, seed=seed))
-    if not every:
-        return rp, col, val
-    rows, cols, vals = [], [], []
-    lens = np.diff(rp)
-    r = np.repeat(np.arange(m), lens)
-    far = np.arange(0, m, every)
-    r = np.concatenate([r, far])
-    c = np.concatenate([col, (far + m // 2) % m]).astype(np.int32)
-    v = np.concatenate([val, np.linspace(0.5, 1.5, len(far))])
-    o = np.lexsort((c, r))
-    return sp.coo_to_csr(m, r[o]), np.ascontiguousarray(c[o]), np.ascontiguousarray(v[o])
-
-
-@pytest.mark.parametrize("lanes", [0, 1, 4, 16, 64])
-@pytest.mark.parametrize("every,rp64", [(0, False), (997, False), (0, True), (5, False)])
-def test_csr_x_window(lanes, every, rp64):
-    """CSR with x staged through an LDS window per workgroup (csr_win_kernel):
-    bit-identical to the global-gather kernel with the same lanes, on windowed,
-    mixed and (every 5th row far) no-window matrices; 1 lane bit-exact vs the
-    oracle's opt_crs sum."""
-    import torch
-    m = 50_021
-    rp, col, val = _banded_with_far_entries(m, every, seed=21)
-    x = sp.generate_vector(m, seed=4)
-    yo = oracle_y(rp, col, val, x)
-    kw = {"csr_lanes": lanes, "csr_row_ptr64": rp64}
-    pw = sp.Plan.from_csr(m, m, rp, col, val, "csr", **kw)
-    pg = sp.Plan.from_csr(m, m, rp, col, val, "csr", x_window=-1, **kw)
-    iw, ig = pw.info(), pg.info()
-    L = iw["csr_lanes"]
-    assert ig["x_window_wgs"] == 0
-    if L == 0:  # adaptive CSR (rows in length bins, not in order): no window
-        assert iw["x_window_wgs"] == 0 and iw["kernel"] == "csr_adaptive_kernel"
-    else:
-        assert ig["kernel"].startswith("csr_vec4_kernel")
-    nwg = -(-m // (256 // max(L, 1)))
-    if L == 0:
-        pass
-    elif every == 0:
-        assert iw["x_window_wgs"] == nwg and iw["kernel"].startswith("csr_win_kernel")
-        assert iw["x_window_max"] <= 256 // L + 63
-    elif 256 // L < every:  # some workgroups hold no far row
-        assert 0 < iw["x_window_wgs"] < nwg
-    else:
-        assert iw["x_window_wgs"] == 0 and iw["kernel"].startswith("csr_vec4_kernel")
-    yw = run_plan(pw, x, m)
-    yg = run_plan(pg, x, m)
-    assert np.array_equal(yw, yg), "LDS window changed the sums"
-    check_close(yw, yo, what=f"csr window lanes={L}")
-    if L == 1:
-        assert np.array_equal(yw, yo)
-    # the device build path plans the same windows
-    pd = sp.Plan.from_device_csr(m, m, torch.from_numpy(rp).cuda(), torch.from_numpy(col).cuda(),
-                                 torch.from_numpy(val).cuda(), "csr", **kw)
-    assert pd.info()["x_window_wgs"] == iw["x_window_wgs"]
-    assert np.array_equal(run_plan(pd, x, m), yw)
-
-
-@pytest.mark.parametrize("fmt", ["ell", "hyb", "jds"])
-@pytest.mark.parametrize("every", [0, 997, 5])
-def test_ell_x_window(fmt, every):
-    """ELL (and the ELL part of HYB / JDS) with x staged through an LDS window
-    per 256-row workgroup: bit-identical to the global-gather kernel, and
-    ELL bit-exact vs the oracle's sequential opt_crs sum."""
-    m = 50_021
-    rp, col, val = _banded_with_far_entries(m, every, seed=22)
-    x = sp.generate_vector(m, seed=6)
-    pw = sp.Plan.from_csr(m, m, rp, col, val, fmt)
-    pg = sp.Plan.from_csr(m, m, rp, col, val, fmt, x_window=-1)
-    nwg = -(-m // 256)
-    wgs = pw.info()["x_window_wgs"]
-    assert pg.info()["x_window_wgs"] == 0
-    if every == 0:
-        assert wgs >= nwg - 1  # JDS: the clipped edge rows sort to the end
-    elif fmt == "ell" and every == 997:
-        assert 0 < wgs < nwg
-    elif fmt == "ell":
-        assert wgs == 0
-    yw = run_plan(pw, x, m)
-    assert np.array_equal(yw, run_plan(pg, x, m)), "LDS window changed the sums"
-    if fmt == "ell":
-        assert np.array_equal(yw, oracle_y(rp, col, val, x))
-    else:
-        check_close(yw, oracle_y(rp, col, val, x), what=f"{fmt} window")
-
-
 @pytest.mark.parametrize("sigma", [4, 8, 12, 16, 20, 24, 32])
 @pytest.mark.parametrize("kind", ["powerlaw", "uniform", "empty_rows"])
 def test_ss_sigma(sigma, kind):
