@@ -22,7 +22,11 @@ ranks (one per GPU) as a child process before anything touches the GPU, and
 exits with the child's return code.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--trials T]
-                  [--config c2|c3|c4] [--formats auto,csr,ell,ss,css] [--no-cpu]
+                  [--config c2|c3|c4] [--formats auto,auto@plain,csr,ell,ss,css] [--no-cpu]
+
+The headline plan asks for the build-time placement search (--placement
+search: the bench owns the GPU); `formats["auto@plain"]` is the same plan with
+the library's default single allocation, reported beside it.
 
 Prints ONE JSON line on rank 0.
 """
@@ -98,8 +102,10 @@ def parse():
                     help="timed trials of K steps; value = the fastest (src/main.cpp:58-102)")
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--rows", type=int, default=0, help="rows per GPU (default: the config's)")
-    ap.add_argument("--formats", default="auto,csr,ell,ss,css",
-                    help="first entry is the headline plan; the rest are reported alongside")
+    ap.add_argument("--formats", default="auto,auto@plain,csr,ell,ss,css",
+                    help="first entry is the headline plan; the rest are reported alongside; "
+                         "fmt@placement overrides --placement for that plan (auto@plain: the "
+                         "library's default placement, reported beside the searched one)")
     ap.add_argument("--placement", default="search", choices=["search", "plain", "vmm", "auto"],
                     help="plan-build placement of the BIN product buffer / DIA values (spmv_hip.h "
                          "SPMV_PLACEMENT_*): the bench owns the GPU, so it asks for the build-time search")
@@ -229,12 +235,14 @@ def main():
     fmts = [f for f in args.formats.split(",") if f]
     results = {}
     headline = None
-    for fi, fmt in enumerate(fmts):
+    for fi, spec_f in enumerate(fmts):
+        fmt, _, placement = spec_f.partition("@")
+        placement = placement or args.placement
         tp = time.time()
         try:
-            plan = sp.Plan.from_csr(rows, n_glob, rp, col, val, fmt=fmt, device=local, placement=args.placement)
+            plan = sp.Plan.from_csr(rows, n_glob, rp, col, val, fmt=fmt, device=local, placement=placement)
         except sp.SpmvError as e:
-            results[fmt] = {"error": str(e)}
+            results[spec_f] = {"error": str(e)}
             continue
         t_plan = time.time() - tp
         info = plan.info()
@@ -284,7 +292,7 @@ def main():
             r["phases_ms"] = plan.profile(x, y, 10)  # Mul / Sum split (opt_ss MulPerf / SumPerf)
         for k in relevant.get(info["format"], ()):
             r[k] = info[k]
-        results[fmt if fmt not in results else f"{fmt}_{fi}"] = r
+        results[spec_f if spec_f not in results else f"{spec_f}_{fi}"] = r
         if fi == 0:
             r["phases_ms"] = plan.profile(x, y, 10)
             headline = (plan, info, r)
