@@ -11,6 +11,7 @@
 //   chunk  : the same per-wave batches, but batch j of wave w sits at
 //            (j*W + w)*64*U: all waves read one moving window of W batches
 // Output: one JSON line per (shape, U, waves).
+//   hipcc -O3 --offload-arch=gfx950 -o bin/stream_shape_probe tools/stream_shape_probe.hip
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
