@@ -1,0 +1,16 @@
+#!/bin/bash
+# What holds the Sum: ablations (probe build, wrong sums) at configs 2, 3 and
+# the 8-GPU rank shape -- no LDS atomics (SPMV_BIN_DEBUG=8), no slot loads (512)
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out/r2_sum_ablate
+mkdir -p $O
+cd $R
+export SPMV_HIP_LIBRARY=probes_build/libspmv_hip.so
+V='base:;noat:SPMV_BIN_DEBUG=8;noslot:SPMV_BIN_DEBUG=512;base2:'
+timeout -k 10 300 python3 -u tools/bin_phase_ab.py --fmt bin --kind uniform --rows 10000000 --placement search \
+    --rounds 3 --iters 20 --variants "$V" > $O/c2.jsonl 2> $O/c2.err || exit $?
+timeout -k 10 300 python3 -u tools/bin_phase_ab.py --fmt bin --kind powerlaw --rows 5000000 --placement search \
+    --rounds 3 --iters 20 --variants "$V" > $O/c3.jsonl 2> $O/c3.err || exit $?
+timeout -k 10 300 python3 -u tools/bin_phase_ab.py --fmt bin --kind uniform --rows 10000000 --ncols 80000000 \
+    --placement search --rounds 3 --iters 20 --variants "$V" > $O/w8.jsonl 2> $O/w8.err || exit $?
