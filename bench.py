@@ -506,6 +506,13 @@ def main():
             v = t[key]
             out["roofline"]["traffic"] = v["bytes"] if isinstance(v, dict) else v
             out["roofline"]["traffic_kind"] = kind
+            # the HBM bandwidth the kernels actually sustain: the profiled
+            # bytes of one launch over this run's launch time (BIN moves
+            # ~2.4x the algorithmic bytes; frac above prices only those)
+            tg = out["roofline"]["traffic"] / (r["event_ms_per_launch"] * 1e-3) / 1e9
+            out["roofline"]["traffic_gbs"] = tg
+            out["roofline"]["traffic_frac"] = tg / HBM_PEAK_GBS
+            out["roofline"]["traffic_frac_of_stream"] = tg / stream_gbs
             break
     if rank == 0:
         print(json.dumps(out), flush=True)
