@@ -411,6 +411,25 @@ def test_driver_binary_reports_block(fmt, name):
     assert out.returncode == 0, out.stderr + out.stdout
     assert "++++" in out.stdout and "Performance(GFLOPS)" in out.stdout
     assert f"MatrixFormat\t{name}" in out.stdout.replace(" ", "")
+    # the block parses the way the reference's log tooling reads it
+    # (log/format.cpp:32-49: a line of 40 '+' opens a record, each line is
+    # "key value" split on whitespace, a line of 40 '-' closes it)
+    records, cur = [], None
+    for line in out.stdout.splitlines():
+        if line == "+" * 40:
+            cur = {}
+        elif line == "-" * 40:
+            records.append(cur)
+            cur = None
+        elif cur is not None:
+            kv = line.split()
+            if len(kv) >= 2:
+                cur[kv[0]] = kv[1]
+    assert len(records) == 1, out.stdout
+    rec = records[0]
+    assert (rec["Architecture"], rec["MatrixFormat"]) == ("GPU", name)
+    assert (int(rec["nRow"]), int(rec["nCol"]), int(rec["nNnz"])) == (10, 10, 95)
+    assert rec["Matrix"].startswith("random") and float(rec["Performance(GFLOPS)"]) > 0
 
 
 def _with_empty_rows(rp, col, val, frac, seed):
