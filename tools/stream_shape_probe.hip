@@ -60,6 +60,45 @@ __global__ __launch_bounds__(256) void rd(const double *__restrict__ a, long lon
     if (s == 1.2345) out[0] = s;
 }
 
+// one wave per workgroup (one per CU), its own region, two batches in flight
+// (ping-pong, like the Sum); VEC: 16-byte loads (lane l reads entries 2l, 2l+1
+// of every 128-entry block) instead of 8-byte ones
+template <int U, bool VEC>
+__global__ __launch_bounds__(64) void rd1(const double *__restrict__ a, long long n, double *__restrict__ out) {
+    typedef double f64x2 __attribute__((ext_vector_type(2)));
+    const long long W = gridDim.x, w = blockIdx.x;
+    const int lane = threadIdx.x;
+    const long long step = 64LL * U, nb = n / (W * step);
+    double s = 0;
+    double A[U], B[U];
+    auto load = [&](double *v, long long j) {
+        const long long base = (w * nb + j) * step;
+        if (VEC) {
+#pragma unroll
+            for (int u = 0; u < U; u += 2) {
+                const f64x2 t = __builtin_nontemporal_load(reinterpret_cast<const f64x2 *>(a + base + (u / 2) * 128 + 2 * lane));
+                v[u] = t.x;
+                v[u + 1] = t.y;
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < U; ++u) v[u] = __builtin_nontemporal_load(a + base + u * 64 + lane);
+        }
+    };
+    load(A, 0);
+    for (long long j = 0; j < nb; j += 2) {
+        if (j + 1 < nb) load(B, j + 1);
+#pragma unroll
+        for (int u = 0; u < U; ++u) s += A[u];
+        if (j + 1 < nb) {
+            if (j + 2 < nb) load(A, j + 2);
+#pragma unroll
+            for (int u = 0; u < U; ++u) s += B[u];
+        }
+    }
+    if (s == 1.2345) out[0] = s;
+}
+
 int main() {
     const long long bytes = 1792LL << 20;  // 1.75 GB: 7 * 2^28, divisible by every W*64*U below
     const long long n = bytes / 8;
@@ -100,6 +139,12 @@ int main() {
         report("region", 16, W, t_of([&] { rd<1, 16><<<wg, 256>>>(buf, n, out); }));
         report("chunk", 16, W, t_of([&] { rd<2, 16><<<wg, 256>>>(buf, n, out); }));
     }
+    // one wave per CU (the one-wave Sum of 20479-row bins)
+    report("region1w", 32, 256, t_of([&] { rd1<32, false><<<256, 64>>>(buf, n, out); }));
+    report("region1w_vec", 32, 256, t_of([&] { rd1<32, true><<<256, 64>>>(buf, n, out); }));
+    report("region1w", 64, 256, t_of([&] { rd1<64, false><<<256, 64>>>(buf, n, out); }));
+    report("region1w_vec", 64, 256, t_of([&] { rd1<64, true><<<256, 64>>>(buf, n, out); }));
+    report("region2w_vec", 32, 512, t_of([&] { rd1<32, true><<<512, 64>>>(buf, n, out); }));
     CHECK(hipFree(buf));
     CHECK(hipFree(out));
     return 0;
