@@ -711,7 +711,7 @@ static int bin_finish(spmv_plan_s *p, int64_t n, const BinLayout &L, const spmv_
     B.prod_cap = B.reuse ? 0 : (L.LL > 0 ? L.TRASH + L.PAD : E);
     if (B.reuse)
         for (int g = 0; g < B.G; ++g) B.prod_cap = std::max(B.prod_cap, B.g_prod[(size_t)g + 1] - B.g_prod[(size_t)g]);
-    const size_t prod_bytes = sizeof(double) * (size_t)std::max<int64_t>(B.prod_cap, 1);
+    const size_t prod_bytes = sizeof(double) * (size_t)(std::max<int64_t>(B.prod_cap, 1) + kBinProdSlack);
     SPMV_RETURN_IF(upload_vec(p, &B.piece_off, piece_off));
     SPMV_RETURN_IF(upload_vec(p, &B.piece_strip, pstrip));
     SPMV_RETURN_IF(upload_vec(p, &B.piece_begin, pbeg));

@@ -458,7 +458,9 @@ int spmv_css_layout(spmv_plan_t p, int64_t *bstart, int64_t *woff) {
 int spmv_bin_realloc_prod(spmv_plan_t p) {
     if (!p || p->format != SPMV_FORMAT_BIN || !p->bin.prod) return -1;
     void *q = nullptr;
-    if (p->arena.alloc(&q, sizeof(double) * (size_t)std::max<int64_t>(p->bin.prod_cap, 1)) != SPMV_SUCCESS) return -1;
+    if (p->arena.alloc(&q, sizeof(double) * (size_t)(std::max<int64_t>(p->bin.prod_cap, 1) + kBinProdSlack)) !=
+        SPMV_SUCCESS)
+        return -1;
     p->bin.prod = (double *)q;
     return 0;
 }

@@ -251,6 +251,10 @@ __host__ __device__ inline int64_t bin_slot_index(int64_t e, int64_t r0, int64_t
     const int64_t u = w >> 6, lane = w & 63;
     return s0 + i * step + (u >> 3) * 512 + lane * 8 + (u & 7);
 }
+// The Sum reads whole batches of 64*U products without clamping at a run's
+// end (the padded slot batches send those lanes to the dummy slot), so the
+// product buffer carries one batch of slack past its last run.
+constexpr int64_t kBinProdSlack = 64 * 32;
 struct BinDev {
     int strip = 20480;     // x strip width in columns (<= kBinMaxStrip)
     int pad_log = 3;       // segments padded to 2^pad_log entries (8: 64-B product lines)

@@ -235,13 +235,22 @@ __device__ __forceinline__ void sum_load(SumBatch<U, MODE> &B, int64_t base, int
             B.v[u] = v.x;
             B.v[u + 1] = v.y;
         }
-    } else {
+    } else if constexpr ((MODE & 40) != 0) {  // slot-linear ablation / 32: the clamped loads (A/B)
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int64_t e = base + u * 64 + lane;
             const int64_t ee = e < p1 ? e : p0;
             B.v[u] = (MODE & 1) ? ld_stream(prod + (ee - pbase)) : prod[ee - pbase];
         }
+    } else {
+        // the whole batch, unclamped: lanes past the run's end read the next
+        // run's products (or the buffer's slack, kBinProdSlack) and their
+        // slots -- the padding of the batch's slot block -- are the dummy
+        // slot, so nothing but +x reaches a real row.  One base address, the
+        // u offsets are immediates: no per-entry clamp or 64-bit address math.
+        const double *pp = prod + (base - pbase) + lane;
+#pragma unroll
+        for (int u = 0; u < U; ++u) B.v[u] = (MODE & 1) ? ld_stream(pp + u * 64) : pp[u * 64];
     }
     if ((MODE & 12) == 4) {
 #pragma unroll
@@ -254,15 +263,20 @@ __device__ __forceinline__ void sum_add(const SumBatch<U, MODE> &B, int64_t base
                                         double &sink) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-        // masked lanes (past the bin) add +0.0 to the dummy slot
-        const bool ok = base + u * 64 + lane < p1;
-        if (MODE & 2) sink += B.v[u] * (double)B.slot(u);
-        else atomicAdd(&ys[ok ? B.slot(u) : DUMMY], ok ? B.v[u] : 0.0);
+        // lanes past the run read the padding of the slot block: the dummy slot
+        if (MODE & 2) {
+            sink += B.v[u] * (double)B.slot(u);
+        } else if constexpr ((MODE & 40) != 0) {  // slot-linear ablation / clamped A/B: mask here
+            const bool ok = base + u * 64 + lane < p1;
+            atomicAdd(&ys[ok ? B.slot(u) : DUMMY], ok ? B.v[u] : 0.0);
+        } else {
+            atomicAdd(&ys[B.slot(u)], B.v[u]);  // past the run: the dummy slot
+        }
     }
 }
 
 // MODE (internal ablations): 1 nontemporal product loads (the default), 2 no LDS atomics,
-// 4 no slot loads.  W2 waves per workgroup, each owning a slice of
+// 4 no slot loads, 32 product loads clamped at the run's end (the round-2 loads, A/B).  W2 waves per workgroup, each owning a slice of
 // kBinLdsDoubles / W2 doubles.  A bin's products are NBK runs (one per strip
 // block, run_off[blk*nbins + b]); the batches walk them in order (a batch
 // never crosses a run), ping-ponged so one batch is always in flight.
@@ -386,6 +400,10 @@ static void launch_sum_w(const spmv_plan_s *p, int g, double *y) {
     }
     if (p->bin.dbg & 1024) {  // ablation: 16-byte product loads (wrong sums)
         launch_sum_t<W2, U, 17>(p, g, y);
+        return;
+    }
+    if (p->bin.dbg & 8192) {  // A/B: product loads clamped at the run's end, masked adds
+        launch_sum_t<W2, U, 33>(p, g, y);
         return;
     }
     // default: nontemporal product loads (config 2 Sum 0.308 -> 0.298 ms,

@@ -14,7 +14,7 @@
 //     blocks after its segments, and the trash line lies past every run.
 //   * emulates both kernels (k_bin.hip bin_mul_kernel / bin_sum_kernel: the
 //     same workgroup pieces, wave batches, lane clamps, long-block scan and
-//     Sum batches) on the host builder's arrays, checking every index a lane
+//     unclamped Sum batches) on the host builder's arrays, checking every index a lane
 //     forms against its array's bounds, that the Sum reads only products the
 //     Mul wrote, and that y is the sequential row sum -- bit for bit on
 //     short rows, within 1e-12 of sum |a x| on long rows.
@@ -141,7 +141,14 @@ static int emulate(const BinDev &B, const HostCsr &A, const BinLayout &L, const 
                         const int64_t e = pos + u * 64 + lane;
                         const int64_t si = sbase + (u / 8) * 512 + lane * 8 + (u % 8);
                         if (si >= L.ES) return fail("slot index", si, L.ES);
-                        if (e >= bhi) continue;
+                        if (e >= bhi) {
+                            // sum_load reads the whole batch unclamped: past the
+                            // run it must stay inside the buffer (with its slack)
+                            // and hit the dummy slot
+                            if (e >= prod_cap + kBinProdSlack) return fail("sum reads past the product buffer", e, prod_cap);
+                            if (H.slot2[(size_t)si] != SLICE - 1) return fail("slot past a run is not the dummy", e, H.slot2[(size_t)si]);
+                            continue;
+                        }
                         if (e >= prod_cap || !written[(size_t)e]) return fail("sum reads an unwritten product", e);
                         const int slot = H.slot2[(size_t)si];
                         if (slot > SLICE - 1) return fail("slot past the dummy", slot);
