@@ -411,10 +411,10 @@ static void bin_fill_arrays(const BinDev &B, const HostCsr &A, const BinLayout &
     std::vector<double> &val1 = H.val1;
     std::vector<uint16_t> &cs1 = H.cs1, &slot2 = H.slot2;
     std::vector<int32_t> &dst1 = H.dst1;
-    val1.assign((size_t)E1, 0.0);
-    cs1.assign((size_t)E1, 0);
+    val1.assign((size_t)(E1 + kBinMulSlack), 0.0);
+    cs1.assign((size_t)(E1 + kBinMulSlack), 0);
     slot2.assign((size_t)L.ES, (uint16_t)max_rows);
-    dst1.assign((size_t)(E1 >> B.pad_log), (int32_t)(L.TRASH >> B.pad_log));
+    dst1.assign((size_t)((E1 + kBinMulSlack) >> B.pad_log), (int32_t)(L.TRASH >> B.pad_log));
     std::vector<int> gof((size_t)NB);
     for (int g = 0; g < B.G; ++g)
         for (int64_t b = B.g_bin[(size_t)g]; b < B.g_bin[(size_t)g + 1]; ++b) gof[(size_t)b] = g;

@@ -255,6 +255,10 @@ __host__ __device__ inline int64_t bin_slot_index(int64_t e, int64_t r0, int64_t
 // end (the padded slot batches send those lanes to the dummy slot), so the
 // product buffer carries one batch of slack past its last run.
 constexpr int64_t kBinProdSlack = 64 * 32;
+// Likewise the Mul loads a wave's batch (64 x 8 entries) of val1 / cs1 / dst1
+// without clamping at its piece's end (the stores past it are masked), so
+// those arrays carry one batch of slack.
+constexpr int64_t kBinMulSlack = 64 * 8;
 struct BinDev {
     int strip = 20480;     // x strip width in columns (<= kBinMaxStrip)
     int pad_log = 3;       // segments padded to 2^pad_log entries (8: 64-B product lines)

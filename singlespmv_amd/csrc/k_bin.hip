@@ -59,16 +59,36 @@ __device__ __forceinline__ void mul_load(MulBatch<U> &B, int64_t base, int64_t e
                                          const double *__restrict__ val1, const uint16_t *__restrict__ cs1,
                                          const int32_t *__restrict__ dst1, int64_t ls, int64_t lsh,
                                          const int32_t *__restrict__ lcode) {
+    if constexpr ((MODE & 64) == 0 && !LONG) {
+        // lanes past the piece load the next entries unclamped (the arrays
+        // carry kBinMulSlack; their stores are masked): one base address per
+        // array, the u offsets are immediates (64 entries = 64 >> PL groups).
+        // (With long blocks the extra live addresses spill: clamped below.)
+        const double *vb = val1 + base + lane;
+        const uint16_t *cb = cs1 + base + lane;
+        const int32_t *db = dst1 + ((base + lane) >> PL);
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-        const int64_t e = base + u * 64 + lane;
-        const int64_t ee = e < e1 ? e : e0;
-        B.v[u] = ld_stream(val1 + ee);
-        B.c[u] = (MODE & 8) ? (uint32_t)((ee * 2654435761u) & 16383) : (uint32_t)__builtin_nontemporal_load(cs1 + ee);
-        // a lane past the piece (e >= e1, masked at the store) reads word 0:
-        // its clamped e0 may lie in the segments, before the long blocks
-        if (LONG && base + u * 64 >= ls) B.d[u] = ld_stream(lcode + (e < e1 ? e + lsh : 0));
-        else B.d[u] = ld_stream(dst1 + (ee >> PL));
+        for (int u = 0; u < U; ++u) {
+            B.v[u] = ld_stream(vb + u * 64);
+            B.c[u] = (MODE & 8) ? (uint32_t)(((base + u * 64 + lane) * 2654435761u) & 16383)
+                                : (uint32_t)__builtin_nontemporal_load(cb + u * 64);
+            // a lane past the piece (e >= e1, masked at the store) reads word 0:
+            // its e may lie beyond the strip's long blocks
+            const int64_t e = base + u * 64 + lane;
+            if (LONG && base + u * 64 >= ls) B.d[u] = ld_stream(lcode + (e < e1 ? e + lsh : 0));
+            else B.d[u] = ld_stream(db + u * (64 >> PL));
+        }
+        (void)e0;
+    } else {  // LONG, or MODE 64 (A/B): every load clamped at the piece's end
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t e = base + u * 64 + lane;
+            const int64_t ee = e < e1 ? e : e0;
+            B.v[u] = ld_stream(val1 + ee);
+            B.c[u] = (MODE & 8) ? (uint32_t)((ee * 2654435761u) & 16383) : (uint32_t)__builtin_nontemporal_load(cs1 + ee);
+            if (LONG && base + u * 64 >= ls) B.d[u] = ld_stream(lcode + (e < e1 ? e + lsh : 0));
+            else B.d[u] = ld_stream(dst1 + (ee >> PL));
+        }
     }
 }
 
@@ -362,8 +382,10 @@ static void launch_mul_p(const spmv_plan_s *p, int g, const double *x) {
             else launch_mul_t<5, PL>(p, g, x);
             break;
         default:
-            // long-block partial stores: 2048 nontemporal, 4096 none (ablations)
-            if (p->bin.dbg & 2048) launch_mul_t<17, PL>(p, g, x);
+            // long-block partial stores: 2048 nontemporal, 4096 none (ablations);
+            // 16384: loads clamped at the piece's end (A/B)
+            if (p->bin.dbg & 16384) launch_mul_t<65, PL>(p, g, x);
+            else if (p->bin.dbg & 2048) launch_mul_t<17, PL>(p, g, x);
             else if (p->bin.dbg & 4096) launch_mul_t<33, PL>(p, g, x);
             else launch_mul_t<1, PL>(p, g, x);
     }

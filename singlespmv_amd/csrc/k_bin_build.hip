@@ -210,14 +210,18 @@ int bin_fill_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, c
         for (int g = 0; g < B.G; ++g)
             for (int64_t b = B.g_bin[(size_t)g]; b < B.g_bin[(size_t)g + 1]; ++b) pbb[(size_t)b] = B.g_prod[(size_t)g];
     void *q;
-    SPMV_RETURN_IF(p->arena.alloc(&q, sizeof(double) * (size_t)E));
+    // val1 / cs1 / dst1 with the Mul's unclamped-batch slack (kBinMulSlack), zeroed
+    SPMV_RETURN_IF(p->arena.alloc(&q, sizeof(double) * (size_t)(E + kBinMulSlack)));
     B.val1 = (double *)q;
-    SPMV_RETURN_IF(p->arena.alloc(&q, sizeof(uint16_t) * (size_t)E));
+    SPMV_HIP_TRY(hipMemsetAsync(B.val1 + E, 0, sizeof(double) * (size_t)kBinMulSlack, st));
+    SPMV_RETURN_IF(p->arena.alloc(&q, sizeof(uint16_t) * (size_t)(E + kBinMulSlack)));
     B.cs1 = (uint16_t *)q;
+    SPMV_HIP_TRY(hipMemsetAsync(B.cs1 + E, 0, sizeof(uint16_t) * (size_t)kBinMulSlack, st));
     SPMV_RETURN_IF(p->arena.alloc(&q, sizeof(uint16_t) * (size_t)std::max<int64_t>(ES, 1)));
     B.slot2 = (uint16_t *)q;
-    SPMV_RETURN_IF(p->arena.alloc(&q, sizeof(int32_t) * (size_t)std::max<int64_t>(E >> B.pad_log, 1)));
+    SPMV_RETURN_IF(p->arena.alloc(&q, sizeof(int32_t) * (size_t)std::max<int64_t>((E + kBinMulSlack) >> B.pad_log, 1)));
     B.dst1 = (int32_t *)q;
+    SPMV_HIP_TRY(hipMemsetAsync(B.dst1 + (E >> B.pad_log), 0, sizeof(int32_t) * (size_t)(kBinMulSlack >> B.pad_log), st));
     Scratch sc{st, {}};
     int32_t *d_row0, *d_cnt;
     int64_t *d_bstart, *d_off1, *d_off2, *d_pbb, *d_ks, *d_run, *d_srun;

@@ -62,19 +62,23 @@ static int emulate(const BinDev &B, const HostCsr &A, const BinLayout &L, const 
                         int32_t d[64];
                         bool ok[64];
                         for (int lane = 0; lane < 64; ++lane) {
-                            const int64_t e = bs + lane, ee = e < e1 ? e : e0;
+                            // mul_load: unclamped -- lanes past the piece read on
+                            // into the slack (their stores are masked)
+                            const int64_t e = bs + lane, ee = e;
                             ok[lane] = e < e1;
-                            if (ee < 0 || ee >= L.E1) return fail("mul val1/cs1 index", ee, L.E1);
+                            if (ee < 0 || ee >= (int64_t)H.val1.size() || ee >= (int64_t)H.cs1.size())
+                                return fail("mul val1/cs1 index", ee, H.val1.size());
                             const int64_t c = H.cs1[(size_t)ee];
-                            if (c >= cw) return fail("mul x strip index", c, cw);
-                            v[lane] = H.val1[(size_t)ee] * x[(size_t)(c0 + c)];
+                            if (c >= C) return fail("mul LDS strip index", c, C);
+                            if (ok[lane] && c >= cw) return fail("mul x strip index", c, cw);
+                            v[lane] = ok[lane] ? H.val1[(size_t)ee] * x[(size_t)(c0 + c)] : 0.0;
                             if (lng) {
                                 const int64_t i = e < e1 ? e + lsh : 0;
                                 if (i < 0 || i >= (int64_t)H.lcode.size()) return fail("mul lcode index", i, H.lcode.size());
                                 d[lane] = H.lcode[(size_t)i];
                             } else {
                                 const int64_t i = ee >> PL;
-                                if (i >= (int64_t)H.dst1.size()) return fail("mul dst1 index", i, H.dst1.size());
+                                if (i < 0 || i >= (int64_t)H.dst1.size()) return fail("mul dst1 index", i, H.dst1.size());
                                 d[lane] = H.dst1[(size_t)i];
                             }
                         }
