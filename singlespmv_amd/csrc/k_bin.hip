@@ -296,7 +296,8 @@ __device__ __forceinline__ void sum_add(const SumBatch<U, MODE> &B, int64_t base
 }
 
 // MODE (internal ablations): 1 nontemporal product loads (the default), 2 no LDS atomics,
-// 4 no slot loads, 32 product loads clamped at the run's end (the round-2 loads, A/B).  W2 waves per workgroup, each owning a slice of
+// 4 no slot loads, 32 product loads clamped at the run's end (the round-2 loads, A/B),
+// 128 no LDS zeroing / y write-back.  W2 waves per workgroup, each owning a slice of
 // kBinLdsDoubles / W2 doubles.  A bin's products are NBK runs (one per strip
 // block, run_off[blk*nbins + b]); the batches walk them in order (a batch
 // never crosses a run), ping-ponged so one batch is always in flight.
@@ -315,7 +316,8 @@ __global__ __launch_bounds__(64 * W2) void bin_sum_kernel(
     for (int64_t b = b0 + (int64_t)blockIdx.x * W2 + w; b < b1; b += (int64_t)gridDim.x * W2) {
         const int64_t r0 = bin_row0[b];
         const int rows = (int)(bin_row0[b + 1] - r0);
-        for (int i = lane; i < rows; i += 64) ys[i] = 0.0;
+        if ((MODE & 128) == 0)  // 128 (ablation): no LDS zeroing / y write-back
+            for (int i = lane; i < rows; i += 64) ys[i] = 0.0;
         double sink = 0.0;
         // run cursor: batch = [pos, min(pos + STEP, end)) of run k
         // run k of bin b: products from rs, slots from ss (batch-aligned)
@@ -348,7 +350,8 @@ __global__ __launch_bounds__(64 * W2) void bin_sum_kernel(
         }
         if ((MODE & 2) && sink == 1.2345e300) ys[0] = sink;
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        for (int i = lane; i < rows; i += 64) y[r0 + i] = ys[i];
+        if ((MODE & 128) == 0)
+            for (int i = lane; i < rows; i += 64) y[r0 + i] = ys[i];
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     }
 }
@@ -426,6 +429,10 @@ static void launch_sum_w(const spmv_plan_s *p, int g, double *y) {
     }
     if (p->bin.dbg & 8192) {  // A/B: product loads clamped at the run's end, masked adds
         launch_sum_t<W2, U, 33>(p, g, y);
+        return;
+    }
+    if (p->bin.dbg & 32768) {  // ablation: no LDS zeroing / y write-back (wrong y)
+        launch_sum_t<W2, U, 129>(p, g, y);
         return;
     }
     // default: nontemporal product loads (config 2 Sum 0.308 -> 0.298 ms,
