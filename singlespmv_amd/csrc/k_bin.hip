@@ -297,10 +297,14 @@ __device__ __forceinline__ void sum_add(const SumBatch<U, MODE> &B, int64_t base
 
 // MODE (internal ablations): 1 nontemporal product loads (the default), 2 no LDS atomics,
 // 4 no slot loads, 32 product loads clamped at the run's end (the round-2 loads, A/B),
-// 128 no LDS zeroing / y write-back.  W2 waves per workgroup, each owning a slice of
-// kBinLdsDoubles / W2 doubles.  A bin's products are NBK runs (one per strip
-// block, run_off[blk*nbins + b]); the batches walk them in order (a batch
-// never crosses a run), ping-ponged so one batch is always in flight.
+// 128 no LDS zeroing / y write-back, 256 one bin at a time (A/B: the loads of a
+// bin's first batch wait for the previous bin's y write-back).  W2 waves per
+// workgroup, each owning a slice of kBinLdsDoubles / W2 doubles.  A bin's
+// products are NBK runs (one per strip block, run_off[blk*nbins + b]); the
+// batches walk them in order (a batch never crosses a run), ping-ponged so one
+// batch is always in flight -- across the wave's bins too: the next bin's
+// first batches are already loading while the finished bin's y is written
+// from LDS (its write-back and the loads overlap instead of alternating).
 template <int W2, int U, int MODE>
 __global__ __launch_bounds__(64 * W2) void bin_sum_kernel(
     int64_t b0, int64_t b1, int64_t nbins, int64_t nblk, const int64_t *__restrict__ run_off,
@@ -313,46 +317,119 @@ __global__ __launch_bounds__(64 * W2) void bin_sum_kernel(
     const int w = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
     double *ys = ylds + w * SLICE;
-    for (int64_t b = b0 + (int64_t)blockIdx.x * W2 + w; b < b1; b += (int64_t)gridDim.x * W2) {
-        const int64_t r0 = bin_row0[b];
-        const int rows = (int)(bin_row0[b + 1] - r0);
-        if ((MODE & 128) == 0)  // 128 (ablation): no LDS zeroing / y write-back
-            for (int i = lane; i < rows; i += 64) ys[i] = 0.0;
-        double sink = 0.0;
-        // run cursor: batch = [pos, min(pos + STEP, end)) of run k
-        // run k of bin b: products from rs, slots from ss (batch-aligned)
-        int64_t k = 0, pos = run_off[b], end = run_off[b + 1], rs = pos, ss = srun_off[b];
-        auto next = [&](int64_t &lo, int64_t &hi, int64_t &sb) -> bool {
+    const int64_t bfirst = b0 + (int64_t)blockIdx.x * W2 + w, bstride = (int64_t)gridDim.x * W2;
+    if constexpr ((MODE & (2 | 128 | 256)) != 0) {
+        for (int64_t b = bfirst; b < b1; b += bstride) {
+            const int64_t r0 = bin_row0[b];
+            const int rows = (int)(bin_row0[b + 1] - r0);
+            if ((MODE & 128) == 0)  // 128 (ablation): no LDS zeroing / y write-back
+                for (int i = lane; i < rows; i += 64) ys[i] = 0.0;
+            double sink = 0.0;
+            // run cursor: batch = [pos, min(pos + STEP, end)) of run k
+            // run k of bin b: products from rs, slots from ss (batch-aligned)
+            int64_t k = 0, pos = run_off[b], end = run_off[b + 1], rs = pos, ss = srun_off[b];
+            auto next = [&](int64_t &lo, int64_t &hi, int64_t &sb) -> bool {
+                while (pos >= end) {
+                    if (++k >= nblk) return false;
+                    pos = rs = run_off[k * nbins + b];
+                    end = run_off[k * nbins + b + 1];
+                    ss = srun_off[k * nbins + b];
+                }
+                lo = pos;
+                hi = pos + STEP < end ? pos + STEP : end;
+                sb = ss + (lo - rs);
+                pos = hi;
+                return true;
+            };
+            SumBatch<U, MODE> A, B;
+            int64_t alo, ahi, asb, blo, bhi, bsb;
+            bool has_a = next(alo, ahi, asb);
+            if (has_a) sum_load<U, MODE>(A, alo, alo, ahi, lane, pbase, asb, slot2, prod);
+            while (has_a) {
+                const bool has_b = next(blo, bhi, bsb);
+                if (has_b) sum_load<U, MODE>(B, blo, blo, bhi, lane, pbase, bsb, slot2, prod);
+                sum_add<U, MODE, SLICE - 1>(A, alo, ahi, lane, ys, sink);
+                if (!has_b) break;
+                has_a = next(alo, ahi, asb);
+                if (has_a) sum_load<U, MODE>(A, alo, alo, ahi, lane, pbase, asb, slot2, prod);
+                sum_add<U, MODE, SLICE - 1>(B, blo, bhi, lane, ys, sink);
+            }
+            if ((MODE & 2) && sink == 1.2345e300) ys[0] = sink;
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            if ((MODE & 128) == 0)
+                for (int i = lane; i < rows; i += 64) y[r0 + i] = ys[i];
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        }
+    } else {
+        if (bfirst >= b1) return;
+        // one cursor over all of the wave's bins: bin cb, its run k, the
+        // batch [pos, min(pos + STEP, end)); products from rs, slots from ss
+        int64_t cb = bfirst, k = 0, pos = run_off[cb], end = run_off[cb + 1], rs = pos, ss = srun_off[cb];
+        auto next = [&](int64_t &lo, int64_t &hi, int64_t &sb, int64_t &bb) -> bool {
             while (pos >= end) {
-                if (++k >= nblk) return false;
-                pos = rs = run_off[k * nbins + b];
-                end = run_off[k * nbins + b + 1];
-                ss = srun_off[k * nbins + b];
+                if (++k >= nblk) {  // bin cb exhausted: the wave's next bin
+                    cb += bstride;
+                    if (cb >= b1) return false;
+                    k = 0;
+                    pos = rs = run_off[cb];
+                    end = run_off[cb + 1];
+                    ss = srun_off[cb];
+                    continue;
+                }
+                pos = rs = run_off[k * nbins + cb];
+                end = run_off[k * nbins + cb + 1];
+                ss = srun_off[k * nbins + cb];
             }
             lo = pos;
             hi = pos + STEP < end ? pos + STEP : end;
             sb = ss + (lo - rs);
+            bb = cb;
             pos = hi;
             return true;
         };
+        // acc: the bin in the LDS slice; done: the wave's first bin whose y
+        // is not written yet (bins without products get zeros)
+        int64_t acc = -1, done = bfirst;
+        auto write_zero = [&](int64_t bz) {
+            const int64_t r0 = bin_row0[bz];
+            const int rows = (int)(bin_row0[bz + 1] - r0);
+            for (int i = lane; i < rows; i += 64) y[r0 + i] = 0.0;
+        };
+        auto finish = [&]() {  // the slice's bin: LDS adds done -> y
+            const int64_t r0 = bin_row0[acc];
+            const int rows = (int)(bin_row0[acc + 1] - r0);
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            for (int i = lane; i < rows; i += 64) y[r0 + i] = ys[i];
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            done = acc + bstride;
+        };
+        auto begin = [&](int64_t nb) {  // the next batch belongs to bin nb
+            if (nb == acc) return;
+            if (acc >= 0) finish();
+            for (; done < nb; done += bstride) write_zero(done);
+            const int rows = (int)(bin_row0[nb + 1] - bin_row0[nb]);
+            for (int i = lane; i < rows; i += 64) ys[i] = 0.0;
+            acc = nb;
+            done = nb + bstride;
+        };
+        double sink = 0.0;
         SumBatch<U, MODE> A, B;
-        int64_t alo, ahi, asb, blo, bhi, bsb;
-        bool has_a = next(alo, ahi, asb);
+        int64_t alo, ahi, asb, ab, blo, bhi, bsb, bbn;
+        bool has_a = next(alo, ahi, asb, ab);
         if (has_a) sum_load<U, MODE>(A, alo, alo, ahi, lane, pbase, asb, slot2, prod);
         while (has_a) {
-            const bool has_b = next(blo, bhi, bsb);
+            const bool has_b = next(blo, bhi, bsb, bbn);
             if (has_b) sum_load<U, MODE>(B, blo, blo, bhi, lane, pbase, bsb, slot2, prod);
+            begin(ab);
             sum_add<U, MODE, SLICE - 1>(A, alo, ahi, lane, ys, sink);
             if (!has_b) break;
-            has_a = next(alo, ahi, asb);
+            has_a = next(alo, ahi, asb, ab);
             if (has_a) sum_load<U, MODE>(A, alo, alo, ahi, lane, pbase, asb, slot2, prod);
+            begin(bbn);
             sum_add<U, MODE, SLICE - 1>(B, blo, bhi, lane, ys, sink);
         }
-        if ((MODE & 2) && sink == 1.2345e300) ys[0] = sink;
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        if ((MODE & 128) == 0)
-            for (int i = lane; i < rows; i += 64) y[r0 + i] = ys[i];
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        if (acc >= 0) finish();
+        for (; done < b1; done += bstride) write_zero(done);
     }
 }
 
@@ -433,6 +510,10 @@ static void launch_sum_w(const spmv_plan_s *p, int g, double *y) {
     }
     if (p->bin.dbg & 32768) {  // ablation: no LDS zeroing / y write-back (wrong y)
         launch_sum_t<W2, U, 129>(p, g, y);
+        return;
+    }
+    if (p->bin.dbg & 65536) {  // A/B: one bin at a time
+        launch_sum_t<W2, U, 257>(p, g, y);
         return;
     }
     // default: nontemporal product loads (config 2 Sum 0.308 -> 0.298 ms,

@@ -811,6 +811,36 @@ def test_bin_edge_cases():
         sp.Plan.from_csr(50_000, 50_000, rp, col, val, "bin", bin_strip_cols=20481)
 
 
+@pytest.mark.parametrize("sum_waves", [0, 2])
+def test_bin_empty_bins_between_full_ones(sum_waves):
+    """Bins without products among a wave's bins (runs of empty rows longer
+    than a bin, 2+ bins per Sum wave): the Sum walks all of a wave's bins with
+    one batch cursor (the next bin's loads in flight during the write-back),
+    so an empty bin must still get its zeros -- y starts as garbage here."""
+    m, n = 6_000_000, 1_000_000
+    rng = np.random.default_rng(17)
+    lens = np.zeros(m, np.int64)
+    lens[100_000:3_000_000] = 2
+    lens[3_200_000:m] = 1
+    lens[4_000_000:4_040_000] = 0  # an empty stretch in the middle of the wave sequence
+    rp = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    nnz = int(rp[-1])
+    col = np.sort(rng.integers(0, n, size=nnz).astype(np.int32).reshape(-1, 1), axis=1).ravel()
+    # columns ascending within each row (2-entry rows: sort pairs)
+    two = np.flatnonzero(lens == 2)
+    starts = rp[two]
+    a, b = col[starts], col[starts + 1]
+    col[starts], col[starts + 1] = np.minimum(a, b), np.maximum(a, b)
+    val = rng.random(nnz) + 0.5
+    x = sp.generate_vector(n, seed=5)
+    plan = sp.Plan.from_csr(m, n, rp, col, val, "bin", bin_sum_waves=sum_waves)
+    info = plan.info()
+    assert info["bin_bins"] >= 1024  # two or more bins per Sum wave
+    y = run_plan(plan, x, m)
+    assert np.array_equal(y, oracle_y(rp, col, val, x))
+    assert not y[:100_000].any() and not y[4_000_000:4_040_000].any()
+
+
 @pytest.mark.parametrize("opts", [{}, {"bin_strip_cols": 3001}, {"bin_groups": 3}])
 def test_bin_device_build(opts, monkeypatch):
     """spmv_plan_create_csr_device with BIN: the segments are counted, laid
