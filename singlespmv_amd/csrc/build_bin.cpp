@@ -93,10 +93,13 @@ static int bin_params(spmv_plan_s *p, const spmv_options_t &o, int64_t m, int64_
     // N = 4: 1.00 -> 0.97-1.00; N = 2 and config 2 stay faster with 4,
     // profiles/round1/probe/bin_sum_waves_wide.jsonl).  Since the Sum's
     // unclamped batches and one-cursor walk (round 2) the 2-wave Sum costs
-    // less, and segments below 128 entries take it too: config 3 (92 at 4
+    // less, and segments below 256 entries take it too: config 3 (92 at 4
     // waves) 0.166-0.177 -> 0.161-0.165 ms, rank 0 of the 2-GPU job (84)
-    // 0.880-0.912 -> 0.833-0.835 ms, both then with 128-B lines; config 2
-    // (167) stays at 4 (profiles/round2/probe/sum_waves_pad*_*.jsonl)
+    // 0.880-0.912 -> 0.833-0.835 ms, both then with 128-B lines
+    // (profiles/round2/probe/sum_waves_pad*_*.jsonl); config 2 (167): four
+    // plans each, 0.8235-0.8323 (mean 0.830) -> 0.811-0.834 ms (mean 0.824),
+    // Mul 0.536-0.542 -> 0.519-0.536, Sum 0.296 -> 0.298-0.307
+    // (sum_waves_c2_4plans.jsonl)
     {
         const int64_t S0 = std::max<int64_t>(1, (n + C - 1) / C);
         auto seg_for = [&](int w) {
@@ -104,7 +107,7 @@ static int bin_params(spmv_plan_s *p, const spmv_options_t &o, int64_t m, int64_
             return (double)nnz / ((double)S0 * (double)NB0);
         };
         double seg = seg_for(4);
-        if (seg < 128.0) {
+        if (seg < 256.0) {
             B.sum_waves = 2;
             seg = seg_for(2);
         }

@@ -1,0 +1,13 @@
+#!/bin/bash
+# after 2 Sum waves below 256-entry segments (config 2 included): full GPU
+# suite, smoke, config 2/3 bench lines, final profiles
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out/r2_final4
+mkdir -p $O
+cd $R
+timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || exit $?
+timeout -k 10 120 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit $?
+timeout -k 10 400 python3 -u bench.py --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err || exit $?
+timeout -k 10 400 python3 -u bench.py --config c3 > $O/bench_c3.json 2> $O/bench_c3.err || exit $?
+bash tools/r2_prof_final.sh || exit $?
