@@ -12,18 +12,20 @@
 //    Mul-ordered entry stream strip by strip.  Per strip it stages the
 //    x strip (<= kBinMaxStrip columns) in LDS, then every entry gathers x from LDS and
 //    writes its product to the product buffer at the entry's place in Sum
-//    order.  The entry stream is ordered [strip][bin][row, col] and padded per
-//    (strip, bin) segment to 8 entries, so 8 consecutive lanes write one
-//    aligned 64-byte product line;
-//  * Sum (bin_sum_kernel): one wave per bin (<= kBinMaxRows rows) streams the
-//    bin's products -- contiguous, ordered [strip][row, col] -- and adds them
-//    with ds_add_f64 into its own LDS y slice, then writes the bin's y rows.
+//    order.  The entry stream is ordered [strip][bin][k-th entry, row] and
+//    padded per (strip, bin) segment to 16 entries (8 when segments are
+//    short), so 16 (8) consecutive lanes write one aligned 128-byte (64-byte)
+//    product line;
+//  * Sum (bin_sum_kernel): one wave per bin (<= bin_max_rows(W2) rows)
+//    streams the bin's products -- contiguous, ordered [strip][k, row] -- and
+//    adds them with ds_add_f64 into its own LDS y slice, then writes the
+//    bin's y rows; each wave walks all of its bins with one batch cursor.
 //
-// HBM bytes per nnz: Mul 8 (val) + 2 (column in strip) + 0.5 (destination)
-// + 8 (product), Sum 8 (product) + 2 (row in bin): ~28.5 B, streamed and
-// fully coalesced, against 12 B + an uncoalesced gather for row-parallel
-// kernels.  With row groups (G > 1) the product buffer is re-used by every
-// group so its write/read round trip can stay in the 256 MB Infinity Cache.
+// HBM bytes per nnz: Mul 8 (val) + 2 (column in strip) + 0.25-0.5
+// (destination) + 8 (product), Sum 8 (product) + 2 (row in bin): ~28.5 B,
+// streamed and fully coalesced, against 12 B + an uncoalesced gather for
+// row-parallel kernels (the Infinity Cache gives the product
+// round trip no re-read benefit, so row groups (G > 1) only bound the buffer).
 //
 // Determinism / exactness: a bin is owned by one wave, which adds its
 // products in Sum order = column order within each row (strips ascending,
