@@ -71,16 +71,28 @@ def streamed_bytes(info) -> dict:
             "mul_read": mul_read, "mul_write": mul_write, "sum_read": sum_read, "sum_write": sum_write}
 
 
-def bin_ceiling(model: dict, read_gbs: float, write_gbs: float, nnz: int) -> dict:
+def bin_ceiling(model: dict, read_gbs: float, write_gbs: float, mixed_gbs: float, nnz: int) -> dict:
     """BIN's own floor: its streamed bytes (not the 12 B/nnz roofline) moved at
-    the measured STREAM read / write ceilings of this GPU, Mul then Sum."""
+    the measured ceilings of this GPU, Mul then Sum -- everything at the
+    STREAM-read rate (`implied_ms`), and the Mul's reads + writes at the
+    measured mixed read/write rate with the Sum at the read rate
+    (`implied_ms_mixed`, the tighter one: HBM turns writes around slower)."""
     ms = model["total"] / read_gbs / 1e6
     ms_rw = ((model["mul_read"] + model["sum_read"]) / read_gbs + (model["mul_write"] + model["sum_write"]) / write_gbs) / 1e6
+    ms_mixed = (model["mul"] / mixed_gbs + model["sum"] / read_gbs) / 1e6
     return {"model": "BIN streamed bytes (Mul 8+2+0.25 B read + 8 B write, Sum 8+2 B read per stored entry, "
-                     "x strips, y), all moved at the measured STREAM-read ceiling",
-            "bytes": model["total"], "read_gbs": read_gbs, "write_gbs": write_gbs,
+                     "x strips, y), all moved at the measured STREAM-read ceiling; _mixed: the Mul at the "
+                     "measured mixed read+write ceiling (3/4 written back), the Sum at the read ceiling",
+            "bytes": model["total"], "read_gbs": read_gbs, "write_gbs": write_gbs, "mixed_gbs": mixed_gbs,
             "implied_ms": ms, "implied_gflops": 2.0 * nnz / (ms * 1e-3) / 1e9,
-            "implied_ms_separate_write": ms_rw}
+            "implied_ms_separate_write": ms_rw, "implied_ms_mixed": ms_mixed}
+
+
+def _bin_ceiling_line(model, read_gbs, write_gbs, mixed_gbs, nnz, launch_ms) -> dict:
+    c = bin_ceiling(model, read_gbs, write_gbs, mixed_gbs, nnz)
+    c["frac_of_ceiling"] = c["implied_ms"] / launch_ms
+    c["frac_of_ceiling_mixed"] = c["implied_ms_mixed"] / launch_ms
+    return c
 
 
 def cpu_model() -> str:
@@ -413,6 +425,7 @@ def main():
     # measured STREAM-read ceiling of this GPU (reported beside the spec peak)
     stream_gbs = sp.stream_probe(local, 2 << 30, 10)
     stream_write_gbs = sp.stream_write_probe(local, 2 << 30, 10)
+    mixed_gbs = sp.mixed_probe(local, 1792 << 20, 3, 10)
     # and the measured ceiling of random 8-byte x gathers that hit L2: every
     # format here issues one x gather per nnz, so this bounds the gather side
     gather_gps = sp.gather_probe(local, 64 << 20, 1 << 20)
@@ -469,16 +482,15 @@ def main():
                      "kernel": r["kernel"], "algo_bytes_per_launch": r["algo_bytes"],
                      "launch_ms": r["event_ms_per_launch"],
                      "stream_ceiling_gbs": stream_gbs, "frac_of_stream": achieved / stream_gbs,
-                     "stream_write_gbs": stream_write_gbs,
+                     "stream_write_gbs": stream_write_gbs, "mixed_rw_gbs": mixed_gbs,
                      **gather_fields,
                      "csr5_model_gbs": csr5_bytes / (r["event_ms_per_launch"] * 1e-3) / 1e9},
         "cpu_baseline": cpu,
         "streamed_bytes_model": streamed_bytes(info) if info["format"] == "bin" else None,
         # BIN's own byte floor: what this format could do on this GPU at best;
         # the headline's launch time over it is how close the kernels are
-        "ceiling": (dict(bin_ceiling(streamed_bytes(info), stream_gbs, stream_write_gbs, nnz_local),
-                         frac_of_ceiling=bin_ceiling(streamed_bytes(info), stream_gbs, stream_write_gbs,
-                                                     nnz_local)["implied_ms"] / r["event_ms_per_launch"])
+        "ceiling": (_bin_ceiling_line(streamed_bytes(info), stream_gbs, stream_write_gbs, mixed_gbs, nnz_local,
+                                      r["event_ms_per_launch"])
                     if info["format"] == "bin" else None),
         "formats": results,
         "gen_s": round(t_gen, 2),

@@ -186,6 +186,12 @@ int spmv_stream_probe(int32_t device, int64_t bytes, int32_t iters, double *read
  * stores over a `bytes` buffer, `iters` launches timed with events. */
 int spmv_stream_write_probe(int32_t device, int64_t bytes, int32_t iters, double *write_gbs);
 
+/* Measured mixed read + write ceiling of `device` (GB/s of reads + writes): a
+ * grid-stride stream reading `bytes` (16-byte loads) and writing
+ * write_quarters/4 of them back (nontemporal 16-byte stores); BIN's Mul moves
+ * about 3 quarters. */
+int spmv_mixed_probe(int32_t device, int64_t bytes, int32_t write_quarters, int32_t iters, double *gbs);
+
 /* Measured ceiling of random 8-byte gathers (gathers/s): n streamed int32
  * indices into a `table_bytes` table (1 MB: L2-resident, the best case of a
  * gather-bound SpMV), 8 gathers in flight per lane, best of 5 launches. */

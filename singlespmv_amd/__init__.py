@@ -103,6 +103,7 @@ EXPORTS = [
     "spmv_gen_fill", "spmv_gen_vector", "spmv_partition_rows", "spmv_save_csr_bin",
     "spmv_load_csr_bin", "spmv_lds_order_probe", "spmv_dist_layout", "spmv_dist_create_csr",
     "spmv_dist_execute", "spmv_dist_time", "spmv_dist_info", "spmv_dist_destroy", "spmv_stream_write_probe",
+    "spmv_mixed_probe",
 ]
 
 _lib = None
@@ -133,6 +134,7 @@ def lib():
     L.spmv_profile.argtypes = [vp, vp, vp, i32, C.POINTER(f64), i32, C.POINTER(i32)]
     L.spmv_stream_probe.argtypes = [i32, i64, i32, C.POINTER(f64)]
     L.spmv_stream_write_probe.argtypes = [i32, i64, i32, C.POINTER(f64)]
+    L.spmv_mixed_probe.argtypes = [i32, i64, i32, i32, C.POINTER(f64)]
     L.spmv_gather_probe.argtypes = [i32, i64, i64, C.POINTER(f64)]
     L.spmv_lds_order_probe.argtypes = [i32, i32, _I32P, _F64P, _F64P]
     L.spmv_dist_layout.argtypes = [_I64P, i64, i32, _I64P, C.POINTER(i64)]
@@ -305,6 +307,14 @@ def stream_write_probe(device: int = 0, bytes_: int = 2 << 30, iters: int = 10) 
     """Measured STREAM-write GB/s of the device (nontemporal 16-B stores)."""
     g = C.c_double()
     _check(lib().spmv_stream_write_probe(device, bytes_, iters, C.byref(g)), "spmv_stream_write_probe")
+    return g.value
+
+
+def mixed_probe(device: int = 0, bytes_: int = 1792 << 20, write_quarters: int = 3, iters: int = 10) -> float:
+    """Measured GB/s of reads + writes when a stream writes back
+    write_quarters/4 of what it reads (BIN's Mul: about 3/4)."""
+    g = C.c_double()
+    _check(lib().spmv_mixed_probe(device, bytes_, write_quarters, iters, C.byref(g)), "spmv_mixed_probe")
     return g.value
 
 

@@ -79,6 +79,33 @@ __global__ __launch_bounds__(256) void stream_write_kernel(f64x2 *__restrict__ a
         __builtin_nontemporal_store(f64x2{1.0, (double)i}, a + i);
 }
 
+// Mixed read + write ceiling: every thread reads 4 vectors (16-B loads) and
+// writes WQ of them back (nontemporal 16-B stores), grid-stride -- BIN's Mul
+// moves reads and writes in about that ratio (1.71 GB in, 1.31 GB out at
+// config 2: WQ = 3).  The loads not stored are kept live through a sink.
+template <int WQ>
+__global__ __launch_bounds__(256) void mixed_rw_kernel(const f64x2 *__restrict__ a, f64x2 *__restrict__ b,
+                                                       int64_t n2, double *__restrict__ sink) {
+    const int64_t G = (int64_t)gridDim.x * blockDim.x;
+    double acc = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n2; i += G * 4) {
+        f64x2 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int64_t j = i + u * G;
+            v[u] = j < n2 ? __builtin_nontemporal_load(a + j) : f64x2{0.0, 0.0};
+        }
+#pragma unroll
+        for (int u = WQ; u < 4; ++u) acc += v[u].x + v[u].y;
+#pragma unroll
+        for (int u = 0; u < WQ; ++u) {
+            const int64_t j = i + u * G;
+            if (j < n2) __builtin_nontemporal_store(v[u], b + j);
+        }
+    }
+    if (acc == 12345.678) *sink = acc;
+}
+
 // Scattered-line write probe (placement experiments, tools/placement_probe.py):
 // every 128-byte line of a window is written once, 16 lanes per line with
 // nontemporal stores (the BIN Mul's product-write shape), lines visited in
@@ -324,5 +351,62 @@ extern "C" int spmv_stream_write_probe(int32_t device, int64_t bytes, int32_t it
         return SPMV_ERROR_HIP;
     }
     *write_gbs = (double)n2 * 16 * iters / (ms * 1e-3) / 1e9;
+    return SPMV_SUCCESS;
+}
+
+extern "C" int spmv_mixed_probe(int32_t device, int64_t bytes, int32_t write_quarters, int32_t iters, double *gbs) {
+    using namespace spmv;
+    SPMV_CHECK_ARG(gbs != nullptr && bytes >= (1 << 20) && iters > 0 && write_quarters >= 0 && write_quarters <= 4,
+                   "bad arguments");
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count == 0) {
+        (void)hipGetLastError();
+        set_error("no HIP device visible");
+        return SPMV_ERROR_NO_DEVICE;
+    }
+    SPMV_CHECK_ARG(device >= 0 && device < count, "device ordinal out of range");
+    SPMV_HIP_TRY(hipSetDevice(device));
+    const int64_t n2 = bytes / 16;
+    f64x2 *a = nullptr, *b = nullptr;
+    double *sink = nullptr;
+    SPMV_HIP_TRY(hipMalloc(&a, (size_t)n2 * 16));
+    if (hipMalloc(&b, (size_t)n2 * 16) != hipSuccess || hipMalloc(&sink, 64) != hipSuccess) {
+        (void)hipGetLastError();
+        (void)hipFree(a);
+        (void)hipFree(b);
+        set_error("mixed probe: out of device memory");
+        return SPMV_ERROR_OUT_OF_MEMORY;
+    }
+    (void)hipMemset(a, 0, (size_t)n2 * 16);
+    const unsigned blocks = 256 * 32;
+    auto launch = [&] {
+        switch (write_quarters) {
+            case 0: hipLaunchKernelGGL(mixed_rw_kernel<0>, dim3(blocks), dim3(256), 0, 0, a, b, n2, sink); break;
+            case 1: hipLaunchKernelGGL(mixed_rw_kernel<1>, dim3(blocks), dim3(256), 0, 0, a, b, n2, sink); break;
+            case 2: hipLaunchKernelGGL(mixed_rw_kernel<2>, dim3(blocks), dim3(256), 0, 0, a, b, n2, sink); break;
+            case 3: hipLaunchKernelGGL(mixed_rw_kernel<3>, dim3(blocks), dim3(256), 0, 0, a, b, n2, sink); break;
+            default: hipLaunchKernelGGL(mixed_rw_kernel<4>, dim3(blocks), dim3(256), 0, 0, a, b, n2, sink);
+        }
+    };
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    launch();  // warm-up
+    (void)hipEventRecord(e0, 0);
+    for (int i = 0; i < iters; ++i) launch();
+    (void)hipEventRecord(e1, 0);
+    const hipError_t e = hipEventSynchronize(e1);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    (void)hipFree(a);
+    (void)hipFree(b);
+    (void)hipFree(sink);
+    if (e != hipSuccess) {
+        set_error(std::string("mixed probe: ") + hipGetErrorString(e));
+        return SPMV_ERROR_HIP;
+    }
+    *gbs = (double)n2 * 16 * (1.0 + write_quarters / 4.0) * iters / (ms * 1e-3) / 1e9;
     return SPMV_SUCCESS;
 }
