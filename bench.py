@@ -425,7 +425,7 @@ def main():
     # measured STREAM-read ceiling of this GPU (reported beside the spec peak)
     stream_gbs = sp.stream_probe(local, 2 << 30, 10)
     stream_write_gbs = sp.stream_write_probe(local, 2 << 30, 10)
-    mixed_gbs = sp.mixed_probe(local, 1792 << 20, 3, 10)
+    mixed_gbs = sp.mixed_probe(local, 1792 << 20, 3, 20)
     # and the measured ceiling of random 8-byte x gathers that hit L2: every
     # format here issues one x gather per nnz, so this bounds the gather side
     gather_gps = sp.gather_probe(local, 64 << 20, 1 << 20)

@@ -188,8 +188,8 @@ int spmv_stream_write_probe(int32_t device, int64_t bytes, int32_t iters, double
 
 /* Measured mixed read + write ceiling of `device` (GB/s of reads + writes): a
  * grid-stride stream reading `bytes` (16-byte loads) and writing
- * write_quarters/4 of them back (nontemporal 16-byte stores); BIN's Mul moves
- * about 3 quarters. */
+ * write_quarters/4 of them back (nontemporal 16-byte stores), the fastest of
+ * `iters` launches; BIN's Mul moves about 3 quarters. */
 int spmv_mixed_probe(int32_t device, int64_t bytes, int32_t write_quarters, int32_t iters, double *gbs);
 
 /* Measured ceiling of random 8-byte gathers (gathers/s): n streamed int32

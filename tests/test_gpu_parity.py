@@ -984,3 +984,16 @@ def test_bin_refuses_huge_sparse_grid_and_auto_avoids_it():
     col2 = np.sort(rng.integers(0, n2, size=(m2, per2)), axis=1).astype(np.int32).ravel()
     plan = sp.Plan.from_csr(m2, n2, rp2, col2, rng.random(per2 * m2), "auto")
     assert plan.info()["format"] != "bin"
+
+
+def test_bandwidth_probes_report_plausible_rates():
+    """The live ceilings bench.py prices its roofline fields with: STREAM
+    read, nontemporal write, mixed read+write (3/4 written back) -- each a
+    positive rate below the 8 TB/s HBM spec; argument errors are refused."""
+    r = sp.stream_probe(0, 512 << 20, 3)
+    w = sp.stream_write_probe(0, 512 << 20, 3)
+    m = sp.mixed_probe(0, 512 << 20, 3, 3)
+    for v in (r, w, m):
+        assert 500.0 < v < 8000.0, (r, w, m)
+    with pytest.raises(sp.SpmvError):
+        sp.mixed_probe(0, 512 << 20, 5, 3)
