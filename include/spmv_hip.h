@@ -234,6 +234,28 @@ int spmv_set_stream(spmv_plan_t plan, void *hip_stream);
 int spmv_time(spmv_plan_t plan, const double *x_dev, double *y_dev, int32_t iters,
               double *ms);
 
+/* ---- HIP graph of the device-resident execute -----------------------------
+ * The plan's launch sequence for (x_dev -> y_dev), captured `reps` times in a
+ * row into one hipGraph (stream capture on a private stream) and
+ * instantiated.  spmv_graph_launch enqueues all reps x n_kernels kernels on
+ * the plan's current stream with one submission -- the per-call launch cost
+ * that dominates small matrices, whose kernels are shorter than their
+ * launches (the reference driver repeats SpMV until >= 1 s,
+ * src/main.cpp:58-102).  Each rep computes exactly what spmv_execute does
+ * (y bit-identical); x_dev and y_dev are fixed in the graph, so the caller
+ * keeps them allocated until spmv_graph_destroy.  CSS plans (whose sweep
+ * tags its progress flags with a per-launch sequence number) return
+ * SPMV_ERROR_NOT_SUPPORTED. */
+typedef struct spmv_graph_s *spmv_graph_t;
+int spmv_graph_create(spmv_plan_t plan, const double *x_dev, double *y_dev, int32_t reps,
+                      spmv_graph_t *graph);
+/* flags: SPMV_ASYNC = return without synchronising the stream */
+int spmv_graph_launch(spmv_graph_t graph, uint32_t flags);
+/* `launches` back-to-back graph launches between two hipEvents on the plan's
+ * stream; *ms = elapsed milliseconds total (launches x reps executes). */
+int spmv_graph_time(spmv_graph_t graph, int32_t launches, double *ms);
+int spmv_graph_destroy(spmv_graph_t graph);
+
 typedef struct spmv_plan_info {
     int32_t format;          /* resolved spmv_format_t                         */
     int32_t device;

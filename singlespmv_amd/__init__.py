@@ -103,7 +103,7 @@ EXPORTS = [
     "spmv_gen_fill", "spmv_gen_vector", "spmv_partition_rows", "spmv_save_csr_bin",
     "spmv_load_csr_bin", "spmv_lds_order_probe", "spmv_dist_layout", "spmv_dist_create_csr",
     "spmv_dist_execute", "spmv_dist_time", "spmv_dist_info", "spmv_dist_destroy", "spmv_stream_write_probe",
-    "spmv_mixed_probe",
+    "spmv_mixed_probe", "spmv_graph_create", "spmv_graph_launch", "spmv_graph_time", "spmv_graph_destroy",
 ]
 
 _lib = None
@@ -131,6 +131,10 @@ def lib():
     L.spmv_plan_create_csr32_device.argtypes = [i32, i32, i32, vp, vp, vp, C.POINTER(Options), C.POINTER(vp)]
     L.spmv_set_stream.argtypes = [vp, vp]
     L.spmv_time.argtypes = [vp, vp, vp, i32, C.POINTER(f64)]
+    L.spmv_graph_create.argtypes = [vp, vp, vp, i32, C.POINTER(vp)]
+    L.spmv_graph_launch.argtypes = [vp, C.c_uint32]
+    L.spmv_graph_time.argtypes = [vp, i32, C.POINTER(f64)]
+    L.spmv_graph_destroy.argtypes = [vp]
     L.spmv_profile.argtypes = [vp, vp, vp, i32, C.POINTER(f64), i32, C.POINTER(i32)]
     L.spmv_stream_probe.argtypes = [i32, i64, i32, C.POINTER(f64)]
     L.spmv_stream_write_probe.argtypes = [i32, i64, i32, C.POINTER(f64)]
@@ -396,6 +400,35 @@ def _check_vec(a, length: int, name: str, device: int, writable: bool) -> None:
     raise ValueError(f"{name} must be a numpy array or a torch tensor (raw addresses: use the C-ABI)")
 
 
+class Graph:
+    """An instantiated HIP graph of `reps` executes of one plan (spmv_graph_*)."""
+
+    def __init__(self, handle: int, plan, keep, reps: int):
+        self._h = C.c_void_p(handle)
+        self._plan, self._keep, self.reps = plan, keep, reps
+
+    def launch(self, async_: bool = False) -> None:
+        _check(lib().spmv_graph_launch(self._h, ASYNC if async_ else 0), "spmv_graph_launch")
+
+    def time(self, launches: int) -> float:
+        """Milliseconds for `launches` back-to-back graph launches (launches x
+        reps executes), HIP events on the plan's stream."""
+        ms = C.c_double()
+        _check(lib().spmv_graph_time(self._h, launches, C.byref(ms)), "spmv_graph_time")
+        return ms.value
+
+    def destroy(self) -> None:
+        if self._h is not None and self._h.value:
+            lib().spmv_graph_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.destroy()
+        except Exception:
+            pass
+
+
 class Plan:
     """A device-resident matrix in one format (the SpMatOpt of a plugin)."""
 
@@ -490,6 +523,17 @@ class Plan:
         ms = C.c_double()
         _check(lib().spmv_time(self._h, _ptr(x_dev), _ptr(y_dev), iters, C.byref(ms)), "spmv_time")
         return ms.value
+
+    def graph(self, x_dev, y_dev, reps: int = 1) -> "Graph":
+        """The device-resident execute x_dev -> y_dev captured `reps` times
+        into one HIP graph (spmv_graph_create); keep x_dev / y_dev alive."""
+        self._check_xy(x_dev, y_dev)
+        if not (_is_device(x_dev) or self.n == 0) or not (_is_device(y_dev) or self.m == 0):
+            raise ValueError("graph() needs device tensors for x and y")
+        h = C.c_void_p()
+        _check(lib().spmv_graph_create(self._h, _ptr(x_dev), _ptr(y_dev), reps, C.byref(h)),
+               "spmv_graph_create")
+        return Graph(h.value, self, (x_dev, y_dev), reps)
 
     def profile(self, x_dev, y_dev, iters: int = 10) -> dict:
         """Mean ms per phase of one execute ({"tile": .., "fixup": ..} for SS),

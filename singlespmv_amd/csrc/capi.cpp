@@ -385,6 +385,127 @@ int spmv_time(spmv_plan_t p, const double *x_dev, double *y_dev, int32_t iters, 
     return st;
 }
 
+}  // extern "C"
+
+struct spmv_graph_s {
+    spmv_plan_t plan = nullptr;
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t exec = nullptr;
+    int32_t reps = 0;
+};
+
+namespace spmv {
+
+// Capture `reps` dispatches on a private stream (the plan's stream may be the
+// null stream, which cannot be captured); the plan's stream is restored
+// whatever happens.
+static int graph_capture(spmv_plan_s *p, const double *x, double *y, int32_t reps, hipGraph_t *out) {
+    hipStream_t cs = nullptr;
+    SPMV_HIP_TRY(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+    const hipStream_t saved = p->stream;
+    const int saved_prof = p->prof_k;
+    p->stream = cs;
+    p->prof_k = -1;  // no profile events inside the graph
+    int st = SPMV_SUCCESS;
+    hipError_t e = hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal);
+    if (e == hipSuccess) {
+        for (int32_t r = 0; r < reps && st == SPMV_SUCCESS; ++r) st = dispatch(p, x, y);
+        hipGraph_t g = nullptr;
+        const hipError_t e2 = hipStreamEndCapture(cs, &g);
+        if (st == SPMV_SUCCESS && e2 != hipSuccess) e = e2;
+        if (st == SPMV_SUCCESS && e == hipSuccess) *out = g;
+        else if (g) (void)hipGraphDestroy(g);
+    }
+    p->stream = saved;
+    p->prof_k = saved_prof;
+    (void)hipStreamDestroy(cs);
+    if (st != SPMV_SUCCESS) return st;
+    if (e != hipSuccess) {
+        set_error(std::string("graph capture: ") + hipGetErrorString(e));
+        (void)hipGetLastError();
+        return SPMV_ERROR_HIP;
+    }
+    return SPMV_SUCCESS;
+}
+
+}  // namespace spmv
+
+extern "C" {
+
+int spmv_graph_create(spmv_plan_t p, const double *x_dev, double *y_dev, int32_t reps, spmv_graph_t *out) {
+    SPMV_CHECK_ARG(out != nullptr, "graph out-pointer is NULL");
+    *out = nullptr;
+    SPMV_CHECK_ARG(p != nullptr && reps > 0, "bad arguments");
+    SPMV_CHECK_ARG((x_dev != nullptr || p->n == 0) && (y_dev != nullptr || p->m == 0), "x or y is NULL");
+    if (p->format == SPMV_FORMAT_CSS) {
+        // the sweep's progress flags are tagged with a per-launch sequence
+        // number passed as a kernel argument: a replayed graph would repeat it
+        set_error("spmv_graph_create: CSS plans cannot be replayed from a graph");
+        return SPMV_ERROR_NOT_SUPPORTED;
+    }
+    SPMV_RETURN_IF(bind_device(p));
+    hipGraph_t g = nullptr;
+    SPMV_RETURN_IF(graph_capture(p, x_dev, y_dev, reps, &g));
+    hipGraphExec_t ex = nullptr;
+    const hipError_t e = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
+    if (e != hipSuccess) {
+        (void)hipGraphDestroy(g);
+        set_error(std::string("hipGraphInstantiate: ") + hipGetErrorString(e));
+        (void)hipGetLastError();
+        return SPMV_ERROR_HIP;
+    }
+    spmv_graph_s *G = new (std::nothrow) spmv_graph_s;
+    if (!G) {
+        (void)hipGraphExecDestroy(ex);
+        (void)hipGraphDestroy(g);
+        set_error("host allocation of the graph failed");
+        return SPMV_ERROR_OUT_OF_MEMORY;
+    }
+    G->plan = p;
+    G->graph = g;
+    G->exec = ex;
+    G->reps = reps;
+    *out = G;
+    return SPMV_SUCCESS;
+}
+
+int spmv_graph_launch(spmv_graph_t G, uint32_t flags) {
+    SPMV_CHECK_ARG(G != nullptr && G->exec != nullptr, "graph is NULL");
+    SPMV_RETURN_IF(bind_device(G->plan));
+    SPMV_HIP_TRY(hipGraphLaunch(G->exec, G->plan->stream));
+    if (!(flags & SPMV_ASYNC)) SPMV_HIP_TRY(hipStreamSynchronize(G->plan->stream));
+    return SPMV_SUCCESS;
+}
+
+int spmv_graph_time(spmv_graph_t G, int32_t launches, double *ms) {
+    SPMV_CHECK_ARG(G != nullptr && G->exec != nullptr && ms != nullptr && launches > 0, "bad arguments");
+    SPMV_RETURN_IF(bind_device(G->plan));
+    const hipStream_t s = G->plan->stream;
+    hipEvent_t a, b;
+    SPMV_HIP_TRY(hipEventCreate(&a));
+    SPMV_HIP_TRY(hipEventCreate(&b));
+    hipError_t e = hipEventRecord(a, s);
+    for (int32_t i = 0; i < launches && e == hipSuccess; ++i) e = hipGraphLaunch(G->exec, s);
+    if (e == hipSuccess) e = hipEventRecord(b, s);
+    if (e == hipSuccess) e = hipEventSynchronize(b);
+    float f = 0;
+    if (e == hipSuccess) e = hipEventElapsedTime(&f, a, b);
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    SPMV_HIP_TRY(e);
+    *ms = f;
+    return SPMV_SUCCESS;
+}
+
+int spmv_graph_destroy(spmv_graph_t G) {
+    if (!G) return SPMV_SUCCESS;
+    if (G->plan) (void)bind_device(G->plan);
+    if (G->exec) (void)hipGraphExecDestroy(G->exec);
+    if (G->graph) (void)hipGraphDestroy(G->graph);
+    delete G;
+    return SPMV_SUCCESS;
+}
+
 static const char *const kPhases[][3] = {
     {"", "", ""},           {"csr", "", ""},   {"ell", "", ""},     {"tile", "fixup", ""},
     {"dia", "", ""},        {"ell", "overflow", ""}, {"sweep", "", ""}, {"zero_y", "segment", ""},

@@ -997,3 +997,46 @@ def test_bandwidth_probes_report_plausible_rates():
         assert 500.0 < v < 8000.0, (r, w, m)
     with pytest.raises(sp.SpmvError):
         sp.mixed_probe(0, 512 << 20, 5, 3)
+
+
+@pytest.mark.parametrize("fmt", ["csr", "ell", "ss", "hyb", "dia", "coo", "jds", "bin"])
+def test_graph_replays_the_execute(fmt):
+    """spmv_graph_*: reps executes captured in one HIP graph give the
+    spmv_execute y bit for bit on every launch (COO: its f64 atomics, 1e-12),
+    on the null stream and on a side stream; CSS is refused."""
+    import torch
+    m = 60_013
+    if fmt == "dia":
+        rp, col, val = sp.generate_csr(sp.gen_spec("banded", m, band_lo=-5, band_hi=6, seed=4))
+    else:
+        rp, col, val = _bin_matrix("powerlaw" if fmt in ("hyb", "jds", "ss") else "uniform", m, m, 4)
+    x = sp.generate_vector(m, seed=5)
+    plan = sp.Plan.from_csr(m, m, rp, col, val, fmt)
+    xd = torch.from_numpy(x).cuda()
+    ye = torch.full((m,), float("nan"), dtype=torch.float64, device="cuda")
+    plan.execute(xd, ye)
+    torch.cuda.synchronize()
+    y_exec = ye.cpu().numpy()
+    if fmt == "bin":
+        assert_bin_rows(plan, y_exec, rp, col, val, x, "exec")
+    else:
+        check_close(y_exec, oracle_y(rp, col, val, x), what=fmt)
+    yg = torch.full((m,), float("nan"), dtype=torch.float64, device="cuda")
+    g = plan.graph(xd, yg, reps=3)
+    for stream in (None, torch.cuda.Stream()):
+        plan.set_stream(stream)
+        for _ in range(2):
+            yg.fill_(float("nan"))
+            torch.cuda.synchronize()
+            g.launch()
+            y = yg.cpu().numpy()
+            if fmt == "coo":
+                check_close(y, y_exec, what="coo graph")
+            else:
+                assert np.array_equal(y, y_exec), f"{fmt}: graph y differs from execute"
+        assert g.time(2) > 0
+    plan.set_stream(None)
+    g.destroy()
+    css = sp.Plan.from_csr(m, m, rp, col, val, "css")
+    with pytest.raises(sp.SpmvError, match="not supported"):
+        css.graph(xd, yg)
