@@ -230,11 +230,17 @@ static int bin_rows(spmv_plan_s *p, const int64_t *row_ptr, int64_t m, int64_t n
     L.PAD = (int64_t)1 << B.pad_log;
     B.n_strips = L.S;
     const int64_t waves = (int64_t)B.nwg2 * B.sum_waves;
-    int64_t nb = std::max<int64_t>(1, (m + max_rows - 1) / max_rows);
-    if (nb * 2 >= waves) nb = (nb + waves - 1) / waves * waves;
     // cut on the Sum entries per row (long rows: their run pieces)
     const int64_t *cum = L.LL > 0 ? L.eff_rp.data() : row_ptr;
     const int64_t total = cum[m];
+    int64_t nb = std::max<int64_t>(1, (m + max_rows - 1) / max_rows);
+    // small matrices: more (shorter) bins than m / max_rows, up to one per
+    // Sum wave, while the expected (bin, strip) segment keeps >= 128
+    // entries -- else a few waves sum everything (100 K x 100 K, 16 / row:
+    // 20 bins for 1024 waves).  Configs 2, 3 and the rank shapes already
+    // have a bin per wave.
+    if (nb < waves) nb = std::max(nb, std::min<int64_t>(std::min<int64_t>(waves, m), total / (L.S * 128)));
+    if (nb * 2 >= waves) nb = (nb + waves - 1) / waves * waves;
     L.row0.assign(1, 0);
     for (int64_t r = 0; r < m;) {
         const int64_t b = (int64_t)L.row0.size() - 1;
