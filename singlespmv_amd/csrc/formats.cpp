@@ -1004,15 +1004,18 @@ int choose_format(const HostCsr &A, const spmv_options_t &o) {
     // crossover (profiles/round1/probe/auto_sweep.jsonl): row-parallel formats
     // win at n = 0.5 M (x = 4 MB), CSS from n = 1 M (x = 8 MB) on uniform and
     // power-law rows alike.
-    // Larger still: the binned Mul/Sum (x strips in LDS, no gathers at all)
-    // beats the column-slab sweep from ~3.5 M columns and ~20 M entries
-    // (profiles/round1/probe/bin_vs_css_sizes.jsonl: 0.50 vs 0.58 ms at
-    // 5 M x 5 M uniform, 0.25 vs 0.28 ms at config 3; CSS wins at 1-2 M), and
-    // its advantage grows with n (1.2 vs 2.6 ms at 10 M x 80 M)
+    // The binned Mul/Sum (x strips in LDS, no gathers at all) beats the
+    // column-slab sweep in that same range once it has ~8 M entries: with a
+    // Sum bin per wave on small plans (bin_rows) it runs 1 M x 1 M uniform
+    // 16 / row in 0.104 ms against CSS's 0.132, 2 M power-law (9.9 M nnz)
+    // 0.084 vs 0.122, 1 M power-law (5 M nnz) 0.059 vs 0.061
+    // (profiles/round2/bin_small/auto_cross.jsonl; round 1, with m / 5119
+    // bins, it took ~3.5 M columns, bin_vs_css_sizes.jsonl), and its
+    // advantage grows with n (1.2 vs 2.6 ms at 10 M x 80 M)
     // ... as long as its (bin, strip) segments stay long enough for the
     // 8/16-entry padding (expected segment >= 12 entries: 20 at the N = 8
     // rank shape, 128 at config 2)
-    if (A.n >= 3500000 && A.nnz >= 20000000 && mean >= 2.0) {
+    if (A.n * 8 > ((int64_t)6 << 20) && A.nnz >= 8000000 && mean >= 2.0) {
         const double bins = std::ceil((double)A.m / 5119.0), strips = std::ceil((double)A.n / 20480.0);
         if ((double)A.nnz / (bins * strips) >= 12.0 && bins * strips <= (double)(1 << 28)) return SPMV_FORMAT_BIN;
     }

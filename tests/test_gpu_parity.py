@@ -566,12 +566,13 @@ def test_csr_64bit_row_pointers(lanes):
 
 def test_auto_format_choice():
     """AUTO follows the measured crossovers (profiles/round1/probe/
-    auto_sweep.jsonl, bin_vs_css_sizes.jsonl): banded -> DIA; >= 3.5 M
-    columns and 20 M entries -> BIN; x beyond ~6 MB -> CSS; below that,
-    near-uniform rows -> CSR, skewed rows -> SS."""
+    auto_sweep.jsonl; round 2: bin_small/auto_cross.jsonl): banded -> DIA;
+    x beyond ~6 MB and >= 8 M entries -> BIN; x beyond ~6 MB, fewer
+    entries -> CSS; below that, near-uniform rows -> CSR, skewed rows -> SS."""
     cases = [(sp.gen_spec("banded", 300000, band_lo=-8, band_hi=8), "dia"),
              (sp.gen_spec("uniform", 4_000_000, per_row=6, seed=6), "bin"),
-             (sp.gen_spec("uniform", 1_000_000, per_row=8, seed=1), "css"),
+             (sp.gen_spec("uniform", 1_000_000, per_row=8, seed=1), "bin"),
+             (sp.gen_spec("uniform", 1_000_000, per_row=4, seed=1), "css"),
              (sp.gen_spec("powerlaw", 1_000_000, max_len=500, seed=2), "css"),
              (sp.gen_spec("uniform", 400_000, per_row=8, seed=3), "csr"),
              (sp.gen_spec("powerlaw", 300_000, max_len=500, seed=4), "ss")]
