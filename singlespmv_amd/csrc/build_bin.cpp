@@ -229,6 +229,14 @@ static int bin_rows(spmv_plan_s *p, const int64_t *row_ptr, int64_t m, int64_t n
     L.S = std::max<int64_t>(1, (n + B.strip - 1) / B.strip);
     L.PAD = (int64_t)1 << B.pad_log;
     B.n_strips = L.S;
+    // x strips staged with several loads in flight per thread when each Mul
+    // workgroup walks many strips (the N = 4, 8 rank shapes: 7.6 / 15 per
+    // workgroup): N = 8 shape Mul 0.738 -> 0.719 ms; with ~2 strips per
+    // workgroup (config 2) or pieces of one strip (1 M rows) the burst of x
+    // loads costs 0.4-2.4 % instead (profiles/round2/probe/xstage_ab_*.jsonl)
+    B.xburst = L.S >= 4 * (int64_t)B.nwg1 ? 1 : 0;
+    if (B.dbg & 131072) B.xburst = 0;  // probe A/B: serial staging
+    if (B.dbg & 262144) B.xburst = 1;  // probe A/B: burst staging
     const int64_t waves = (int64_t)B.nwg2 * B.sum_waves;
     // cut on the Sum entries per row (long rows: their run pieces)
     const int64_t *cum = L.LL > 0 ? L.eff_rp.data() : row_ptr;

@@ -268,6 +268,7 @@ struct BinDev {
     bool reuse = false;    // one product buffer re-used per group (Sum per group)
     int nwg1 = 0, nwg2 = 0;
     int64_t n_bins = 0, n_strips = 0, n_entries = 0;
+    int32_t xburst = 0;           // Mul: stage x strips with several loads in flight (wide shapes)
     std::vector<int64_t> g_bin;    // host [G+1]: bin range of each group
     std::vector<int64_t> g_prod;   // host [G+1]: product (= Mul entry) range of each group
     int64_t *piece_off = nullptr;  // [G*nwg1 + 1]: pieces of (group, workgroup)

@@ -176,7 +176,8 @@ __global__ __launch_bounds__(kBinMulThreads) void bin_mul_kernel(
     const int64_t *__restrict__ piece_begin, const int64_t *__restrict__ piece_end,
     const double *__restrict__ val1, const uint16_t *__restrict__ cs1, const int32_t *__restrict__ dst1,
     const double *__restrict__ x, int64_t n, int32_t strip, double *__restrict__ prod,
-    const int64_t *__restrict__ lstart, const int64_t *__restrict__ lshift, const int32_t *__restrict__ lcode) {
+    const int64_t *__restrict__ lstart, const int64_t *__restrict__ lshift, const int32_t *__restrict__ lcode,
+    int32_t xburst) {
     __shared__ double xs[kBinMaxStrip];
     constexpr int NW = kBinMulThreads / 64;
     constexpr int64_t STEP = (int64_t)NW * 64 * U;
@@ -191,7 +192,26 @@ __global__ __launch_bounds__(kBinMulThreads) void bin_mul_kernel(
         const int64_t ls = LONG ? lstart[st] : INT64_MAX, lsh = LONG ? lshift[st] : 0;
         const int cw = (int)(n - c0 < strip ? n - c0 : strip);
         __syncthreads();  // the previous strip's readers are done
-        for (int i = threadIdx.x; i < cw; i += kBinMulThreads) xs[i] = x[c0 + i];
+        // xburst (wide shapes, build_bin.cpp): XL loads in flight per thread
+        // before their LDS writes (3 round trips for a 20480-column strip
+        // instead of 20); else, and always with long rows (their run path's
+        // live registers would spill), one load per round trip
+        constexpr int XL = 8;
+        if (LONG || !xburst) {
+            for (int i = threadIdx.x; i < cw; i += kBinMulThreads) xs[i] = x[c0 + i];
+        } else for (int i0 = threadIdx.x; i0 < cw; i0 += XL * kBinMulThreads) {
+            double t[XL];
+#pragma unroll
+            for (int k = 0; k < XL; ++k) {
+                const int i = i0 + k * kBinMulThreads;
+                t[k] = i < cw ? x[c0 + i] : 0.0;
+            }
+#pragma unroll
+            for (int k = 0; k < XL; ++k) {
+                const int i = i0 + k * kBinMulThreads;
+                if (i < cw) xs[i] = t[k];
+            }
+        }
         __syncthreads();
         const int64_t first = e0 + (int64_t)w * 64 * U;
         const int64_t nit = first < e1 ? (e1 - first + STEP - 1) / STEP : 0;
@@ -441,11 +461,13 @@ static void launch_mul_t(const spmv_plan_s *p, int g, const double *x) {
     if (B.long_len > 0)
         hipLaunchKernelGGL((bin_mul_kernel<8, MODE, PL, true>), dim3((unsigned)B.nwg1), dim3(kBinMulThreads), 0,
                            p->stream, B.piece_off, (int64_t)g * B.nwg1, B.piece_strip, B.piece_begin, B.piece_end,
-                           B.val1, B.cs1, B.dst1, x, p->n, (int32_t)B.strip, B.prod, B.lstart, B.lshift, B.lcode);
+                           B.val1, B.cs1, B.dst1, x, p->n, (int32_t)B.strip, B.prod, B.lstart, B.lshift, B.lcode,
+                           B.xburst);
     else
         hipLaunchKernelGGL((bin_mul_kernel<8, MODE, PL, false>), dim3((unsigned)B.nwg1), dim3(kBinMulThreads), 0,
                            p->stream, B.piece_off, (int64_t)g * B.nwg1, B.piece_strip, B.piece_begin, B.piece_end,
-                           B.val1, B.cs1, B.dst1, x, p->n, (int32_t)B.strip, B.prod, nullptr, nullptr, nullptr);
+                           B.val1, B.cs1, B.dst1, x, p->n, (int32_t)B.strip, B.prod, nullptr, nullptr, nullptr,
+                           B.xburst);
 }
 
 template <int PL>
@@ -465,7 +487,8 @@ static void launch_mul_p(const spmv_plan_s *p, int g, const double *x) {
             break;
         default:
             // long-block partial stores: 2048 nontemporal, 4096 none (ablations);
-            // 16384: loads clamped at the piece's end (A/B)
+            // 16384: loads clamped at the piece's end (A/B); 131072 / 262144:
+            // x strips staged serially / in bursts (A/B, build_bin.cpp xburst)
             if (p->bin.dbg & 16384) launch_mul_t<65, PL>(p, g, x);
             else if (p->bin.dbg & 2048) launch_mul_t<17, PL>(p, g, x);
             else if (p->bin.dbg & 4096) launch_mul_t<33, PL>(p, g, x);
