@@ -68,6 +68,19 @@ def test_invalid_inputs_rejected_before_device():
         sp.Plan.from_csr(1, 1, np.array([0, 3], np.int64), np.array([0], np.int32), np.array([1.0]))
 
 
+def test_graph_entry_points_reject_bad_arguments():
+    """spmv_graph_*: NULL plan / graph and non-positive counts come back as
+    SPMV_ERROR_INVALID_VALUE (no device needed); destroy(NULL) is a no-op."""
+    L = sp.lib()
+    g = C.c_void_p()
+    assert L.spmv_graph_create(None, None, None, 1, C.byref(g)) == 1
+    assert g.value is None
+    assert L.spmv_graph_launch(None, 0) == 1
+    ms = C.c_double()
+    assert L.spmv_graph_time(None, 1, C.byref(ms)) == 1
+    assert L.spmv_graph_destroy(None) == 0
+
+
 def test_options_struct_layout_matches_header(tmp_path):
     """The ctypes mirrors of spmv_options_t / spmv_plan_info_t match the C
     header field for field (sizeof and every offsetof, compiled with gcc)."""
