@@ -320,7 +320,8 @@ __device__ __forceinline__ void sum_add(const SumBatch<U, MODE> &B, int64_t base
 // MODE (internal ablations): 1 nontemporal product loads (the default), 2 no LDS atomics,
 // 4 no slot loads, 32 product loads clamped at the run's end (the round-2 loads, A/B),
 // 128 no LDS zeroing / y write-back, 256 one bin at a time (A/B: the loads of a
-// bin's first batch wait for the previous bin's y write-back).  W2 waves per
+// bin's first batch wait for the previous bin's y write-back), 512 nontemporal
+// y stores (the default, with 1; y is not re-read by the kernel).  W2 waves per
 // workgroup, each owning a slice of kBinLdsDoubles / W2 doubles.  A bin's
 // products are NBK runs (one per strip block, run_off[blk*nbins + b]); the
 // batches walk them in order (a batch never crosses a run), ping-ponged so one
@@ -415,13 +416,19 @@ __global__ __launch_bounds__(64 * W2) void bin_sum_kernel(
         auto write_zero = [&](int64_t bz) {
             const int64_t r0 = bin_row0[bz];
             const int rows = (int)(bin_row0[bz + 1] - r0);
-            for (int i = lane; i < rows; i += 64) y[r0 + i] = 0.0;
+            for (int i = lane; i < rows; i += 64) {
+                if constexpr ((MODE & 512) != 0) __builtin_nontemporal_store(0.0, y + r0 + i);
+                else y[r0 + i] = 0.0;
+            }
         };
         auto finish = [&]() {  // the slice's bin: LDS adds done -> y
             const int64_t r0 = bin_row0[acc];
             const int rows = (int)(bin_row0[acc + 1] - r0);
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            for (int i = lane; i < rows; i += 64) y[r0 + i] = ys[i];
+            for (int i = lane; i < rows; i += 64) {
+                if constexpr ((MODE & 512) != 0) __builtin_nontemporal_store(ys[i], y + r0 + i);
+                else y[r0 + i] = ys[i];
+            }
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             done = acc + bstride;
         };
@@ -518,7 +525,9 @@ static void launch_sum_w(const spmv_plan_s *p, int g, double *y) {
 #ifndef SPMV_PROBES
     // nontemporal product loads (config 2 Sum 0.308 -> 0.298 ms, neutral at
     // config 3 and the N = 8 shape, profiles/round1/probe/bin_sum_nt_loads.jsonl)
-    launch_sum_t<W2, U, 1>(p, g, y);
+    // and nontemporal y stores (config 2 Sum 0.302 -> 0.292 ms, N = 8 shape
+    // 0.318 -> 0.308, config 3 -0.5 %, profiles/round2/probe/sum_nt_y_*.jsonl)
+    launch_sum_t<W2, U, 1 | 512>(p, g, y);
 #else
     // probe build: SPMV_BIN_DEBUG bits 2-3 -> Sum MODE
     if (p->bin.dbg & 512) {  // ablation: no slot loads
@@ -537,6 +546,10 @@ static void launch_sum_w(const spmv_plan_s *p, int g, double *y) {
         launch_sum_t<W2, U, 129>(p, g, y);
         return;
     }
+    if (p->bin.dbg & 524288) {  // A/B: ordinary y stores (the default's are nontemporal)
+        launch_sum_t<W2, U, 1>(p, g, y);
+        return;
+    }
     if (p->bin.dbg & 65536) {  // A/B: one bin at a time
         launch_sum_t<W2, U, 257>(p, g, y);
         return;
@@ -551,7 +564,7 @@ static void launch_sum_w(const spmv_plan_s *p, int g, double *y) {
     switch ((p->bin.dbg >> 2) & 3) {
         case 1: launch_sum_t<W2, U, 0>(p, g, y); break;
         case 2: launch_sum_t<W2, U, 2>(p, g, y); break;
-        default: launch_sum_t<W2, U, 1>(p, g, y);
+        default: launch_sum_t<W2, U, 1 | 512>(p, g, y);
     }
 #endif
 }
