@@ -84,8 +84,17 @@ __global__ __launch_bounds__(256) void dia_kernel(int64_t m, int64_t mp, int64_t
         acc0 = madd(v.x, a, acc0);
         acc1 = madd(v.y, b, acc1);
     }
-    y[r] = acc0;
-    if (r + 1 < m) y[r + 1] = acc1;
+    // y is written once and not re-read: the row pair as one 16-byte
+    // nontemporal store where y is 16-byte aligned (r is even)
+    if (r + 1 < m && (reinterpret_cast<uintptr_t>(y) & 15) == 0) {
+        f64x2 yv;
+        yv.x = acc0;
+        yv.y = acc1;
+        __builtin_nontemporal_store(yv, reinterpret_cast<f64x2 *>(y + r));
+    } else {
+        y[r] = acc0;
+        if (r + 1 < m) y[r + 1] = acc1;
+    }
 }
 
 // LDS x window of a 512-row workgroup: 512 rows + diagonal span + 1

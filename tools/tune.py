@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--grid", default="")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--placement", default="", help="plan placement (e.g. search); default: the library's")
     ap.add_argument("--check", action="store_true", help="max rel err (and bit-equality) vs the oracle")
     a = ap.parse_args()
     import torch
@@ -45,6 +46,8 @@ def main():
     plans = []
     for combo in itertools.product(*vals) if vals else [()]:
         kw = dict(zip(keys, combo))
+        if a.placement:
+            kw["placement"] = a.placement
         t0 = time.time()
         p = sp.Plan.from_csr(m, n, rp, col, val, a.fmt, **kw)
         plans.append((kw, p, time.time() - t0))
