@@ -335,14 +335,18 @@ int build_ell(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &, int cap,
             }
             int32_t last = 0;
             for (int64_t k = 0; k < w; ++k) {
+                // columns: lane li's 4 slots of quad k/4 contiguous (16 B);
+                // values: slots 0-1 in the quad's first 1 KB, 2-3 in its
+                // second, lane li's pair at 16 B * li (k_ell.hip)
                 const int64_t pos = base + (k >> 2) * 256 + li * 4 + (k & 3);
+                const int64_t vpos = base + (k >> 2) * 256 + ((k & 2) ? 128 : 0) + li * 2 + (k & 1);
                 if (k < len) {
                     last = A.col[rs + k];
                     col[pos] = last;
-                    val[pos] = A.val[rs + k];
+                    val[vpos] = A.val[rs + k];
                 } else {
                     col[pos] = last;  // repeat a real column: no new cache line
-                    val[pos] = 0.0;
+                    val[vpos] = 0.0;
                 }
             }
         }

@@ -4,8 +4,9 @@
 //
 // One wave = one slice of 64 consecutive rows, one lane = one row.  Slots are
 // interleaved by 4 (see EllDev): at step q a lane issues one 16-byte load of
-// 4 column indices and two 16-byte loads of 4 values -- every wave
-// instruction reads 1 KiB contiguous -- then 4 x gathers.  The slice width is
+// 4 column indices and two 16-byte loads of 4 values (slots 0-1 from the
+// quad's first KiB of values, 2-3 from its second) -- every wave instruction
+// reads 1 KiB contiguous -- then 4 x gathers.  The slice width is
 // wave-uniform, so the loop has no divergence.  Each row is summed
 // sequentially in slot order with a rounded multiply + rounded add, i.e. the
 // same arithmetic as opt_crs/opt_ell (bit-exact against oracle/).  Padding
@@ -31,7 +32,7 @@ __global__ __launch_bounds__(256) void ell_slice_kernel(int64_t m, int64_t n_sli
     const int64_t base = slice_off[slice];
     const int64_t quads = (slice_off[slice + 1] - base) >> 8;  // (width/4)
     const int32_t *cp = col + base + lane * 4;
-    const double *vp = val + base + lane * 4;
+    const double *vp = val + base + lane * 2;
     double acc = 0.0;
     int64_t q = 0;
     for (; q + UNROLL <= quads; q += UNROLL) {
@@ -41,7 +42,7 @@ __global__ __launch_bounds__(256) void ell_slice_kernel(int64_t m, int64_t n_sli
         for (int u = 0; u < UNROLL; ++u) {
             c[u] = ld_stream4(cp + (q + u) * 256);
             a[u] = ld_stream2(vp + (q + u) * 256);
-            b[u] = ld_stream2(vp + (q + u) * 256 + 2);
+            b[u] = ld_stream2(vp + (q + u) * 256 + 128);
         }
         double g[UNROLL][4];
 #pragma unroll
@@ -62,7 +63,7 @@ __global__ __launch_bounds__(256) void ell_slice_kernel(int64_t m, int64_t n_sli
     for (; q < quads; ++q) {
         const i32x4 c = ld_stream4(cp + q * 256);
         const f64x2 a = ld_stream2(vp + q * 256);
-        const f64x2 b = ld_stream2(vp + q * 256 + 2);
+        const f64x2 b = ld_stream2(vp + q * 256 + 128);
         const double g0 = ld_x(x, c.x), g1 = ld_x(x, c.y), g2 = ld_x(x, c.z), g3 = ld_x(x, c.w);
         acc = madd(a.x, g0, acc);
         acc = madd(a.y, g1, acc);
