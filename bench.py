@@ -1,11 +1,12 @@
 #!/usr/bin/env python3
 """bench.py -- SpMV GFLOP/s + achieved HBM GB/s (fp64) on 1..8 MI355X.
 
-Workload (BASELINE.json configs[1], weak-scaled): every rank owns a block of
-10M rows x 16 nnz/row of a uniform random CSR whose column space is the
-whole matrix (N*10M columns): N=1 is the 10M x 10M config, N=8 is the
-80M x 80M row-partitioned config (configs[4]).  x is generated on rank 0 and
-replicated with an RCCL broadcast over xGMI (setup, untimed -- x is fixed
+Headline workload (BASELINE.json configs[1], weak-scaled): every rank owns a
+block of 10M rows x 16 nnz/row of a uniform random CSR whose column space is
+the whole matrix (N*10M columns): N=1 is the 10M x 10M config, N=8 is the
+80M x 80M row-partitioned config (configs[4]).  Rows are cut nnz-balanced
+(equal blocks for the uniform matrix).  x is generated on rank 0
+and replicated with an RCCL broadcast over xGMI (setup, untimed -- x is fixed
 across calls as in the reference driver, src/main.cpp:36-102); y slices are
 gathered with RCCL all_gather, timed separately ("collective_ms").
 
@@ -15,18 +16,24 @@ barrier + torch.cuda.synchronize(); a trial's time is the max over ranks and
 `value` comes from the fastest trial -- the reference driver's "min over
 trials of the mean per call" (src/main.cpp:58-102).  The same K steps are
 timed with HIP events on the plan's stream (spmv_time): that per-launch
-duration feeds `roofline.achieved`.
+duration feeds `roofline.achieved`.  Every plan is built with the library's
+default placement (what a caller of OptimizeProblem gets).
+
+At N = 1 the same line also carries configs 3 and 4 (BASELINE.json
+configs[2], configs[3]) under `configs`: the power-law matrix through AUTO
+(BIN) and the banded matrix through DIA with CSR beside it ("report DIA
+against CSR"), each with its own roofline, PMC traffic and
+max_rel_err_vs_cpu against the CPU port on the same matrix (`--only-config`
+skips them).  At N > 1 `per_rank` lists every rank's rows, nnz, Mul / Sum
+phases and event time, so the max-over-ranks step can be read per rank.
 
 `--gpus N` with no torchrun environment starts `torch.distributed.run` with N
-ranks (one per GPU) as a child process before anything touches the GPU, and
-exits with the child's return code.
+ranks (one per GPU) as a child process before anything in this process loads
+HIP (the GPUs are counted from the KFD topology in sysfs), and exits with the
+child's return code.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--trials T]
-                  [--config c2|c3|c4] [--formats auto,auto@plain,csr,ell,ss,css] [--no-cpu]
-
-The headline plan asks for the build-time placement search (--placement
-search: the bench owns the GPU); `formats["auto@plain"]` is the same plan with
-the library's default single allocation, reported beside it.
+                  [--config c2|c3|c4] [--formats auto,csr,ell,ss,css] [--only-config] [--no-cpu]
 
 Prints ONE JSON line on rank 0.
 """
@@ -46,11 +53,14 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
 
 CONFIGS = {
-    # name: (generator kwargs per rank, description)
+    # name: (generator kwargs, description, rows per GPU)
     "c2": (dict(kind="uniform", per_row=16), "uniform 10M x 10M, 16 nnz/row (per GPU)", 10_000_000),
     "c3": (dict(kind="powerlaw", max_len=10000, alpha=2.0), "power-law 5M rows, 1-10k nnz/row", 5_000_000),
     "c4": (dict(kind="banded", band_lo=-32, band_hi=31), "banded 20M rows, 64 diagonals", 20_000_000),
 }
+# the configs the N = 1 line carries beside the headline: (config, formats)
+EXTRA_CONFIGS = (("c3", ["auto"]), ("c4", ["auto", "csr"]))
+KFD_TOPOLOGY = "/sys/class/kfd/kfd/topology/nodes"
 
 
 def streamed_bytes(info) -> dict:
@@ -114,15 +124,13 @@ def parse():
                     help="timed trials of K steps; value = the fastest (src/main.cpp:58-102)")
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--rows", type=int, default=0, help="rows per GPU (default: the config's)")
-    ap.add_argument("--formats", default="auto,auto@plain,csr,ell,ss,css",
-                    help="first entry is the headline plan; the rest are reported alongside; "
-                         "fmt@placement overrides --placement for that plan (auto@plain: the "
-                         "library's default placement, reported beside the searched one)")
-    ap.add_argument("--placement", default="search", choices=["search", "plain", "vmm", "auto"],
-                    help="plan-build placement of the BIN product buffer / DIA values (spmv_hip.h "
-                         "SPMV_PLACEMENT_*): the bench owns the GPU, so it asks for the build-time search")
+    ap.add_argument("--formats", default="auto,csr,ell,ss,css",
+                    help="first entry is the headline plan; the rest are reported alongside")
+    ap.add_argument("--only-config", action="store_true",
+                    help="time --config alone (no configs 3 / 4 beside the N = 1 headline)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
-    ap.add_argument("--cpu-seconds", type=float, default=2.0)
+    ap.add_argument("--cpu-seconds", type=float, default=1.0,
+                    help="CPU warm-up: double the calls until this long (src/main.cpp:58-71)")
     ap.add_argument("--verify", action="store_true",
                     help="gather y to rank 0 and compare with the oracle over the full matrix "
                          "(tests; small sizes only)")
@@ -132,11 +140,37 @@ def parse():
     return ap.parse_args()
 
 
-def self_launch(args):
+def visible_gpu_count(topology: str = None) -> int:
+    """GPUs this process may use, counted WITHOUT loading HIP: KFD topology
+    nodes with SIMDs (CPU nodes have none), capped by the length of a
+    HIP/ROCR/CUDA_VISIBLE_DEVICES list.  (torch.cuda.device_count() needs
+    amdsmi to stay off HIP; this does not depend on it.)"""
+    root = topology or os.environ.get("BENCH_KFD_TOPOLOGY", KFD_TOPOLOGY)
+    gpus = 0
+    try:
+        for node in os.listdir(root):
+            try:
+                for line in open(os.path.join(root, node, "properties")):
+                    k, _, v = line.partition(" ")
+                    if k == "simd_count" and int(v) > 0:
+                        gpus += 1
+                        break
+            except (OSError, ValueError):
+                continue
+    except OSError:
+        return 0
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            gpus = min(gpus, len([t for t in v.split(",") if t.strip()]))
+    return gpus
+
+
+def self_launch(args, runner=None):
     """--gpus N outside torchrun: run this script under torch.distributed.run
-    with N ranks (rendezvous on 127.0.0.1) and return its exit code.  Called
-    before any GPU call in this process (device_count() does not initialise
-    the GPU); None = run in-process."""
+    with N ranks (rendezvous on 127.0.0.1) and return its exit code.  Nothing
+    here loads HIP (tests/test_guards.py checks the parent's memory map at
+    the spawn); None = run in-process."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if args.gpus <= 1 or world == args.gpus or args.sim_world:
         return None
@@ -144,8 +178,7 @@ def self_launch(args):
         print(json.dumps({"error": f"--gpus {args.gpus} inside a launcher with WORLD_SIZE={world}"}))
         return 2
     if os.environ.get("BENCH_DIST_BACKEND", "nccl") == "nccl":
-        import torch
-        ndev = torch.cuda.device_count()
+        ndev = visible_gpu_count()
         if ndev < args.gpus:
             print(json.dumps({"error": f"--gpus {args.gpus} but {ndev} GPUs visible "
                                        "(BENCH_DIST_BACKEND=gloo shares one GPU between ranks)"}))
@@ -157,13 +190,225 @@ def self_launch(args):
            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    return subprocess.call(cmd, env=env)
+    return (runner or subprocess.call)(cmd, env=env)
 
 
 def traffic_key(config: str, m: int, n: int, kernel: str) -> str:
     """profiles/pmc_traffic*.json key: the PMC bytes of one launch of
     `kernel` on an m x n rank shape of `config` (none for other shapes)."""
     return f"{config}:{m}x{n}:{kernel}"
+
+
+def lookup_traffic(config: str, m: int, n: int, kernel: str):
+    """(bytes, kind) of the profiled launch of `kernel` on this shape: the
+    calibrated table (2*FETCH_SIZE + WRITE_SIZE, the gfx950 correction)
+    first, else raw FETCH + WRITE; (None, None) for an unprofiled shape."""
+    key = traffic_key(config, m, n, kernel)
+    for fname, kind in (("pmc_traffic_calibrated.json", "pmc_calibrated"), ("pmc_traffic.json", "pmc_raw")):
+        path = os.path.join(ROOT, "profiles", fname)
+        try:
+            t = json.load(open(path)) if os.path.exists(path) else {}
+        except ValueError:
+            t = {}
+        if key in t:
+            v = t[key]
+            return (v["bytes"] if isinstance(v, dict) else v), kind
+    return None, None
+
+
+def cpu_time(oracle, rp, col, val, x, nthreads: int, min_seconds: float):
+    """src/main.cpp:58-102 on the CPU port: double the calls until >=
+    min_seconds, then the min over 10 trials of the mean per call."""
+    return oracle.csr_time(rp, col, val, x, nthreads=nthreads, min_seconds=min_seconds, ntry=10)
+
+
+class Ctx:
+    """Process-wide state: ranks, device, distributed flags."""
+
+    def __init__(self, args):
+        import torch
+        import torch.distributed as dist
+
+        from singlespmv_amd import dist as sdist
+        self.torch, self.dist, self.sdist = torch, dist, sdist
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        # BENCH_DIST_BACKEND=gloo lets several ranks share one GPU (development
+        # rehearsal of the multi-GPU flow); the driver's runs use nccl = RCCL.
+        self.backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")
+        ndev = torch.cuda.device_count()
+        self.local = local % ndev if self.backend == "gloo" else local
+        torch.cuda.set_device(self.local)
+        self.dev = torch.device("cuda", self.local)
+        self.distributed = self.world > 1
+        if self.distributed:
+            if self.backend == "nccl":
+                dist.init_process_group("nccl", device_id=self.dev)
+            else:
+                dist.init_process_group(self.backend)
+        sdist.set_cpu_collectives(self.backend == "gloo")
+        self.shape_world = args.sim_world if (args.sim_world and self.world == 1) else self.world
+
+
+def build_matrix(ctx, args, config: str, rows_override: int = 0):
+    """This rank's shard of `config` (nnz-balanced rows) and the replicated x."""
+    import singlespmv_amd as sp
+    torch = ctx.torch
+    gen_kw, desc, rows_default = CONFIGS[config]
+    rows = rows_override or rows_default
+    m_glob = rows * ctx.shape_world
+    n_glob = m_glob
+    t0 = time.time()
+    spec = sp.gen_spec(gen_kw["kind"], m_glob, n_glob, per_row=gen_kw.get("per_row", 16),
+                       max_len=gen_kw.get("max_len", 10000), alpha=gen_kw.get("alpha", 2.0),
+                       band_lo=gen_kw.get("band_lo", -32), band_hi=gen_kw.get("band_hi", 31), seed=42)
+    cuts = ctx.sdist.generated_cuts(spec, ctx.shape_world)
+    rank = ctx.rank if ctx.world > 1 else 0
+    (row0, row1), rp, col, val = ctx.sdist.shard_generated(spec, rank, ctx.shape_world, cuts)
+    nnz_local = int(rp[-1])
+    # total flops of the job: every rank's own nnz
+    nnz_total = int(round(ctx.sdist.sum_over_ranks([float(nnz_local)], ctx.dev)[0]))
+    t_gen = time.time() - t0
+    # x: generated once on rank 0, replicated by RCCL broadcast over xGMI
+    x = torch.empty(n_glob, dtype=torch.float64, device=ctx.dev)
+    if ctx.rank == 0:
+        x.copy_(torch.from_numpy(sp.generate_vector(n_glob, seed=43)))
+    t_bcast = None
+    if ctx.distributed:
+        torch.cuda.synchronize()
+        ctx.dist.barrier()
+        tb = time.perf_counter()
+        ctx.sdist.replicate_x(x, src=0)
+        torch.cuda.synchronize()
+        t_bcast = time.perf_counter() - tb
+    return dict(config=config, desc=desc, spec=spec, cuts=cuts, rows=row1 - row0, row0=row0, row1=row1,
+                rows_nominal=rows, m=m_glob, n=n_glob, rp=rp, col=col, val=val, nnz_local=nnz_local,
+                nnz_total=nnz_total, x=x, gen_s=t_gen, bcast_s=t_bcast)
+
+
+RELEVANT = {"csr": ("csr_lanes",), "ss": ("ss_sigma",), "ell": ("ell_width",),
+            "hyb": ("ell_width",), "dia": ("n_diags",), "css": ("css_passes", "css_slabs"),
+            "bin": ("bin_bins", "bin_strips", "bin_strip_cols", "bin_pad", "bin_sum_waves",
+                    "bin_long_len", "bin_long_rows", "bin_long_pieces", "bin_products")}
+
+
+def time_formats(ctx, args, M, fmts, trials_head: int):
+    """Build and time each format on M; the first is the headline (kept, with
+    its y).  Returns (results, headline (plan, info, r) or None, y_head)."""
+    import singlespmv_amd as sp
+    torch = ctx.torch
+    y = torch.empty(M["rows"], dtype=torch.float64, device=ctx.dev)
+    results, headline, y_head = {}, None, None
+    for fi, fmt in enumerate(fmts):
+        tp = time.time()
+        try:
+            plan = sp.Plan.from_csr(M["rows"], M["n"], M["rp"], M["col"], M["val"], fmt=fmt, device=ctx.local)
+        except sp.SpmvError as e:
+            results[fmt] = {"error": str(e)}
+            continue
+        t_plan = time.time() - tp
+        info = plan.info()
+        stream = torch.cuda.Stream(device=ctx.dev)
+        plan.set_stream(stream)
+        torch.cuda.synchronize()
+        if args.warmup:
+            plan.time(M["x"], y, args.warmup)
+        trials = []  # (max-over-ranks wall s, this rank's event ms, this rank's wall s)
+        for _ in range(trials_head if fi == 0 else min(trials_head, 2)):
+            torch.cuda.synchronize()
+            if ctx.distributed:
+                ctx.dist.barrier()
+            torch.cuda.synchronize()
+            tw = time.perf_counter()
+            ev_ms = plan.time(M["x"], y, args.steps)  # K launches between HIP events
+            torch.cuda.synchronize()
+            if ctx.distributed:
+                ctx.dist.barrier()
+            wall = time.perf_counter() - tw
+            wall_max = ctx.sdist.max_over_ranks([wall], ctx.dev)[0]
+            trials.append((wall_max, ev_ms, wall))
+        wall_max, ev_ms, wall_own = min(trials)
+        launch_s = ev_ms / 1e3 / args.steps
+        r = {
+            "format": info["format"], "kernel": info["kernel"],
+            "gflops": 2.0 * M["nnz_total"] * args.steps / wall_max / 1e9,
+            "ms_per_step": wall_max / args.steps * 1e3,
+            "trials_ms_per_step": [round(t[0] / args.steps * 1e3, 5) for t in trials],
+            "event_ms_per_launch": launch_s * 1e3,
+            "own_wall_ms_per_step": wall_own / args.steps * 1e3,
+            "achieved_gbs": info["algo_bytes"] / launch_s / 1e9,
+            "algo_bytes": info["algo_bytes"], "stored_slots": info["stored_slots"],
+            "device_bytes": info["device_bytes"], "plan_build_s": round(t_plan, 3),
+            "n_kernels": info["n_kernels"], "placement": info["placement"],
+        }
+        for k in RELEVANT.get(info["format"], ()):
+            r[k] = info[k]
+        if info["n_kernels"] > 1:
+            r["phases_ms"] = plan.profile(M["x"], y, 10)  # e.g. BIN Mul / Sum (opt_ss MulPerf / SumPerf)
+        results[fmt if fmt not in results else f"{fmt}_{fi}"] = r
+        if fi == 0:
+            headline = (plan, info, r)
+            y_head = y.clone()
+        else:
+            plan.destroy()
+        torch.cuda.synchronize()
+    return results, headline, y_head
+
+
+def roofline_of(config: str, M, r) -> dict:
+    ach = r["achieved_gbs"]
+    out = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+           "traffic": None, "kernel": r["kernel"], "algo_bytes_per_launch": r["algo_bytes"],
+           "launch_ms": r["event_ms_per_launch"]}
+    # roofline.traffic: PMC bytes per launch of this kernel on this rank shape
+    tb, kind = lookup_traffic(config, M["rows"], M["n"], r["kernel"])
+    if tb is not None:
+        out["traffic"] = tb
+        out["traffic_kind"] = kind
+        # the HBM bandwidth the kernels actually sustain: the profiled bytes of
+        # one launch over this run's launch time (frac above prices only the
+        # algorithmic bytes)
+        tg = tb / (r["event_ms_per_launch"] * 1e-3) / 1e9
+        out["traffic_gbs"] = tg
+        out["traffic_frac"] = tg / HBM_PEAK_GBS
+    return out
+
+
+def extra_config(ctx, args, config: str, fmts, stream_gbs: float) -> dict:
+    """One of configs 3 / 4 beside the N = 1 headline: headline format, the
+    others beside it, roofline + PMC traffic, y against the CPU port."""
+    import oracle
+    M = build_matrix(ctx, args, config)
+    results, head, y_head = time_formats(ctx, args, M, fmts, trials_head=3)
+    if head is None:
+        return {"error": "no plan could be built", "details": results}
+    plan, info, r = head
+    plan.destroy()
+    x_host = M["x"].cpu().numpy()
+    tc = time.perf_counter()
+    y_cpu = oracle.csr_spmv(M["rp"], M["col"], M["val"], x_host)
+    t_cpu = time.perf_counter() - tc
+    ygpu = y_head.cpu().numpy()
+    max_rel = float(np.max(np.abs(ygpu - y_cpu) / np.maximum(np.abs(y_cpu), 1e-300)))
+    for fr in results.values():
+        if "achieved_gbs" in fr:
+            fr["frac_of_stream"] = fr["achieved_gbs"] / stream_gbs
+            fr["roofline_frac"] = fr["achieved_gbs"] / HBM_PEAK_GBS
+    roof = roofline_of(config, M, r)
+    roof["frac_of_stream"] = r["achieved_gbs"] / stream_gbs
+    out = {"workload": f"{config}: {M['desc']}", "m": M["m"], "n": M["n"], "nnz": M["nnz_local"],
+           "format": r["format"], "kernel": r["kernel"], "value": r["gflops"], "unit": "GFLOP/s",
+           "ms_per_step": r["ms_per_step"], "event_ms_per_launch": r["event_ms_per_launch"],
+           "roofline": roof, "max_rel_err_vs_cpu": max_rel,
+           "cpu_check": {"kind": "port", "ms_one_call": t_cpu * 1e3,
+                         "note": "oracle opt_crs restatement (src/opt_crs.cpp:44-70), all host threads, one call"},
+           "gen_s": round(M["gen_s"], 2), "formats": results}
+    if "csr" in results and "event_ms_per_launch" in results["csr"] and r["format"] != "csr":
+        out[f"{r['format']}_vs_csr"] = results["csr"]["event_ms_per_launch"] / r["event_ms_per_launch"]
+    del M, y_head
+    ctx.torch.cuda.empty_cache()
+    return out
 
 
 def main():
@@ -187,158 +432,59 @@ def main():
         # (read by the library's OpenMP runtime when it loads, below)
         local_world = max(1, int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "1"))))
         os.environ["OMP_NUM_THREADS"] = str(max(1, host_cores // local_world))
-    import torch
-    import torch.distributed as dist
-
     import singlespmv_amd as sp
-    from singlespmv_amd import dist as sdist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    # BENCH_DIST_BACKEND=gloo lets several ranks share one GPU (development
-    # rehearsal of the multi-GPU flow); the driver's runs use nccl = RCCL.
-    backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")
-    ndev = torch.cuda.device_count()
-    local_dev = local % ndev if backend == "gloo" else local
-    torch.cuda.set_device(local_dev)
-    dev = torch.device("cuda", local_dev)
-    local = local_dev
-    distributed = world > 1
-    if distributed:
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group(backend)
-    sdist.set_cpu_collectives(backend == "gloo")
+    ctx = Ctx(args)
+    torch, dist, sdist = ctx.torch, ctx.dist, ctx.sdist
+    world, rank, dev, distributed = ctx.world, ctx.rank, ctx.dev, ctx.distributed
 
-    gen_kw, desc, rows_default = CONFIGS[args.config]
-    rows = args.rows or rows_default
-    shape_world = args.sim_world if (args.sim_world and world == 1) else world
-    m_glob = rows * shape_world
-    n_glob = m_glob
-    t0 = time.time()
-    kind = gen_kw["kind"]
-    spec = sp.gen_spec(kind, m_glob, n_glob, per_row=gen_kw.get("per_row", 16),
-                       max_len=gen_kw.get("max_len", 10000), alpha=gen_kw.get("alpha", 2.0),
-                       band_lo=gen_kw.get("band_lo", -32), band_hi=gen_kw.get("band_hi", 31),
-                       seed=42)
-    (row0, row1), rp, col, val = sdist.shard_generated(spec, rank, shape_world)
-    nnz_local = int(rp[-1])
-    # total flops of the job: every rank's own nnz (power-law rows make the
-    # equal row blocks unequal in nnz)
-    nnz_total = int(round(sdist.sum_over_ranks([float(nnz_local)], dev)[0]))
-    t_gen = time.time() - t0
-
-    # x: generated once on rank 0, replicated by RCCL broadcast over xGMI
-    x = torch.empty(n_glob, dtype=torch.float64, device=dev)
-    if rank == 0:
-        x.copy_(torch.from_numpy(sp.generate_vector(n_glob, seed=43)))
-    t_bcast = 0.0
-    if distributed:
-        torch.cuda.synchronize()
-        dist.barrier()
-        tb = time.perf_counter()
-        sdist.replicate_x(x, src=0)
-        torch.cuda.synchronize()
-        t_bcast = time.perf_counter() - tb
-    y = torch.empty(rows, dtype=torch.float64, device=dev)
+    M = build_matrix(ctx, args, args.config, args.rows)
+    rows, n_glob, m_glob = M["rows"], M["n"], M["m"]
+    nnz_local, nnz_total, x = M["nnz_local"], M["nnz_total"], M["x"]
 
     fmts = [f for f in args.formats.split(",") if f]
-    results = {}
-    headline = None
-    for fi, spec_f in enumerate(fmts):
-        fmt, _, placement = spec_f.partition("@")
-        placement = placement or args.placement
-        tp = time.time()
-        try:
-            plan = sp.Plan.from_csr(rows, n_glob, rp, col, val, fmt=fmt, device=local, placement=placement)
-        except sp.SpmvError as e:
-            results[spec_f] = {"error": str(e)}
-            continue
-        t_plan = time.time() - tp
-        info = plan.info()
-        stream = torch.cuda.Stream(device=dev)
-        plan.set_stream(stream)
-        torch.cuda.synchronize()
-        # warm-up
-        if args.warmup:
-            plan.time(x, y, args.warmup)
-        trials = []  # (max-over-ranks wall s, this rank's event ms)
-        for _ in range(args.trials if fi == 0 else min(args.trials, 2)):
-            torch.cuda.synchronize()
-            if distributed:
-                dist.barrier()
-            torch.cuda.synchronize()
-            tw = time.perf_counter()
-            ev_ms = plan.time(x, y, args.steps)  # K launches between HIP events
-            torch.cuda.synchronize()
-            if distributed:
-                dist.barrier()
-            wall = time.perf_counter() - tw
-            wall_max, _ = sdist.max_over_ranks([wall, ev_ms], dev)
-            trials.append((wall_max, ev_ms))
-        wall_max, ev_ms = min(trials)
-        launch_s = ev_ms / 1e3 / args.steps
-        flops_total = 2.0 * nnz_total * args.steps
-        r = {
-            "format": info["format"], "kernel": info["kernel"],
-            "gflops": flops_total / wall_max / 1e9,
-            "ms_per_step": wall_max / args.steps * 1e3,
-            "trials_ms_per_step": [round(t[0] / args.steps * 1e3, 5) for t in trials],
-            "event_ms_per_launch": launch_s * 1e3,
-            "achieved_gbs": info["algo_bytes"] / launch_s / 1e9,
-            "algo_bytes": info["algo_bytes"], "stored_slots": info["stored_slots"],
-            "device_bytes": info["device_bytes"], "plan_build_s": round(t_plan, 3),
-            "n_kernels": info["n_kernels"],
-            "placement": info["placement"],
-        }
-        if info["placement_candidates"]:
-            r["placement_candidates_ms"] = [round(info["placement_best_ms"], 4), round(info["placement_worst_ms"], 4),
-                                            info["placement_candidates"]]
-        relevant = {"csr": ("csr_lanes",), "ss": ("ss_sigma",), "ell": ("ell_width",),
-                    "hyb": ("ell_width",), "dia": ("n_diags",), "css": ("css_passes", "css_slabs"),
-                    "bin": ("bin_bins", "bin_strips", "bin_strip_cols", "bin_pad", "bin_sum_waves",
-                            "bin_long_len", "bin_long_rows", "bin_long_pieces", "bin_products")}
-        if info["format"] == "bin" and fi != 0:
-            r["phases_ms"] = plan.profile(x, y, 10)  # Mul / Sum split (opt_ss MulPerf / SumPerf)
-        for k in relevant.get(info["format"], ()):
-            r[k] = info[k]
-        results[spec_f if spec_f not in results else f"{spec_f}_{fi}"] = r
-        if fi == 0:
-            r["phases_ms"] = plan.profile(x, y, 10)
-            headline = (plan, info, r)
-            y_head = y.clone()
-        else:
-            del plan
-        torch.cuda.synchronize()
-
+    results, headline, y_head = time_formats(ctx, args, M, fmts, args.trials)
     if headline is None:
         if rank == 0:
             print(json.dumps({"error": "no plan could be built", "details": results}))
         return 1
     plan, info, r = headline
 
+    # per-rank view of the headline step (the value is the max over ranks)
+    per_rank = None
+    if distributed:
+        ph = r.get("phases_ms", {})
+        rows_all = sdist.gather_floats([float(rank), float(M["row0"]), float(M["row1"]), float(nnz_local),
+                                        r["own_wall_ms_per_step"], r["event_ms_per_launch"],
+                                        float(ph.get("mul", -1.0)), float(ph.get("sum", -1.0))], dev)
+        per_rank = [{"rank": int(v[0]), "rows": [int(v[1]), int(v[2])], "nnz": int(v[3]),
+                     "wall_ms_per_step": v[4], "event_ms_per_launch": v[5],
+                     "phases_ms": {"mul": v[6], "sum": v[7]} if v[6] >= 0 else None,
+                     "placement": info["placement"]} for v in rows_all]
+
     # y gather (RCCL all_gather over xGMI), timed separately from the kernel
+    # (slices padded to the longest rank's rows)
+    rows_max = int(np.max(np.diff(M["cuts"]))) if distributed else rows
     coll_ms = None
     if distributed:
         for _ in range(3):
-            sdist.gather_y(y_head, rows)
+            sdist.gather_y(y_head, rows_max)
         torch.cuda.synchronize()
         dist.barrier()
         tc = time.perf_counter()
         reps = 10
         for _ in range(reps):
-            sdist.gather_y(y_head, rows)
+            sdist.gather_y(y_head, rows_max)
         torch.cuda.synchronize()
         coll_ms = (time.perf_counter() - tc) / reps * 1e3
 
     # iterative use (power-iteration shape): every step is the
     # local SpMV followed by ONE all_gather of the y slices into the next x
     # (RCCL over xGMI), both on the current stream; reported beside `value`,
-    # never as it.  Runs on a copy of x.
+    # never as it.  Runs on a copy of x; needs equal slices (uniform rows).
     iterative = None
-    if distributed and n_glob == rows * world:
+    equal_slices = bool(np.all(np.diff(M["cuts"]) == rows)) and n_glob == rows * world
+    if distributed and equal_slices:
         x_it = x.clone()
         cur = torch.cuda.current_stream(dev)
         plan.set_stream(cur)
@@ -357,7 +503,6 @@ def main():
         iterative = {"ms_per_iter": t_it * 1e3, "gflops": 2.0 * nnz_total / t_it / 1e9,
                      "step": "local SpMV + all_gather(y slices -> next x)"}
         del x_it
-        plan.set_stream(stream)
         plan.execute(x, y_head)  # y_head back to A x for the checks below
 
     # the drop-in's host-buffer mode (opt_cusparse's per-call H2D x / D2H y,
@@ -382,30 +527,38 @@ def main():
         # the whole y (all ranks' slices, RCCL/gloo all_gather) vs the oracle's
         # opt_crs restatement of the full global matrix
         import oracle
-        y_full = sdist.gather_y(y_head, rows)[:m_glob].cpu().numpy() if distributed else y_head.cpu().numpy()
+        if distributed:
+            parts = sdist.gather_y(y_head, rows_max).cpu().numpy().reshape(world, rows_max)
+            y_full = np.concatenate([parts[k, :int(M["cuts"][k + 1] - M["cuts"][k])] for k in range(world)])
+        else:
+            y_full = y_head.cpu().numpy()
         if rank == 0:
-            grp, gcol, gval = sp.generate_csr(spec)
+            grp, gcol, gval = sp.generate_csr(M["spec"])
             yref = oracle.csr_spmv(grp, gcol, gval, x.cpu().numpy())
+            if ctx.shape_world != world:  # emulated rank 0: its rows only
+                yref = yref[:rows]
             verify_rel = float(np.max(np.abs(y_full - yref) / np.maximum(np.abs(yref), 1e-300)))
 
     # CPU baseline: the oracle's restatement of opt_crs SpMV (src/opt_crs.cpp:
     # 44-70; OpenMP static over rows, every host core of this process's
     # affinity, pinned), timed with the reference driver's method
-    # (src/main.cpp:58-102: doubling warm-up to --cpu-seconds, min over 3
-    # trials of the mean per call) on rank 0 at N = 1.  The reference's own
-    # compiled opt_crs never ships to the GPU box; it was
-    # timed beside the port in the build container (profiles/round2/cpu_ref_vs_port.json).
+    # (src/main.cpp:58-102: double the calls until >= 1 s, then the min over
+    # 10 trials of the mean per call) on rank 0 at N = 1; the 1-thread figure
+    # the same way on a bounded sample (the matrix's first tenth of rows, all
+    # of x).  The reference's own compiled opt_crs never ships to the GPU box
+    # (SURVEY §8(c)); it was timed beside the port in the build container
+    # (profiles/round2/cpu_ref_vs_port.json).
     cpu = None
     max_rel = None
     if rank == 0 and world == 1 and not args.no_cpu:
         import oracle
         nthreads = min(host_cores, int(os.environ.get("OMP_NUM_THREADS", host_cores)))
         x_host = x.cpu().numpy()
-        t_cpu, loop, y_cpu = oracle.csr_time(rp, col, val, x_host, nthreads=nthreads,
-                                             min_seconds=args.cpu_seconds, ntry=3)
-        # the 1-thread figure BASELINE.md §4 asks for (short doubling warm-up,
-        # one trial: a bounded sample of the same matrix)
-        t_cpu1, _, _ = oracle.csr_time(rp, col, val, x_host, nthreads=1, min_seconds=0.5, ntry=1)
+        t_cpu, loop, y_cpu = cpu_time(oracle, M["rp"], M["col"], M["val"], x_host, nthreads, args.cpu_seconds)
+        r1 = max(1, rows // 10)
+        e1 = int(M["rp"][r1])
+        t_cpu1, loop1, _ = cpu_time(oracle, M["rp"][:r1 + 1], M["col"][:e1], M["val"][:e1], x_host, 1,
+                                    args.cpu_seconds)
         ygpu = y_head.cpu().numpy()
         max_rel = float(np.max(np.abs(ygpu - y_cpu) / np.maximum(np.abs(y_cpu), 1e-300)))
         cpu = {"value": 2.0 * nnz_local / t_cpu / 1e9, "unit": "GFLOP/s", "cores": nthreads,
@@ -413,40 +566,32 @@ def main():
                "omp_proc_bind": os.environ.get("OMP_PROC_BIND"),
                "omp_places": os.environ.get("OMP_PLACES"),
                "sample": f"full {rows}-row matrix ({nnz_local} nnz), oracle opt_crs restatement "
-                         f"(oracle/oracle.c, src/opt_crs.cpp:44-70), {loop} calls x 3 trials after a "
-                         f"{args.cpu_seconds:.0f} s doubling warm-up, min mean per call, "
-                         f"{nthreads} threads = the host cores of this process's affinity",
+                         f"(oracle/oracle.c, src/opt_crs.cpp:44-70): calls doubled until >= "
+                         f"{args.cpu_seconds:g} s ({loop} calls), then the min over 10 trials of the mean "
+                         f"per call (src/main.cpp:58-102), {nthreads} threads = the host cores of this "
+                         f"process's affinity",
                "ms_per_call": t_cpu * 1e3,
                "gbs": (12 * nnz_local + 4 * (rows + 1) + 16 * rows) / t_cpu / 1e9,
-               "value_1thread": 2.0 * nnz_local / t_cpu1 / 1e9,
+               "value_1thread": 2.0 * e1 / t_cpu1 / 1e9,
+               "sample_1thread": f"first {r1} rows ({e1} nnz) of the same matrix, all of x, 1 thread, "
+                                 f"same method ({loop1} calls per trial, min of 10)",
                "cpu_model": cpu_model()}
 
-    achieved = r["achieved_gbs"]
-    # measured STREAM-read ceiling of this GPU (reported beside the spec peak)
+    # measured ceilings of this GPU (reported beside the spec peak)
+    local = ctx.local
     stream_gbs = sp.stream_probe(local, 2 << 30, 10)
     stream_write_gbs = sp.stream_write_probe(local, 2 << 30, 10)
     mixed_gbs = sp.mixed_probe(local, 1792 << 20, 3, 20)
-    # and the measured ceiling of random 8-byte x gathers that hit L2: every
-    # format here issues one x gather per nnz, so this bounds the gather side
+    # random 8-byte x gathers that hit L2 (CSS's slab), and from a table of
+    # x's own size (the row-parallel formats' gathers)
     gather_gps = sp.gather_probe(local, 64 << 20, 1 << 20)
-    # ... and from a table of x's own size (beyond L2 once x > 4 MB): the
-    # ceiling of the row-parallel formats, whose gathers go wherever x is
     gather_x_gps = sp.gather_probe(local, 64 << 20, min(max(8 * n_glob, 1 << 20), 2 << 30))
-    gathers_gps = nnz_local / (r["event_ms_per_launch"] * 1e-3)
-    gather_fields = {}
-    if r["format"] not in ("dia", "bin"):  # DIA and BIN read x from LDS, not by gathers
-        gather_fields = {"x_gathers_per_s": gathers_gps, "gather_ceiling_per_s": gather_gps,
-                         "frac_of_gather_ceiling": gathers_gps / gather_gps}
-    # per format: x gathers/s against the ceiling of where its gathers land
-    # (CSS: an L2-resident slab; CSR/ELL/SS/COO/JDS/HYB: an x-sized table of
-    # random gathers -- > 1 when the gathers are not random, as on a banded
-    # matrix, whose bound is then the stream)
     for fr in results.values():
         if "event_ms_per_launch" not in fr:
             continue
-        # and its algorithmic bytes against the measured STREAM-read ceiling
         fr["frac_of_stream"] = fr["achieved_gbs"] / stream_gbs
-        if fr["format"] in ("dia", "bin"):
+        fr["roofline_frac"] = fr["achieved_gbs"] / HBM_PEAK_GBS
+        if fr["format"] in ("dia", "bin"):  # DIA and BIN read x from LDS, not by gathers
             continue
         g = nnz_local / (fr["event_ms_per_launch"] * 1e-3)
         ceil = gather_gps if fr["format"] == "css" else gather_x_gps
@@ -457,6 +602,12 @@ def main():
     # the reference's CSR5 byte model (CSR5_cuda/detail/utils.h:10-14), which
     # charges x per nnz -- for comparability with published CSR5 numbers only
     csr5_bytes = (rows + 1 + nnz_local) * 4 + (2 * nnz_local + rows) * 8
+    roof = roofline_of(args.config, M, r)
+    roof.update({"stream_ceiling_gbs": stream_gbs, "frac_of_stream": r["achieved_gbs"] / stream_gbs,
+                 "stream_write_gbs": stream_write_gbs, "mixed_rw_gbs": mixed_gbs,
+                 "csr5_model_gbs": csr5_bytes / (r["event_ms_per_launch"] * 1e-3) / 1e9})
+    if "traffic_gbs" in roof:
+        roof["traffic_frac_of_stream"] = roof["traffic_gbs"] / stream_gbs
     out = {
         "metric": "SpMV GFLOP/s (fp64) + achieved HBM GB/s",
         "value": r["gflops"],
@@ -465,26 +616,19 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "trials": args.trials,
-        "placement": args.placement,
         "ms_per_step": r["ms_per_step"],
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (seeded generator, seed 42; x seed 43)",
-        "config": {"workload": f"{args.config}: {desc}", "rows_per_gpu": rows,
+        "config": {"workload": f"{args.config}: {M['desc']}", "rows_per_gpu": M["rows_nominal"],
                    "m": m_glob, "n": n_glob, "nnz_per_gpu": nnz_local, "nnz_total": nnz_total,
-                   "format": r["format"], "kernel": r["kernel"],
-                   "parallelism": f"row-partition x{world}, x replicated (RCCL broadcast)"},
-        "achieved_gbs": achieved,
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": r["kernel"], "algo_bytes_per_launch": r["algo_bytes"],
-                     "launch_ms": r["event_ms_per_launch"],
-                     "stream_ceiling_gbs": stream_gbs, "frac_of_stream": achieved / stream_gbs,
-                     "stream_write_gbs": stream_write_gbs, "mixed_rw_gbs": mixed_gbs,
-                     **gather_fields,
-                     "csr5_model_gbs": csr5_bytes / (r["event_ms_per_launch"] * 1e-3) / 1e9},
+                   "format": r["format"], "kernel": r["kernel"], "placement": info["placement"],
+                   "parallelism": f"row-partition x{world} (nnz-balanced), x replicated (RCCL broadcast)"},
+        "achieved_gbs": r["achieved_gbs"],
+        "roofline": roof,
+        "phases_ms": r.get("phases_ms"),
         "cpu_baseline": cpu,
         "streamed_bytes_model": streamed_bytes(info) if info["format"] == "bin" else None,
         # BIN's own byte floor: what this format could do on this GPU at best;
@@ -493,39 +637,27 @@ def main():
                                       r["event_ms_per_launch"])
                     if info["format"] == "bin" else None),
         "formats": results,
-        "gen_s": round(t_gen, 2),
-        "x_broadcast_ms": round(t_bcast * 1e3, 3) if distributed else None,
+        "per_rank": per_rank,
+        "gen_s": round(M["gen_s"], 2),
+        "x_broadcast_ms": round(M["bcast_s"] * 1e3, 3) if M["bcast_s"] is not None else None,
         "collective_ms": coll_ms,
         "iterative": iterative,
         "host_buffers": host_mode,
         "max_rel_err_vs_cpu": max_rel,
         "verify_max_rel": verify_rel,
+        "gather_ceilings_per_s": {"l2_table": gather_gps, "x_table": gather_x_gps},
     }
-    if shape_world != world:
-        out["emulated_world"] = shape_world
-        out["config"]["parallelism"] = f"EMULATED rank 0 of {shape_world} (development only)"
-    # roofline.traffic: PMC bytes per launch of this kernel/config -- the
-    # calibrated figure where one exists (FETCH_SIZE calibrated on a known
-    # byte count of the same access pattern), else raw FETCH+WRITE
-    key = traffic_key(args.config, rows, n_glob, r["kernel"])
-    for fname, kind in (("pmc_traffic_calibrated.json", "pmc_calibrated"), ("pmc_traffic.json", "pmc_raw")):
-        path = os.path.join(ROOT, "profiles", fname)
-        try:
-            t = json.load(open(path)) if os.path.exists(path) else {}
-        except ValueError:
-            t = {}
-        if key in t:
-            v = t[key]
-            out["roofline"]["traffic"] = v["bytes"] if isinstance(v, dict) else v
-            out["roofline"]["traffic_kind"] = kind
-            # the HBM bandwidth the kernels actually sustain: the profiled
-            # bytes of one launch over this run's launch time (BIN moves
-            # ~2.4x the algorithmic bytes; frac above prices only those)
-            tg = out["roofline"]["traffic"] / (r["event_ms_per_launch"] * 1e-3) / 1e9
-            out["roofline"]["traffic_gbs"] = tg
-            out["roofline"]["traffic_frac"] = tg / HBM_PEAK_GBS
-            out["roofline"]["traffic_frac_of_stream"] = tg / stream_gbs
-            break
+    if ctx.shape_world != world:
+        out["emulated_world"] = ctx.shape_world
+        out["config"]["parallelism"] = f"EMULATED rank 0 of {ctx.shape_world} (development only)"
+    plan.destroy()
+    del M, y_head
+    torch.cuda.empty_cache()
+
+    # configs 3 and 4 beside the N = 1 headline (BASELINE.json configs[2-3])
+    if world == 1 and not args.only_config and not args.sim_world and not args.rows and args.config == "c2":
+        out["configs"] = {c: extra_config(ctx, args, c, f, stream_gbs) for c, f in EXTRA_CONFIGS}
+
     if rank == 0:
         print(json.dumps(out), flush=True)
     if distributed:

@@ -18,9 +18,6 @@
  * x only on the first call (the reference driver never changes x,
  * src/main.cpp:36-102).  y is downloaded on every call (opt_cusparse.cpp:82).
  *
- * SPMV_HIP_PLACEMENT=search|vmm|plain picks the placement of the BIN product
- * buffer / DIA values (spmv_hip.h SPMV_PLACEMENT_*; default plain).
- *
  * Multi-GPU: SPMV_HIP_GPUS=N (set, N >= 1) makes OptimizeProblem build a dist plan
  * over devices 0..N-1 (spmv_dist_create_csr: nnz-balanced row ranges, one
  * plan per device, x broadcast and y all-gathered by RCCL over xGMI) and SpMV

@@ -51,7 +51,14 @@
 extern "C" {
 #endif
 
+/* Version 2 changed the layout of spmv_options_t (the bin_* / placement
+ * fields, round 2) and spmv_plan_info_t: a caller built against a version-1
+ * header passes structs of the wrong size and must be rebuilt.  Callers may
+ * check spmv_api_version() == SPMV_HIP_API_VERSION once at startup; the
+ * structs are only ever filled by spmv_options_default / spmv_plan_info of a
+ * library with the same version. */
 #define SPMV_HIP_API_VERSION 2
+int spmv_api_version(void);
 
 /* ---- status codes -------------------------------------------------------- */
 typedef enum spmv_status {
@@ -115,20 +122,18 @@ typedef struct spmv_options {
 #define SPMV_PLACEMENT_AUTO 0   /* = PLAIN                                           */
 #define SPMV_PLACEMENT_PLAIN 1  /* one hipMalloc, nothing timed: create holds no
                                    device memory beyond the plan's own            */
-#define SPMV_PLACEMENT_SEARCH 2 /* BIN products >= 32 MB, DIA values >= 256 MB: up to 8 candidates spread
-                                   over all free HBM, each timed with one launch
-                                   over a zero x, the fastest kept -- create
-                                   briefly holds most of the free device memory;
-                                   for callers that own the GPU (the bench)       */
-#define SPMV_PLACEMENT_VMM 3    /* hipMemCreate handles of 2 MB mapped into one
-                                   VA range                                       */
+#define SPMV_PLACEMENT_SEARCH 2 /* experiment (probe build only; the product library
+                                   returns SPMV_ERROR_NOT_SUPPORTED): up to 8
+                                   candidates spread over all free HBM, each timed
+                                   with one launch, the fastest kept              */
+#define SPMV_PLACEMENT_VMM 3    /* experiment (probe build only): hipMemCreate
+                                   handles of 2 MB mapped into one VA range       */
 
 /* Fill `opt` with defaults (AUTO format, current device, auto tuning). */
 void spmv_options_default(spmv_options_t *opt);
 
 /* Plan builds are untimed setup (OptimizeProblem, src/main.cpp:36).  They
- * allocate the plan's device arrays and nothing else, unless the options ask
- * for SPMV_PLACEMENT_SEARCH.
+ * allocate the plan's device arrays and nothing else.
  *
  * Plan from a host sorted COO (the reference SpMat, src/util.h:7-19).
  * Rows must be sorted ascending (LoadSparseMatrix guarantees it); columns
@@ -243,7 +248,10 @@ int spmv_time(spmv_plan_t plan, const double *x_dev, double *y_dev, int32_t iter
  * launches (the reference driver repeats SpMV until >= 1 s,
  * src/main.cpp:58-102).  Each rep computes exactly what spmv_execute does
  * (y bit-identical); x_dev and y_dev are fixed in the graph, so the caller
- * keeps them allocated until spmv_graph_destroy.  CSS plans (whose sweep
+ * keeps them allocated until spmv_graph_destroy.  A graph replays the plan's
+ * kernels on the plan's device arrays: destroy every graph of a plan before
+ * the plan (launching a graph whose plan is gone is undefined; destroying it
+ * is safe).  CSS plans (whose sweep
  * tags its progress flags with a per-launch sequence number) return
  * SPMV_ERROR_NOT_SUPPORTED. */
 typedef struct spmv_graph_s *spmv_graph_t;
@@ -323,7 +331,9 @@ int spmv_dist_create_csr(int32_t n_devices, const int32_t *devices, int64_t m, i
 
 /* y = A x with host x (n doubles) and host y (m doubles; NULL: the result
  * stays on the devices).  SPMV_X_STAGED: re-use the x broadcast by the
- * previous call (x may be NULL).  Returns after every device is done. */
+ * previous call (x may be NULL).  Returns after every device is done.  Any
+ * other flag bit (SPMV_X_DEVICE, SPMV_Y_DEVICE, SPMV_ASYNC) is refused with
+ * SPMV_ERROR_INVALID_VALUE. */
 int spmv_dist_execute(spmv_dist_t dist, const double *x, double *y, uint32_t flags);
 
 /* Per-step times over `iters` steps with the staged x: the local SpMV (max
@@ -403,7 +413,9 @@ typedef struct spmv_gen_spec {
 int spmv_gen_count(const spmv_gen_spec_t *spec, int64_t row_begin, int64_t row_end,
                    int64_t *nnz);
 /* Fill the CSR of rows [row_begin, row_end): row_ptr has (rows+1) entries and
- * starts at 0; columns are global, sorted within each row. */
+ * starts at 0; columns are global, sorted within each row.  With col_idx and
+ * val both NULL only row_ptr is filled (the row lengths are a function of
+ * (seed, row) alone -- what an nnz-balanced shard cut needs). */
 int spmv_gen_fill(const spmv_gen_spec_t *spec, int64_t row_begin, int64_t row_end,
                   int64_t *row_ptr, int32_t *col_idx, double *val);
 /* x[i] for global indices [begin, begin+count): U[0,1) (or {0..9}). */

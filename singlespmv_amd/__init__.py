@@ -41,6 +41,7 @@ FORMATS = {"auto": 0, "csr": 1, "crs": 1, "ell": 2, "ss": 3, "dia": 4, "hyb": 5,
 FORMAT_NAMES = {0: "auto", 1: "csr", 2: "ell", 3: "ss", 4: "dia", 5: "hyb", 6: "css", 7: "coo", 8: "jds", 9: "bin"}
 X_DEVICE, Y_DEVICE, ASYNC, X_STAGED = 0x1, 0x2, 0x4, 0x8
 GEN_UNIFORM, GEN_POWERLAW, GEN_BANDED = 1, 2, 3
+API_VERSION = 2  # SPMV_HIP_API_VERSION of the structs mirrored here
 
 _I32P = np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")
 _I64P = np.ctypeslib.ndpointer(np.int64, flags="C_CONTIGUOUS")
@@ -98,7 +99,7 @@ EXPORTS = [
     "spmv_plan_create_csr32", "spmv_plan_create_csr_device", "spmv_plan_create_csr32_device",
     "spmv_plan_destroy", "spmv_execute", "spmv_execute_alpha", "spmv_set_stream", "spmv_time",
     "spmv_profile", "spmv_phase_name", "spmv_stream_probe", "spmv_gather_probe", "spmv_plan_info",
-    "spmv_status_string", "spmv_last_error", "spmv_load_mtx", "spmv_load_mtx_csr", "spmv_free_host",
+    "spmv_api_version", "spmv_status_string", "spmv_last_error", "spmv_load_mtx", "spmv_load_mtx_csr", "spmv_free_host",
     "spmv_srand", "spmv_rand_vector", "spmv_verify_coo", "spmv_coo_to_csr", "spmv_gen_count",
     "spmv_gen_fill", "spmv_gen_vector", "spmv_partition_rows", "spmv_save_csr_bin",
     "spmv_load_csr_bin", "spmv_lds_order_probe", "spmv_dist_layout", "spmv_dist_create_csr",
@@ -118,6 +119,9 @@ def lib():
         raise SpmvError(f"{LIB_PATH} missing: run `make` (or __graft_entry__.build()) first; "
                         "there is no CPU fallback")
     L = C.CDLL(LIB_PATH)
+    # the ctypes structs below mirror version 2 of include/spmv_hip.h
+    if L.spmv_api_version() != API_VERSION:
+        raise SpmvError(f"{LIB_PATH} implements C-ABI version {L.spmv_api_version()}, this mirror {API_VERSION}")
     vp, i32, i64, f64 = C.c_void_p, C.c_int32, C.c_int64, C.c_double
     L.spmv_options_default.argtypes = [C.POINTER(Options)]
     L.spmv_plan_create_coo.argtypes = [i32, i32, i32, vp, vp, vp, C.POINTER(Options), C.POINTER(vp)]
@@ -655,6 +659,15 @@ def generate_csr(spec: GenSpec, row_begin: int = 0, row_end: Optional[int] = Non
     _check(L.spmv_gen_fill(C.byref(spec), row_begin, re, rp, col.ctypes.data, val.ctypes.data),
            "spmv_gen_fill")
     return rp, col[:nnz.value], val[:nnz.value]
+
+
+def generate_row_ptr(spec: GenSpec, row_begin: int = 0, row_end: Optional[int] = None) -> np.ndarray:
+    """row_ptr (int64, from 0) of global rows [row_begin, row_end) without
+    the entries: spmv_gen_fill with col_idx = val = NULL."""
+    re = spec.m if row_end is None else row_end
+    rp = np.empty(re - row_begin + 1, np.int64)
+    _check(lib().spmv_gen_fill(C.byref(spec), row_begin, re, rp, None, None), "spmv_gen_fill")
+    return rp
 
 
 def generate_vector(n: int, seed: int = 43, begin: int = 0, integer_values=False) -> np.ndarray:

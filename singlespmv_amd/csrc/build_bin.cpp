@@ -141,7 +141,9 @@ static int bin_params(spmv_plan_s *p, const spmv_options_t &o, int64_t m, int64_
 // (its nnz; a long row: its run pieces, about one per strip it touches)
 static int64_t bin_long_threshold(const spmv_options_t &o, const int64_t *rp, int64_t m, int64_t nnz, int64_t S) {
     if (o.bin_long_len < 0 || o.bin_groups > 1 || nnz == 0) return 0;
-    if (nnz + nnz / 2 + ((int64_t)S << 6) >= ((int64_t)1 << 31)) return 0;  // product positions are int31
+    // product positions are int31 in lcode: a cheap early out here, the
+    // exact check on the finished layout in bin_layout
+    if (nnz + nnz / 2 + ((int64_t)S << 6) >= ((int64_t)1 << 31)) return 0;
     const int64_t LL = o.bin_long_len > 0 ? o.bin_long_len : std::max<int64_t>(128, S);
     int64_t lnnz = 0;
 #pragma omp parallel for schedule(static) reduction(+ : lnnz)
@@ -574,6 +576,7 @@ static int alloc_prod_plain(spmv_plan_s *p, size_t prod_bytes) {
     return SPMV_SUCCESS;
 }
 
+#ifdef SPMV_PROBES
 // SPMV_PLACEMENT_SEARCH: keep the fastest of up to K candidates, each timed
 // with a Mul pass over a zero x at build time (results never depend on it).
 // Up to 8 candidates: best-of-4 still left 5 of 9 config-2 plans in the slow
@@ -663,22 +666,24 @@ static int bin_place_search(spmv_plan_s *p, int64_t n, size_t prod_bytes) {
     B.placement_ms.assign(t.begin(), t.end());
     return SPMV_SUCCESS;
 }
+#endif  // SPMV_PROBES
 
 static int bin_place_prod(spmv_plan_s *p, int64_t n, size_t prod_bytes, const spmv_options_t &o) {
     BinDev &B = p->bin;
     int mode = o.placement;
-    SPMV_CHECK_ARG(mode >= SPMV_PLACEMENT_AUTO && mode <= SPMV_PLACEMENT_VMM, "unknown placement mode");
+    SPMV_RETURN_IF(placement_mode_check(mode));
     if (const char *e = probe_env("SPMV_PLACEMENT_MODE")) mode = std::atoi(e);
     // AUTO = one plain allocation: no transient memory beyond the plan.  The
-    // search is opt-in (SPMV_PLACEMENT_SEARCH) -- it is the only method that
-    // found the Mul's fast mode reliably, but it briefly holds most of the
-    // free HBM; VMM 2-MB handles were fast on some boxes and not on others
+    // search (probe build only) is the only method that found the Mul's fast
+    // mode reliably, but it briefly holds most of the free HBM; VMM 2-MB
+    // handles were fast on some boxes and not on others
     // (profiles/round2/placement/, DESIGN §4a "Placement").
     if (mode == SPMV_PLACEMENT_AUTO) mode = SPMV_PLACEMENT_PLAIN;
     // the Mul of a 184 MB product buffer (config 3 with long rows) varies 0.118-0.151 ms
     // by placement as much as config 2's does: search from 32 MB
     if (mode == SPMV_PLACEMENT_SEARCH && prod_bytes < ((size_t)32 << 20)) mode = SPMV_PLACEMENT_PLAIN;
     B.placement = mode;
+#ifdef SPMV_PROBES
     if (mode == SPMV_PLACEMENT_SEARCH) return bin_place_search(p, n, prod_bytes);
     if (mode == SPMV_PLACEMENT_VMM) {
         size_t chunk = (size_t)2 << 20;
@@ -688,6 +693,7 @@ static int bin_place_prod(spmv_plan_s *p, int64_t n, size_t prod_bytes, const sp
         B.prod = (double *)q;
         return SPMV_SUCCESS;
     }
+#endif
     return alloc_prod_plain(p, prod_bytes);
 }
 
@@ -759,6 +765,51 @@ static int bin_finish(spmv_plan_s *p, int64_t n, const BinLayout &L, const spmv_
     return SPMV_SUCCESS;
 }
 
+// The run path packs a piece's product position into bits 0-30 of its
+// lcode word (bit 31 = piece start), so every position -- the trash line
+// past the runs included -- must stay below 2^31.  That is known exactly only
+// once the layout exists: the segments' padding can be several times nnz
+// when segments are short (up to PAD - 1 per 1-entry segment).
+constexpr int64_t kBinLongPosLimit = (int64_t)1 << 31;
+
+// The host layout of A (row bins, segment counts, offsets).  Long rows take
+// the run path when their product positions fit lcode; otherwise the layout
+// is redone without it (every row then stays in the segments, bit-exact).
+static int bin_layout(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o, BinLayout &L,
+                      int64_t pos_limit) {
+    BinDev &B = p->bin;
+    int64_t LL = bin_long_threshold(o, A.row_ptr, A.m, A.nnz, std::max<int64_t>(1, (A.n + B.strip - 1) / B.strip));
+    for (;;) {
+        L = BinLayout();
+        L.S = std::max<int64_t>(1, (A.n + B.strip - 1) / B.strip);
+        L.LL = LL;
+        B.long_rows = 0;
+        if (L.LL > 0) {
+            bin_long_prep(A, B.strip, L);
+            for (int64_t r = 0; r < A.m; ++r) B.long_rows += L.is_long(A.row_ptr, r) ? 1 : 0;
+        }
+        SPMV_RETURN_IF(bin_rows(p, A.row_ptr, A.m, A.n, L));
+        // segment sizes (bin b, strip s); long rows are not in the segments
+        const int64_t S = L.S, NB = L.NB, C = B.strip;
+        L.cnt.assign((size_t)(NB * S), 0);
+#pragma omp parallel for schedule(dynamic, 16)
+        for (int64_t b = 0; b < NB; ++b) {
+            int32_t *cb = L.cnt.data() + b * S;
+            for (int64_t r = L.row0[(size_t)b]; r < L.row0[(size_t)b + 1]; ++r) {
+                if (L.is_long(A.row_ptr, r)) continue;
+                for (int64_t j = A.row_ptr[r]; j < A.row_ptr[r + 1]; ++j) ++cb[A.col[j] / C];
+            }
+        }
+        if (L.LL > 0) bin_long_count(L);
+        bin_offsets(p, o, L);
+        if (L.LL > 0 && L.TRASH + L.PAD > pos_limit) {
+            LL = 0;  // positions would wrap in lcode: no run path
+            continue;
+        }
+        return SPMV_SUCCESS;
+    }
+}
+
 int build_bin(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
     BinDev &B = p->bin;
     SPMV_RETURN_IF(bin_params(p, o, A.m, A.n, A.nnz));
@@ -767,26 +818,7 @@ int build_bin(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
         return SPMV_SUCCESS;
     }
     BinLayout L;
-    L.S = std::max<int64_t>(1, (A.n + B.strip - 1) / B.strip);
-    L.LL = bin_long_threshold(o, A.row_ptr, A.m, A.nnz, L.S);
-    if (L.LL > 0) {
-        bin_long_prep(A, B.strip, L);
-        for (int64_t r = 0; r < A.m; ++r) B.long_rows += L.is_long(A.row_ptr, r) ? 1 : 0;
-    }
-    SPMV_RETURN_IF(bin_rows(p, A.row_ptr, A.m, A.n, L));
-    // segment sizes (bin b, strip s); long rows are not in the segments
-    const int64_t S = L.S, NB = L.NB, C = B.strip;
-    L.cnt.assign((size_t)(NB * S), 0);
-#pragma omp parallel for schedule(dynamic, 16)
-    for (int64_t b = 0; b < NB; ++b) {
-        int32_t *cb = L.cnt.data() + b * S;
-        for (int64_t r = L.row0[(size_t)b]; r < L.row0[(size_t)b + 1]; ++r) {
-            if (L.is_long(A.row_ptr, r)) continue;
-            for (int64_t j = A.row_ptr[r]; j < A.row_ptr[r + 1]; ++j) ++cb[A.col[j] / C];
-        }
-    }
-    if (L.LL > 0) bin_long_count(L);
-    bin_offsets(p, o, L);
+    SPMV_RETURN_IF(bin_layout(p, A, o, L, kBinLongPosLimit));
     SPMV_RETURN_IF(bin_fill_host(p, A, L));
     return bin_finish(p, A.n, L, o);
 }

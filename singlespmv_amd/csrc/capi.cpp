@@ -145,6 +145,8 @@ using namespace spmv;
 
 extern "C" {
 
+int spmv_api_version(void) { return SPMV_HIP_API_VERSION; }
+
 void spmv_options_default(spmv_options_t *o) {
     if (!o) return;
     std::memset(o, 0, sizeof(*o));
@@ -388,7 +390,8 @@ int spmv_time(spmv_plan_t p, const double *x_dev, double *y_dev, int32_t iters, 
 }  // extern "C"
 
 struct spmv_graph_s {
-    spmv_plan_t plan = nullptr;
+    spmv_plan_t plan = nullptr;  // launches use the plan's stream; destroy does not touch it
+    int device = 0;              // the plan's device, for destroy
     hipGraph_t graph = nullptr;
     hipGraphExec_t exec = nullptr;
     int32_t reps = 0;
@@ -462,6 +465,7 @@ int spmv_graph_create(spmv_plan_t p, const double *x_dev, double *y_dev, int32_t
         return SPMV_ERROR_OUT_OF_MEMORY;
     }
     G->plan = p;
+    G->device = p->device;
     G->graph = g;
     G->exec = ex;
     G->reps = reps;
@@ -499,7 +503,9 @@ int spmv_graph_time(spmv_graph_t G, int32_t launches, double *ms) {
 
 int spmv_graph_destroy(spmv_graph_t G) {
     if (!G) return SPMV_SUCCESS;
-    if (G->plan) (void)bind_device(G->plan);
+    // the plan may already be gone (the header asks for graphs first, but a
+    // destroy must not read it): bind the recorded device only
+    (void)hipSetDevice(G->device);
     if (G->exec) (void)hipGraphExecDestroy(G->exec);
     if (G->graph) (void)hipGraphDestroy(G->graph);
     delete G;

@@ -229,6 +229,11 @@ int spmv_dist_create_csr(int32_t n_devices, const int32_t *devices, int64_t m, i
 
 int spmv_dist_execute(spmv_dist_t d, const double *x, double *y, uint32_t flags) {
     SPMV_CHECK_ARG(d != nullptr, "dist plan is NULL");
+    // host x / host y only (x is uploaded to the first device and broadcast,
+    // y comes back from the all-gathered copy there); the device-pointer and
+    // asynchronous flags of spmv_execute are not implemented here
+    SPMV_CHECK_ARG((flags & ~(uint32_t)SPMV_X_STAGED) == 0,
+                   "spmv_dist_execute takes host x / y: flags other than SPMV_X_STAGED are not supported");
     const bool staged = (flags & SPMV_X_STAGED) != 0;
     SPMV_CHECK_ARG(staged || x != nullptr || d->n == 0, "x is NULL");
     SPMV_CHECK_ARG(!staged || d->x_staged, "SPMV_X_STAGED without a previously broadcast x");
@@ -257,41 +262,51 @@ int spmv_dist_execute(spmv_dist_t d, const double *x, double *y, uint32_t flags)
 int spmv_dist_time(spmv_dist_t d, int32_t iters, double *spmv_ms, double *gather_ms) {
     SPMV_CHECK_ARG(d != nullptr && iters > 0 && spmv_ms && gather_ms, "bad arguments");
     SPMV_CHECK_ARG(d->x_staged, "spmv_dist_time needs an x broadcast by spmv_dist_execute first");
+    // one exit path: the first error is kept, every event created is
+    // destroyed, and nothing is recorded or read after an error
     std::vector<hipEvent_t> ev((size_t)d->nd * 3, nullptr);
     int st = SPMV_SUCCESS;
+    auto hip = [&](hipError_t e, const char *what) {
+        if (st == SPMV_SUCCESS && e != hipSuccess) {
+            set_error(std::string(what) + ": " + hipGetErrorString(e));
+            (void)hipGetLastError();
+            st = SPMV_ERROR_HIP;
+        }
+    };
     for (int k = 0; k < d->nd && st == SPMV_SUCCESS; ++k) {
-        SPMV_HIP_TRY(hipSetDevice(d->devs[k]));
-        for (int j = 0; j < 3; ++j) SPMV_HIP_TRY(hipEventCreate(&ev[(size_t)k * 3 + j]));
+        hip(hipSetDevice(d->devs[k]), "hipSetDevice");
+        for (int j = 0; j < 3 && st == SPMV_SUCCESS; ++j) hip(hipEventCreate(&ev[(size_t)k * 3 + j]), "hipEventCreate");
     }
-    SPMV_RETURN_IF(dist_sync(d));
-    for (int k = 0; k < d->nd; ++k) {
-        SPMV_HIP_TRY(hipSetDevice(d->devs[k]));
-        SPMV_HIP_TRY(hipEventRecord(ev[(size_t)k * 3], d->streams[k]));
-    }
+    if (st == SPMV_SUCCESS) st = dist_sync(d);
+    auto mark = [&](int j) {
+        for (int k = 0; k < d->nd && st == SPMV_SUCCESS; ++k) {
+            hip(hipSetDevice(d->devs[k]), "hipSetDevice");
+            if (st == SPMV_SUCCESS) hip(hipEventRecord(ev[(size_t)k * 3 + j], d->streams[k]), "hipEventRecord");
+        }
+    };
+    mark(0);
     for (int i = 0; i < iters && st == SPMV_SUCCESS; ++i) st = dist_local_spmv(d);
-    for (int k = 0; k < d->nd; ++k) {
-        SPMV_HIP_TRY(hipSetDevice(d->devs[k]));
-        SPMV_HIP_TRY(hipEventRecord(ev[(size_t)k * 3 + 1], d->streams[k]));
-    }
+    mark(1);
     for (int i = 0; i < iters && st == SPMV_SUCCESS; ++i) st = dist_gather_y(d);
-    for (int k = 0; k < d->nd; ++k) {
-        SPMV_HIP_TRY(hipSetDevice(d->devs[k]));
-        SPMV_HIP_TRY(hipEventRecord(ev[(size_t)k * 3 + 2], d->streams[k]));
-    }
-    SPMV_RETURN_IF(dist_sync(d));
+    mark(2);
+    if (st == SPMV_SUCCESS) st = dist_sync(d);
     double a = 0, g = 0;
-    for (int k = 0; k < d->nd; ++k) {
+    for (int k = 0; k < d->nd && st == SPMV_SUCCESS; ++k) {
         float f1 = 0, f2 = 0;
-        SPMV_HIP_TRY(hipEventElapsedTime(&f1, ev[(size_t)k * 3], ev[(size_t)k * 3 + 1]));
-        SPMV_HIP_TRY(hipEventElapsedTime(&f2, ev[(size_t)k * 3 + 1], ev[(size_t)k * 3 + 2]));
+        hip(hipEventElapsedTime(&f1, ev[(size_t)k * 3], ev[(size_t)k * 3 + 1]), "hipEventElapsedTime");
+        hip(hipEventElapsedTime(&f2, ev[(size_t)k * 3 + 1], ev[(size_t)k * 3 + 2]), "hipEventElapsedTime");
         a = std::max(a, (double)f1);
         g = std::max(g, (double)f2);
-        (void)hipSetDevice(d->devs[k]);
-        for (int j = 0; j < 3; ++j) (void)hipEventDestroy(ev[(size_t)k * 3 + j]);
     }
+    for (int k = 0; k < d->nd; ++k) {
+        (void)hipSetDevice(d->devs[k]);
+        for (int j = 0; j < 3; ++j)
+            if (ev[(size_t)k * 3 + j]) (void)hipEventDestroy(ev[(size_t)k * 3 + j]);
+    }
+    if (st != SPMV_SUCCESS) return st;
     *spmv_ms = a / iters;
     *gather_ms = g / iters;
-    return st;
+    return SPMV_SUCCESS;
 }
 
 int spmv_dist_info(spmv_dist_t d, int32_t *n_devices, int64_t *cuts, spmv_plan_t *plans) {

@@ -590,12 +590,17 @@ static bool dia_offsets(const HostCsr &A, int max_diags, double max_fill, std::v
 static int dia_placement(spmv_plan_s *p, int64_t m, int64_t n, size_t bytes, const spmv_options_t &o) {
     DiaDev &d = p->dia;
     int mode = o.placement;
-    SPMV_CHECK_ARG(mode >= SPMV_PLACEMENT_AUTO && mode <= SPMV_PLACEMENT_VMM, "unknown placement mode");
+    SPMV_RETURN_IF(placement_mode_check(mode));
     if (const char *e = probe_env("SPMV_PLACEMENT_MODE")) mode = std::atoi(e);
-    if (mode == SPMV_PLACEMENT_AUTO) mode = SPMV_PLACEMENT_PLAIN;  // the search is opt-in, as BIN's
+    if (mode == SPMV_PLACEMENT_AUTO) mode = SPMV_PLACEMENT_PLAIN;  // the search: probe build only, as BIN's
     if (mode == SPMV_PLACEMENT_SEARCH && bytes < ((size_t)256 << 20)) mode = SPMV_PLACEMENT_PLAIN;
     d.placement = mode;
     if (mode == SPMV_PLACEMENT_PLAIN) return SPMV_SUCCESS;
+#ifndef SPMV_PROBES
+    (void)m;
+    (void)n;
+    return SPMV_SUCCESS;
+#else
     if (mode == SPMV_PLACEMENT_VMM) {  // move the values into a VMM mapping
         size_t chunk = (size_t)2 << 20;
         if (const char *e = probe_env("SPMV_VMM_CHUNK_MB")) chunk = (size_t)std::max(1, std::atoi(e)) << 20;
@@ -680,6 +685,7 @@ static int dia_placement(spmv_plan_s *p, int64_t m, int64_t n, size_t bytes, con
         std::fprintf(stderr, " -> %zu\n", best);
     }
     return st;
+#endif  // SPMV_PROBES
 }
 
 int build_dia(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {

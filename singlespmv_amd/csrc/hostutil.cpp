@@ -132,6 +132,11 @@ int spmv_gen_fill(const spmv_gen_spec_t *s, int64_t rb, int64_t re, int64_t *row
         row_ptr[i + 1] = len;
     }
     for (int64_t i = 0; i < rows; ++i) row_ptr[i + 1] += row_ptr[i];
+    if (col_idx == nullptr && val == nullptr) {  // row pointers only (nnz-balanced shard cuts)
+        delete pl;
+        return SPMV_SUCCESS;
+    }
+    SPMV_CHECK_ARG(col_idx != nullptr && val != nullptr, "col_idx / val is NULL");
     const bool intv = s->integer_values != 0;
 #pragma omp parallel for schedule(dynamic, 1024)
     for (int64_t i = 0; i < rows; ++i) {

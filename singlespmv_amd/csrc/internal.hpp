@@ -57,6 +57,20 @@ inline const char *probe_env(const char *name) {
 #endif
 }
 
+// The placement experiments (SPMV_PLACEMENT_SEARCH, _VMM) exist
+// only in the probe build: the product library makes one plain allocation,
+// holds no transient device memory at create and times nothing.
+inline int placement_mode_check(int mode) {
+    SPMV_CHECK_ARG(mode >= SPMV_PLACEMENT_AUTO && mode <= SPMV_PLACEMENT_VMM, "unknown placement mode");
+#ifndef SPMV_PROBES
+    if (mode == SPMV_PLACEMENT_SEARCH || mode == SPMV_PLACEMENT_VMM) {
+        set_error("placement search / VMM are experiments of the probe build (make probes)");
+        return SPMV_ERROR_NOT_SUPPORTED;
+    }
+#endif
+    return SPMV_SUCCESS;
+}
+
 // ---- device memory owned by a plan --------------------------------------
 // Plain hipMalloc allocations, plus buffers mapped through the HIP virtual
 // memory API (hipMemCreate + hipMemMap: the BIN product buffer, see

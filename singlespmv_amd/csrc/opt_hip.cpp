@@ -63,13 +63,6 @@ void OptimizeProblem(const SpMat &A, const Vec &x, SpMatOpt &A_opt, VecOpt &x_op
     spmv_options_t o;
     spmv_options_default(&o);
     o.format = opt_hip_format();
-    // SPMV_HIP_PLACEMENT=search: the build-time placement search for the BIN
-    // product buffer / DIA values (spmv_hip.h SPMV_PLACEMENT_SEARCH)
-    if (const char *pl = std::getenv("SPMV_HIP_PLACEMENT")) {
-        if (!strcasecmp(pl, "search")) o.placement = SPMV_PLACEMENT_SEARCH;
-        else if (!strcasecmp(pl, "vmm")) o.placement = SPMV_PLACEMENT_VMM;
-        else if (!strcasecmp(pl, "plain")) o.placement = SPMV_PLACEMENT_PLAIN;
-    }
     // SPMV_HIP_EXACT=1: every row the sequential opt_crs sum bit for bit --
     // BIN keeps long power-law rows off its run path (spmv_hip.h bin_long_len)
     if (const char *ex = std::getenv("SPMV_HIP_EXACT"))

@@ -26,10 +26,29 @@ def row_range(m: int, rank: int, world: int, row_ptr=None) -> Tuple[int, int]:
     return min(m, rank * per), min(m, (rank + 1) * per)
 
 
-def shard_generated(spec, rank: int, world: int):
-    """Generate only this rank's rows of a synthetic matrix (equal blocks)."""
+def generated_cuts(spec, world: int) -> np.ndarray:
+    """nnz-balanced cut rows of a synthetic matrix (SURVEY §8e "Partition":
+    cuts[k] = first row with row_ptr[r] >= k*nnz/world, as spmv_partition_rows
+    and dist.cpp's spmv_dist_layout cut a caller's CSR).  The row lengths are
+    a function of (seed, row) alone, so the global row_ptr comes from the
+    generator without building any entries; a uniform matrix (equal rows,
+    equal nnz) is cut into equal row blocks directly."""
+    from . import GEN_UNIFORM, generate_row_ptr, partition_rows
+    if world <= 1:
+        return np.array([0, spec.m], np.int64)
+    if spec.kind == GEN_UNIFORM:
+        per = (spec.m + world - 1) // world
+        return np.minimum(np.arange(world + 1, dtype=np.int64) * per, spec.m)
+    return partition_rows(generate_row_ptr(spec), world)
+
+
+def shard_generated(spec, rank: int, world: int, cuts=None):
+    """Generate only this rank's rows of a synthetic matrix: the rank's
+    nnz-balanced row range (generated_cuts) and its CSR."""
     from . import generate_csr
-    r0, r1 = row_range(spec.m, rank, world)
+    if cuts is None:
+        cuts = generated_cuts(spec, world)
+    r0, r1 = int(cuts[rank]), int(cuts[rank + 1])
     rp, col, val = generate_csr(spec, r0, r1)
     return (r0, r1), rp, col, val
 
@@ -90,6 +109,19 @@ def sum_over_ranks(values, device):
     if _dist_on():
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return [float(v) for v in t.tolist()]
+
+
+def gather_floats(values, device):
+    """Every rank's short list of floats (equal lengths), in rank order."""
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor(values, dtype=torch.float64,
+                     device="cpu" if _CPU_COLLECTIVES else device)
+    if not _dist_on():
+        return [[float(v) for v in t.tolist()]]
+    parts = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(parts, t)
+    return [[float(v) for v in p.tolist()] for p in parts]
 
 
 def gather_y(y_local, rows_per_rank: int):

@@ -349,6 +349,53 @@ int main() {
                     }
                 }
     }
+    // ---- the run path's positions must fit lcode's 31 bits (build_bin.cpp
+    // bin_layout): a very sparse power-law shape (mostly 1-2 entry rows, so
+    // short padded segments, plus long rows) laid out once with the
+    // real limit and once with a limit just below its trash line's end --
+    // the second must drop the run path (LL = 0) and stay a valid layout.
+    {
+        const int64_t m = 20000, n = 300000;
+        std::vector<int64_t> rp(m + 1, 0);
+        std::vector<int32_t> col;
+        for (int64_t r = 0; r < m; ++r) {
+            const int64_t len = (rng() % 100 == 0) ? 300 + (int64_t)(rng() % 1700) : 1 + (int64_t)(rng() % 2);
+            std::vector<int32_t> c(len);
+            for (auto &v : c) v = (int32_t)(rng() % n);
+            std::sort(c.begin(), c.end());
+            col.insert(col.end(), c.begin(), c.end());
+            rp[r + 1] = rp[r] + len;
+        }
+        const int64_t nnz = rp[m];
+        std::vector<double> val((size_t)nnz), x((size_t)n);
+        for (auto &v : val) v = (double)(rng() >> 11) * 0x1.0p-53;
+        for (auto &v : x) v = (double)(rng() >> 11) * 0x1.0p-53;
+        HostCsr A{m, n, nnz, rp.data(), col.data(), val.data()};
+        spmv_plan_s p;
+        BinDev &B = p.bin;
+        B.strip = 3001;
+        B.sum_waves = 4;
+        B.max_rows = bin_max_rows(B.sum_waves);
+        B.sum_u = 32;
+        B.pad_log = 4;
+        B.nwg1 = B.nwg2 = 256;
+        spmv_options_t o;
+        std::memset(&o, 0, sizeof(o));
+        o.bin_long_len = 64;
+        BinLayout L;
+        if (bin_layout(&p, A, o, L, kBinLongPosLimit) != SPMV_SUCCESS) return fail("bin_layout");
+        if (L.LL != 64) return fail("run path expected", L.LL);
+        const int64_t end = L.TRASH + L.PAD;
+        BinLayout K;
+        if (bin_layout(&p, A, o, K, end - 1) != SPMV_SUCCESS) return fail("bin_layout (limit)");
+        if (K.LL != 0 || K.E < nnz || p.bin.long_rows != 0) return fail("run path not dropped", K.LL, K.E);
+        BinHostArrays H;
+        bin_fill_arrays(B, A, K, H);
+        if (emulate(B, A, K, H, x)) return fail("emulation (run path dropped)");
+        BinLayout J;  // exactly at the limit: kept
+        if (bin_layout(&p, A, o, J, end) != SPMV_SUCCESS || J.LL != 64) return fail("limit boundary", J.LL);
+        cases += 3;
+    }
     std::printf("ok %d\n", cases);
     return 0;
 }

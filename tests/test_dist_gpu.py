@@ -46,7 +46,32 @@ def test_two_rank_bench_flow(config, fmts, launch):
     assert d["config"]["nnz_total"] >= d["config"]["nnz_per_gpu"]
     assert d["config"]["m"] == 300000 and d["collective_ms"] is not None
     assert d["verify_max_rel"] is not None and d["verify_max_rel"] <= 1e-12, d["verify_max_rel"]
-    assert d["iterative"] is not None and d["iterative"]["ms_per_iter"] > 0
+    if config == "c2":  # equal slices: the iterative all_gather(y -> next x) step
+        assert d["iterative"] is not None and d["iterative"]["ms_per_iter"] > 0
+    assert [p["rank"] for p in d["per_rank"]] == [0, 1]
+
+
+@pytest.mark.parametrize("ranks", [2, 4])
+def test_power_law_shards_are_nnz_balanced(ranks):
+    """bench.py --config c3 --gpus 2/4 --verify: the generated shards are cut
+    nnz-balanced, every rank's nnz within 1 % of nnz / N, and the
+    gathered y matches the oracle over the whole matrix."""
+    env = dict(os.environ, BENCH_DIST_BACKEND="gloo")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(ranks), "--steps", "3", "--warmup", "1",
+           "--trials", "1", "--rows", "500000", "--config", "c3", "--formats", "auto", "--verify", "--no-cpu"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-3000:]
+    d = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
+    nnz = [p["nnz"] for p in d["per_rank"]]
+    assert len(nnz) == ranks and sum(nnz) == d["config"]["nnz_total"]
+    mean = d["config"]["nnz_total"] / ranks
+    assert max(abs(v - mean) for v in nnz) <= 0.01 * mean, nnz
+    rows = [p["rows"] for p in d["per_rank"]]
+    assert rows[0][0] == 0 and rows[-1][1] == d["config"]["m"]
+    assert all(rows[k][1] == rows[k + 1][0] for k in range(ranks - 1))
+    assert d["verify_max_rel"] is not None and d["verify_max_rel"] <= 1e-12, d["verify_max_rel"]
 
 
 def test_c_abi_dist_plan_one_device():

@@ -655,11 +655,10 @@ def test_bin_long_rows_run_path(long_len, opts):
 
 
 @pytest.mark.parametrize("opts", [{"bin_pad": 8}, {"bin_pad": 16}, {"bin_pad": 32}, {"bin_sum_waves": 2},
-                                  {"bin_sum_waves": 4}, {"bin_sum_waves": 8}, {"placement": "plain"},
-                                  {"placement": "vmm"}, {"placement": "search"}])
+                                  {"bin_sum_waves": 4}, {"bin_sum_waves": 8}, {"placement": "plain"}])
 def test_bin_layout_options(opts):
     """The layout options (product-line padding, Sum waves / bin rows) and the
-    product-buffer placements change speed only."""
+    explicit plain placement change speed only."""
     m = 120_000
     rp, col, val = _bin_matrix("powerlaw", m, m, seed=41)
     x = sp.generate_vector(m, seed=43)
@@ -701,8 +700,9 @@ def _create_peak_drop(make):
 def test_plan_create_holds_only_the_plan(fmt, kind):
     """AUTO placement: while a large BIN / DIA plan is created, free device
     memory never drops by more than the plan's own bytes (+128 MB of runtime
-    slack); ten plans built in a row behave the same.  The opt-in SEARCH
-    placement times several candidates (and reports them in plan info)."""
+    slack); ten plans built in a row behave the same.  The placement
+    experiments (SEARCH, VMM) are refused by the product library: they exist
+    only in the probe build."""
     m = 4_000_000
     spec = sp.gen_spec(kind, m, per_row=16, band_lo=-20, band_hi=20, seed=21)
     rp, col, val = sp.generate_csr(spec)
@@ -712,10 +712,9 @@ def test_plan_create_holds_only_the_plan(fmt, kind):
         assert info["format"] == fmt and info["placement"] == "plain"
         assert drop <= info["device_bytes"] + (128 << 20), (i, drop, info["device_bytes"])
         plan.destroy()
-    plan = sp.Plan.from_csr(m, m, rp, col, val, fmt, placement="search")
-    info = plan.info()
-    assert info["placement"] == "search" and info["placement_candidates"] >= 2
-    assert 0 < info["placement_best_ms"] <= info["placement_worst_ms"]
+    for mode in ("search", "vmm"):
+        with pytest.raises(sp.SpmvError, match="probe build"):
+            sp.Plan.from_csr(m, m, rp, col, val, fmt, placement=mode)
 
 
 def test_experiment_switches_do_not_reach_the_product_library(monkeypatch):

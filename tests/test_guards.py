@@ -11,6 +11,7 @@
   device before any address reaches the C-ABI;
 * bench.py --gpus N self-launches N ranks through torch.distributed.run.
 """
+import json
 import os
 import re
 import subprocess
@@ -127,6 +128,42 @@ def test_bench_self_launch(monkeypatch):
     monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "4"])
     monkeypatch.setenv("WORLD_SIZE", "2")
     assert bench.self_launch(bench.parse()) == 2  # mismatched launcher: refuse
+
+
+def test_bench_self_launch_parent_stays_off_hip(tmp_path):
+    """The self-launching parent counts GPUs from the KFD topology and spawns
+    the launcher without loading HIP: in a fresh interpreter, a fake launcher
+    reads the parent's /proc/self/maps at the spawn -- no libamdhip64 (nor
+    torch) may be mapped.  The fake topology holds one CPU node and two GPU
+    nodes (simd_count > 0); HIP_VISIBLE_DEVICES caps the count."""
+    topo = tmp_path / "nodes"
+    for i, simds in enumerate((0, 256, 256)):
+        (topo / str(i)).mkdir(parents=True)
+        (topo / str(i) / "properties").write_text(f"cpu_cores_count 8\nsimd_count {simds}\n")
+    prog = (
+        "import sys, json; sys.path.insert(0, %r); import bench\n"
+        "seen = {}\n"
+        "def fake(cmd, env=None):\n"
+        "    maps = open('/proc/self/maps').read()\n"
+        "    seen.update(hip='libamdhip64' in maps, torch='libtorch' in maps, cmd=cmd)\n"
+        "    return 5\n"
+        "sys.argv = ['bench.py', '--gpus', '2', '--rows', '1000']\n"
+        "rc = bench.self_launch(bench.parse(), runner=fake)\n"
+        "print(json.dumps(dict(rc=rc, n=bench.visible_gpu_count(), **seen)))\n" % ROOT)
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK",
+                                                            "HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES",
+                                                            "CUDA_VISIBLE_DEVICES", "BENCH_DIST_BACKEND")}
+    env["BENCH_KFD_TOPOLOGY"] = str(topo)
+    out = subprocess.run([sys.executable, "-c", prog], env=env, capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    res = json.loads(out.stdout.strip().splitlines()[-1])
+    assert res["rc"] == 5 and res["n"] == 2 and "--nproc-per-node=2" in res["cmd"]
+    assert res["hip"] is False and res["torch"] is False
+    # one visible device: --gpus 2 is refused before any spawn
+    env["HIP_VISIBLE_DEVICES"] = "0"
+    out = subprocess.run([sys.executable, "-c", prog], env=env, capture_output=True, text=True, timeout=120)
+    res = json.loads(out.stdout.strip().splitlines()[-1])
+    assert res["rc"] == 2 and res["n"] == 1 and "cmd" not in res
 
 
 def test_traffic_keys_name_the_shape():

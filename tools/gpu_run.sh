@@ -1,0 +1,64 @@
+#!/bin/bash
+# One gpurun call = one list of named steps, each under its own time limit,
+# stopping at the first failure (a fault, abort or timeout ends the call).
+#
+#   gpurun --timeout 1200 -- bash tools/gpu_run.sh <out> <step> [<step> ...]
+#
+# Output lands in gpurun_out/<out>/<step>.{json,log,err}.  Steps:
+#   tests             full GPU suite (pytest -m gpu)
+#   smoke             __graft_entry__.smoke()
+#   bench             the driver's default command (bench.py --steps 20 --warmup 5)
+#   bench_c3|bench_c4 bench.py --config c3|c4 (single config)
+#   simN              emulated rank 0 of an N-GPU job (bench.py --sim-world N --no-cpu)
+#   prof_c2|prof_c3|prof_c4|prof_simN
+#                     rocprofv3 kernel trace + FETCH_SIZE / WRITE_SIZE passes
+#                     (tools/profile_round.sh) of the headline plan of that shape
+#   gloo2_c3          the self-launched 2-rank bench (gloo, one GPU) with --verify
+#   py:<script args>  python3 -u <script args> (a tools/ probe), stdout to <step>.log
+# This replaces round 2's one-off tools/r2_*.sh wrappers (profiles/round2/README.md).
+set -o pipefail
+OUTNAME=$1; shift
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out/$OUTNAME
+mkdir -p "$O"
+cd "$R"
+export PYTHONUNBUFFERED=1
+i=0
+for step in "$@"; do
+  i=$((i + 1))
+  tag=$(printf '%02d_%s' $i "$(echo "$step" | tr -c 'A-Za-z0-9_.-' '_' | cut -c1-40)")
+  echo "[$(date +%T)] step $tag" >&2
+  case "$step" in
+    tests)
+      timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+          > "$O/$tag.log" 2>&1 ;;
+    smoke)
+      timeout -k 10 180 python3 -c "import __graft_entry__ as g; g.smoke()" > "$O/$tag.log" 2>&1 ;;
+    bench)
+      timeout -k 10 500 python3 -u bench.py --steps 20 --warmup 5 > "$O/$tag.json" 2> "$O/$tag.err" ;;
+    bench_c3|bench_c4)
+      timeout -k 10 400 python3 -u bench.py --config "${step#bench_}" --only-config > "$O/$tag.json" 2> "$O/$tag.err" ;;
+    sim[0-9]*)
+      timeout -k 10 400 python3 -u bench.py --sim-world "${step#sim}" --no-cpu --only-config \
+          > "$O/$tag.json" 2> "$O/$tag.err" ;;
+    prof_c2|prof_c3|prof_c4)
+      timeout -k 10 1000 bash tools/profile_round.sh "${OUTNAME}_${step#prof_}" --config "${step#prof_}" \
+          --formats auto --only-config --steps 20 --warmup 5 --trials 3 > "$O/$tag.log" 2>&1 ;;
+    prof_sim[0-9]*)
+      timeout -k 10 1000 bash tools/profile_round.sh "${OUTNAME}_${step#prof_}" --sim-world "${step#prof_sim}" \
+          --formats auto --only-config --steps 20 --warmup 5 --trials 3 > "$O/$tag.log" 2>&1 ;;
+    gloo2_c3)
+      BENCH_DIST_BACKEND=gloo timeout -k 10 400 python3 -u bench.py --gpus 2 --config c3 --rows 500000 \
+          --formats auto --no-cpu --only-config --verify > "$O/$tag.json" 2> "$O/$tag.err" ;;
+    py:*)
+      # shellcheck disable=SC2086
+      timeout -k 10 600 python3 -u ${step#py:} > "$O/$tag.log" 2> "$O/$tag.err" ;;
+    *)
+      echo "unknown step $step" >&2; exit 64 ;;
+  esac
+  rc=$?
+  echo "[$(date +%T)] step $tag rc=$rc" >&2
+  if [ $rc -ne 0 ]; then
+    exit $rc
+  fi
+done

@@ -10,7 +10,6 @@
 //
 // Usage: spmv <matrix.mtx | gen:uniform:ROWS:PER | gen:banded:ROWS:HALF | gen:powerlaw:ROWS:MAXLEN>
 //             [--format crs|ell|ss|dia|hyb|css|coo|jds|bin|auto] [--resident] [--gpus N]
-//             [--placement plain|search|vmm]
 //
 // --gpus N spans N devices of the node through the drop-in's multi-GPU plan
 // (SPMV_HIP_GPUS, spmv_dist_*: nnz-balanced row ranges, RCCL broadcast of x,
@@ -72,14 +71,13 @@ int main(int argc, char **argv) {
     srand(3);  // src/main.cpp:18
     if (argc < 2) {
         std::printf("Usage: %s <matrix | gen:uniform:ROWS:PER | gen:banded:ROWS:HALF | gen:powerlaw:ROWS:MAXLEN> "
-                    "[--format crs|ell|ss|dia|hyb|css|coo|jds|bin|auto] [--resident] [--gpus N] [--placement plain|search|vmm]\n", argv[0]);
+                    "[--format crs|ell|ss|dia|hyb|css|coo|jds|bin|auto] [--resident] [--gpus N]\n", argv[0]);
         return 1;
     }
     const std::string matFile = argv[1];
     for (int i = 2; i < argc; ++i) {
         if (!std::strcmp(argv[i], "--format") && i + 1 < argc) setenv("SPMV_HIP_FORMAT", argv[++i], 1);
         else if (!std::strcmp(argv[i], "--resident")) setenv("SPMV_HIP_X_RESIDENT", "1", 1);
-        else if (!std::strcmp(argv[i], "--placement") && i + 1 < argc) setenv("SPMV_HIP_PLACEMENT", argv[++i], 1);
         else if (!std::strcmp(argv[i], "--gpus") && i + 1 < argc) {
             setenv("SPMV_HIP_GPUS", argv[++i], 1);
         }
