@@ -17,6 +17,9 @@ and the outputs of the reference plugins (y per format, VerifyResult flag).
                       (uniform 16/row, power-law, banded 64 diagonals,
                       integer-valued, edge cases), matrices built here with
                       numpy, y from the reference plugins.
+Every fixture also carries y_coo, y_jds, y_css and y_ss_pad: the outputs of
+the reference's opt_coo, opt_jds, opt_css and opt_ss OPTIMIZED+PADDING
+plugins (oracle/Makefile), the (f) rows of SURVEY §8.
 """
 import os
 import shutil
@@ -32,9 +35,16 @@ REF_TEST = "/root/reference/matrix/test"
 OUT = os.path.join(ROOT, "tests", "golden")
 
 
+# the (f) plugins and the SS PADDING variant run on every fixture (SURVEY
+# §8(c): they compile here and pass VERIFY): y_coo (omp atomic scatter --
+# its summation order follows the thread split, so it is compared within
+# 1e-12, not bitwise), y_jds, y_css (3 column blocks), y_ss_pad
+F_PLUGINS = ["coo", "jds", "css", "ss_pad"]
+
+
 def ref_outputs(m, n, row, col, val, x, y0, fmts):
     out = {}
-    for f in fmts:
+    for f in fmts + [f for f in F_PLUGINS if f not in fmts]:
         y, ok = oracle.ref_spmv(f, m, n, row, col, val, x, y_init=y0, calls=2)
         assert ok, f"reference VerifyResult failed for {f}"
         out[f"y_{f}"] = y

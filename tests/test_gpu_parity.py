@@ -107,6 +107,16 @@ def test_golden(name, fmt):
         assert_bin_rows(plan, y, rp, g["col"], g["val"], g["x"], what=name)
     if sequential:
         assert np.array_equal(y, yref), f"{info['format']} is sequential: must be bit-exact"
+    # the format's own reference plugin (oracle/make_golden.py): opt_coo,
+    # opt_jds, opt_css, opt_ss (OPTIMIZED, and OPTIMIZED+PADDING) -- within
+    # 1e-12 of sum |a x| (their summation orders differ from each other)
+    own = {"coo": ("y_coo",), "jds": ("y_jds",), "css": ("y_css",), "ss": ("y_ss_opt", "y_ss_pad"),
+           "ell": ("y_ell",), "dia": ("y_dia",)}.get(fmt, ())
+    mag = oracle_y(rp, g["col"], np.abs(g["val"]), np.abs(g["x"]))
+    for key in own:
+        if key in g:
+            err = np.abs(y - g[key])
+            assert np.all(err <= REL * mag + 1e-300), f"{name}/{fmt} vs the reference's {key}: {err.max()}"
 
 
 @pytest.mark.parametrize("lanes", [1, 2, 4, 8, 16, 32, 64])

@@ -44,6 +44,35 @@ def test_format_restatements_match_reference(name):
         assert np.array_equal(oracle.ss_spmv(rp, idx, val, g["x"], 4, True), g["y_ss_opt"])
 
 
+F_PLUGINS = ("coo", "jds", "css", "ss_pad")
+
+
+def _within(y, yref, mag, rel=1e-12):
+    return bool(np.all(np.abs(y - yref) <= rel * mag + 1e-300))
+
+
+@pytest.mark.parametrize("name", golden_names())
+def test_f_plugin_vectors_pinned(name):
+    """Every fixture carries the outputs of the reference's (f) plugins and of
+    opt_ss OPTIMIZED+PADDING (oracle/make_golden.py): opt_jds and opt_css sum
+    every row in column order (src/opt_jds.cpp:91-103; opt_css per column
+    block, src/opt_css.cpp:226-303, blocks ascending) -- bit-equal to the
+    opt_crs restatement; opt_coo's omp atomic scatter (src/opt_coo.cpp:34-46)
+    and the PADDING tree fold (src/opt_ss.cpp:305-347) change the order --
+    within 1e-12 of sum |a x|, exact on the integer-valued fixture."""
+    g = load_golden(name)
+    _, rp, idx, val = csr_of(g)
+    y = oracle.csr_spmv(rp, idx, val, g["x"])
+    mag = oracle.csr_spmv(rp, idx, np.abs(val), np.abs(g["x"]))
+    for f in F_PLUGINS:
+        assert f"y_{f}" in g, f"{name}: y_{f} missing"
+        yf = g[f"y_{f}"]
+        if f in ("jds", "css") or name == "syn_integer":
+            assert np.array_equal(yf, y), f"{name}: y_{f}"
+        else:
+            assert _within(yf, y, mag), f"{name}: y_{f}"
+
+
 @pytest.mark.parametrize("name", ["3x3", "5x5", "10x10", "random"])
 def test_loader_and_vectors_match_reference(name):
     """LoadSparseMatrix + srand(3)/CreateRandomVector restated exactly."""
@@ -112,3 +141,14 @@ def test_random_instances_against_live_reference(seed):
         assert np.array_equal(ye, oracle.ref_spmv("ell", m, n, row, col, val, x)[0])
     assert np.array_equal(oracle.ss_spmv(rp, idx, cv, x, 4, True),
                           oracle.ref_spmv("ss_opt", m, n, row, col, val, x)[0])
+    # the (f) plugins and SS PADDING, live: the same pins as the golden test
+    mag = oracle.csr_spmv(rp, idx, np.abs(cv), x)
+    for f in F_PLUGINS:
+        if not oracle.ref_available(f):
+            continue
+        yf, okf = oracle.ref_spmv(f, m, n, row, col, val, x)
+        assert okf, f
+        if f in ("jds", "css"):
+            assert np.array_equal(yf, y), f
+        else:
+            assert _within(yf, y, mag), f
