@@ -85,7 +85,12 @@ $(PROBEDIR)/%.o: $(CSRC)/%.hip $(HDRS) Makefile | $(PROBEDIR)
 $(PROBEDIR)/libspmv_hip.so: $(PROBE_OBJ)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $^ -Wl,-soname,libspmv_hip.so -L$(ROCM)/lib -lrccl
 
-probes: $(PROBEDIR)/libspmv_hip.so
+# stand-alone HBM probes (tools/*.hip) used by the placement study
+bin/region_probe: tools/region_probe.hip Makefile
+	mkdir -p bin
+	$(HIPCC) $(HIPFLAGS) -o $@ $<
+
+probes: $(PROBEDIR)/libspmv_hip.so bin/region_probe
 
 # host-code sanitizer build (CPU only): build/asan/libspmv_hip.so
 # with AddressSanitizer + UBSan on every host object (the device code of the

@@ -15,6 +15,9 @@
 #                     (tools/profile_round.sh) of the headline plan of that shape
 #   gloo2_c3          the self-launched 2-rank bench (gloo, one GPU) with --verify
 #   py:<script args>  python3 -u <script args> (a tools/ probe), stdout to <step>.log
+#   exe:<binary args>  a stand-alone probe binary (bin/region_probe ...)
+#   probe:<script args> the same against the probe build (make probes:
+#                     SPMV_HIP_LIBRARY=probes_build/libspmv_hip.so)
 # This replaces round 2's one-off tools/r2_*.sh wrappers (profiles/round2/README.md).
 set -o pipefail
 OUTNAME=$1; shift
@@ -26,7 +29,7 @@ export PYTHONUNBUFFERED=1
 i=0
 for step in "$@"; do
   i=$((i + 1))
-  tag=$(printf '%02d_%s' $i "$(echo "$step" | tr -c 'A-Za-z0-9_.-' '_' | cut -c1-40)")
+  tag=$(printf '%02d_%s' $i "$(printf "%s" "$step" | tr -c 'A-Za-z0-9_.-' '_' | cut -c1-40)")
   echo "[$(date +%T)] step $tag" >&2
   case "$step" in
     tests)
@@ -53,6 +56,13 @@ for step in "$@"; do
     py:*)
       # shellcheck disable=SC2086
       timeout -k 10 600 python3 -u ${step#py:} > "$O/$tag.log" 2> "$O/$tag.err" ;;
+    probe:*)
+      # shellcheck disable=SC2086
+      SPMV_HIP_LIBRARY=$R/probes_build/libspmv_hip.so timeout -k 10 600 python3 -u ${step#probe:} \
+          > "$O/$tag.log" 2> "$O/$tag.err" ;;
+    exe:*)
+      # shellcheck disable=SC2086
+      timeout -k 10 600 ${step#exe:} > "$O/$tag.log" 2> "$O/$tag.err" ;;
     *)
       echo "unknown step $step" >&2; exit 64 ;;
   esac
