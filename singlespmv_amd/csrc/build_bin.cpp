@@ -377,7 +377,6 @@ static void bin_offsets(spmv_plan_s *p, const spmv_options_t &o, BinLayout &L) {
     // bin's product run apart).
     L.mul_bins.resize((size_t)NB);
     if (const char *e = probe_env("SPMV_BIN_MUL_PERM")) B.mul_perm = std::atoi(e) != 0;
-    if (const char *e = probe_env("SPMV_BIN_RR")) B.strip_rr = std::atoi(e) != 0;
     for (int g = 0; g < G; ++g) {
         const int64_t g0 = B.g_bin[(size_t)g], nbg = B.g_bin[(size_t)g + 1] - g0;
         int64_t P = 1;
@@ -719,31 +718,6 @@ static void bin_pieces(const BinDev &B, const BinLayout &L, BinPieces &P) {
             }
         }
     };
-    if (B.strip_rr && B.G == 1 && S >= B.nwg1) {
-        // round-robin strips: workgroup k takes strips k, k + nwg, k + 2 nwg,
-        // ... (whole strips), so at any time the workgroups sweep nwg
-        // CONSECUTIVE strips -- their product segments of one bin are
-        // neighbours in the Sum order -- and the strips of the last, partial
-        // round are cut evenly (64-entry multiples) over all workgroups
-        const int64_t *ss = L.strip_start.data();
-        const int64_t R = S / B.nwg1, t0 = R * B.nwg1, g0 = ss[t0], g1 = L.LL > 0 ? L.E1 : ss[S];
-        for (int k = 0; k < B.nwg1; ++k) {
-            for (int64_t j = 0; j < R; ++j) {
-                const int64_t t = j * B.nwg1 + k;
-                if (ss[t] < ss[t + 1]) {
-                    P.strip.push_back((int32_t)t);
-                    P.beg.push_back(ss[t]);
-                    P.end.push_back(ss[t + 1]);
-                }
-            }
-            const int64_t a = g0 + (int64_t)(((__int128)(g1 - g0) * k / B.nwg1) & ~(__int128)63);
-            const int64_t z = k + 1 == B.nwg1 ? g1 : g0 + (int64_t)(((__int128)(g1 - g0) * (k + 1) / B.nwg1) & ~(__int128)63);
-            int64_t s = t0;
-            if (a < z) add_range(ss, a, z, s);
-            P.off.push_back((int64_t)P.strip.size());
-        }
-        return;
-    }
     for (int g = 0; g < B.G; ++g) {
         // Mul-order range of the group (with long rows, G == 1: segments,
         // voids and long blocks)

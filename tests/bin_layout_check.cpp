@@ -213,7 +213,6 @@ int main() {
                     B.pad_log = pl;
                     B.nwg1 = B.nwg2 = 256;
                     B.mul_perm = (si + wi + pl) % 2 == 0;  // both Mul bin orders
-                    B.strip_rr = (si + pl) % 2 == 1;       // contiguous / round-robin Mul strips
                     spmv_options_t o;
                     std::memset(&o, 0, sizeof(o));
                     BinLayout L;

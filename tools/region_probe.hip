@@ -8,6 +8,8 @@
 //   scatter  128-byte lines written by 16 lanes of 8 B (the Mul's product
 //            lines) at line index (i * P) mod lines -- every line once, in
 //            no regular stride
+//   blocked  256 / 1024 workgroups, each streaming its own contiguous share
+//            (the DIA / BIN Mul shape) with 16-byte nontemporal loads
 // One JSON line per chunk: {"chunk", "va", "read_gbs", "write_gbs",
 // "scatter_gbs"}, best of `reps` launches each.
 //
@@ -16,6 +18,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 typedef double f64x2 __attribute__((ext_vector_type(2)));
@@ -46,15 +49,37 @@ __global__ __launch_bounds__(256) void wr(f64x2 *__restrict__ a, long long n2, d
 }
 
 // lines of 16 doubles; thread t handles line (t / 16) of each step, lane t % 16
+// (lines is a power of two: i * P mod lines, P odd, is a bijection)
 __global__ __launch_bounds__(256) void scat(double *__restrict__ a, long long lines, long long P, double v) {
     const long long nthr = (long long)gridDim.x * 256;
     for (long long i = (blockIdx.x * 256LL + threadIdx.x) >> 4; i < lines; i += nthr >> 4) {
-        const long long L = (long long)(((unsigned __int128)i * (unsigned long long)P) % (unsigned long long)lines);
+        const long long L = (long long)(((unsigned long long)i * (unsigned long long)P) & (unsigned long long)(lines - 1));
         __builtin_nontemporal_store(v, a + L * 16 + (threadIdx.x & 15));
     }
 }
 
+// blocked: workgroup w streams its own contiguous 1/grid of the chunk (the
+// DIA / BIN Mul shape: many concurrent streams far apart), 16-byte loads
+__global__ __launch_bounds__(256) void rd_blocked(const f64x2 *__restrict__ a, long long n2, double *__restrict__ out) {
+    const long long per = n2 / gridDim.x, b0 = (long long)blockIdx.x * per;
+    double s = 0;
+    for (long long i = threadIdx.x; i < per; i += 256) {
+        const f64x2 v = __builtin_nontemporal_load(a + b0 + i);
+        s += v.x + v.y;
+    }
+    if (s == 1.2345) out[0] = s;
+}
+
+// "frag" mode: the same kernels on a 1 GB buffer allocated (A) first,
+// (B) after the last ~9 GB were filled with 2 MB allocations and every other
+// one freed, (C) the same with 64 KB allocations -- B and C can only be
+// backed by the holes (small physical pieces, so small page-table fragments)
+// once the rest of memory is held.  A TLB-bound access pattern slows down
+// from A to C; a bandwidth-bound one does not.
+static int frag_mode(int reps);
+
 int main(int argc, char **argv) {
+    if (argc > 1 && std::string(argv[1]) == "frag") return frag_mode(argc > 2 ? std::atoi(argv[2]) : 3);
     const long long chunk = (argc > 1 ? std::atoll(argv[1]) : 1024) << 20;
     const long long keep = (argc > 2 ? std::atoll(argv[2]) : 16) << 30;
     const int reps = argc > 3 ? std::atoi(argv[3]) : 3;
@@ -100,11 +125,119 @@ int main(int argc, char **argv) {
         const float tw = best([&] { wr<<<grid, 256>>>(c, n2, 1.0); });
         const float tr = best([&] { rd<<<grid, 256>>>(c, n2, out); });
         const float ts = best([&] { scat<<<grid, 256>>>((double *)c, lines, P, 2.0); });
+        const float tb = best([&] { rd_blocked<<<256, 256>>>(c, n2, out); });
+        const float tb2 = best([&] { rd_blocked<<<1024, 256>>>(c, n2, out); });
         std::printf("{\"chunk\": %zu, \"mb\": %lld, \"va\": \"%p\", \"read_gbs\": %.0f, \"write_gbs\": %.0f, "
-                    "\"scatter_gbs\": %.0f}\n",
-                    i, chunk >> 20, ch[i], chunk / tr / 1e6, chunk / tw / 1e6, chunk / ts / 1e6);
+                    "\"scatter_gbs\": %.0f, \"blocked256_gbs\": %.0f, \"blocked1024_gbs\": %.0f}\n",
+                    i, chunk >> 20, ch[i], chunk / tr / 1e6, chunk / tw / 1e6, chunk / ts / 1e6, chunk / tb / 1e6,
+                    chunk / tb2 / 1e6);
         std::fflush(stdout);
     }
     for (void *p : ch) CHECK(hipFree(p));
+    return 0;
+}
+
+static int frag_mode(int reps) {
+    double *out;
+    CHECK(hipMalloc(&out, 64));
+    hipEvent_t a, b;
+    CHECK(hipEventCreate(&a));
+    CHECK(hipEventCreate(&b));
+    auto best = [&](auto launch) {
+        launch();
+        CHECK(hipDeviceSynchronize());
+        float bms = 1e30f;
+        for (int r = 0; r < reps; ++r) {
+            CHECK(hipEventRecord(a));
+            launch();
+            CHECK(hipEventRecord(b));
+            CHECK(hipEventSynchronize(b));
+            float ms;
+            CHECK(hipEventElapsedTime(&ms, a, b));
+            if (ms < bms) bms = ms;
+        }
+        return bms;
+    };
+    const long long bytes = 1024LL << 20, n2 = bytes / 16, lines = bytes / 128;
+    // lines = 12 Mi: not a power of two -- use the largest power of two below
+    long long pl = 1;
+    while (pl * 2 <= lines) pl *= 2;
+    const long long P = (long long)(0.6180339887 * (double)pl) | 1;
+    auto measure = [&](const char *name, void *p) {
+        f64x2 *c = (f64x2 *)p;
+        const float tw = best([&] { wr<<<4096, 256>>>(c, n2, 1.0); });
+        const float tr = best([&] { rd<<<4096, 256>>>(c, n2, out); });
+        const float ts = best([&] { scat<<<4096, 256>>>((double *)c, pl, P, 2.0); });
+        const float tb = best([&] { rd_blocked<<<256, 256>>>(c, n2, out); });
+        const float tb2 = best([&] { rd_blocked<<<1024, 256>>>(c, n2, out); });
+        std::printf("{\"frag\": \"%s\", \"va\": \"%p\", \"read_gbs\": %.0f, \"write_gbs\": %.0f, \"scatter_gbs\": %.0f, "
+                    "\"blocked256_gbs\": %.0f, \"blocked1024_gbs\": %.0f}\n",
+                    name, p, bytes / tr / 1e6, bytes / tw / 1e6, pl * 128.0 / ts / 1e6, bytes / tb / 1e6, bytes / tb2 / 1e6);
+        std::fflush(stdout);
+    };
+    void *A = nullptr;
+    CHECK(hipMalloc(&A, bytes));
+    measure("A_first", A);
+    // hold everything but ~9 GB, so later buffers must come from the holes
+    std::vector<void *> hold;
+    for (;;) {
+        size_t fr = 0, tot = 0;
+        CHECK(hipMemGetInfo(&fr, &tot));
+        if ((long long)fr < (9LL << 30) + (1LL << 30)) break;
+        void *p = nullptr;
+        if (hipMalloc(&p, 1LL << 30) != hipSuccess) {
+            (void)hipGetLastError();
+            break;
+        }
+        hold.push_back(p);
+    }
+    // fill all free memory (down to 64 MB) with `piece`-sized buffers, then
+    // free every other one
+    auto holes = [&](long long piece, long long total) {
+        std::vector<void *> v;
+        for (long long t = 0; t < total; t += piece) {
+            size_t f2 = 0, t2 = 0;
+            CHECK(hipMemGetInfo(&f2, &t2));
+            if ((long long)f2 < (64LL << 20) + piece) break;
+            void *p = nullptr;
+            if (hipMalloc(&p, piece) != hipSuccess) {
+                (void)hipGetLastError();
+                break;
+            }
+            v.push_back(p);
+        }
+        std::vector<void *> keep;
+        for (size_t i = 0; i < v.size(); ++i) {
+            if (i % 2) CHECK(hipFree(v[i]));
+            else keep.push_back(v[i]);
+        }
+        return keep;
+    };
+    // B: ~9 GB in 2 MB pieces, every other freed: ~4.5 GB of 2 MB holes
+    std::vector<void *> k2 = holes(2LL << 20, 16LL << 30);
+    size_t fr = 0, tot = 0;
+    CHECK(hipMemGetInfo(&fr, &tot));
+    std::printf("{\"free_after_2mb_holes_gb\": %.2f}\n", fr / 1073741824.0);
+    void *Bf = nullptr;
+    if (hipMalloc(&Bf, bytes) == hipSuccess) measure("B_2mb_holes", Bf);
+    else (void)hipGetLastError();
+    // C: the rest (~3.5 GB) in 64 KB pieces, every other freed
+    std::vector<void *> k64 = holes(64LL << 10, 16LL << 30);
+    CHECK(hipMemGetInfo(&fr, &tot));
+    std::printf("{\"free_after_64kb_holes_gb\": %.2f}\n", fr / 1073741824.0);
+    void *Cf = nullptr;
+    if (hipMalloc(&Cf, bytes) == hipSuccess) measure("C_64kb_holes", Cf);
+    else (void)hipGetLastError();
+    measure("A_again", A);
+    for (void *p : k64) CHECK(hipFree(p));
+    for (void *p : k2) CHECK(hipFree(p));
+    for (void *p : hold) CHECK(hipFree(p));
+    if (Cf) CHECK(hipFree(Cf));
+    if (Bf) CHECK(hipFree(Bf));
+    void *D = nullptr;
+    CHECK(hipMalloc(&D, bytes));
+    measure("D_after_all_freed", D);
+    CHECK(hipFree(D));
+    CHECK(hipFree(A));
     return 0;
 }
