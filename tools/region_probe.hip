@@ -77,9 +77,11 @@ __global__ __launch_bounds__(256) void rd_blocked(const f64x2 *__restrict__ a, l
 // once the rest of memory is held.  A TLB-bound access pattern slows down
 // from A to C; a bandwidth-bound one does not.
 static int frag_mode(int reps);
+static int alloc_mode(int reps);
 
 int main(int argc, char **argv) {
     if (argc > 1 && std::string(argv[1]) == "frag") return frag_mode(argc > 2 ? std::atoi(argv[2]) : 3);
+    if (argc > 1 && std::string(argv[1]) == "alloc") return alloc_mode(argc > 2 ? std::atoi(argv[2]) : 3);
     const long long chunk = (argc > 1 ? std::atoll(argv[1]) : 1024) << 20;
     const long long keep = (argc > 2 ? std::atoll(argv[2]) : 16) << 30;
     const int reps = argc > 3 ? std::atoi(argv[3]) : 3;
@@ -239,5 +241,159 @@ static int frag_mode(int reps) {
     measure("D_after_all_freed", D);
     CHECK(hipFree(D));
     CHECK(hipFree(A));
+    return 0;
+}
+
+// "alloc" mode: which allocation method gives a buffer the fast mode?  Each
+// method allocates 4 buffers of 1.5 GB (kept, so each is new memory) and
+// measures them like frag mode; then 20 GB of 2 MB pieces with every other
+// one freed fragment the free memory, and the methods run again.
+//   plain        hipMalloc
+//   vmm1g_one    hipMemAddressReserve aligned to 1 GB + ONE hipMemCreate handle
+//   vmm1g_chunks the same with 512 MB handles
+//   contig       hipExtMallocWithFlags(hipDeviceMallocContiguous)
+static int alloc_mode(int reps) {
+    double *out;
+    CHECK(hipMalloc(&out, 64));
+    hipEvent_t a, b;
+    CHECK(hipEventCreate(&a));
+    CHECK(hipEventCreate(&b));
+    auto best = [&](auto launch) {
+        launch();
+        CHECK(hipDeviceSynchronize());
+        float bms = 1e30f;
+        for (int r = 0; r < reps; ++r) {
+            CHECK(hipEventRecord(a));
+            launch();
+            CHECK(hipEventRecord(b));
+            CHECK(hipEventSynchronize(b));
+            float ms;
+            CHECK(hipEventElapsedTime(&ms, a, b));
+            if (ms < bms) bms = ms;
+        }
+        return bms;
+    };
+    const long long bytes = 1536LL << 20, n2 = bytes / 16;
+    long long pl = 1;
+    while (pl * 2 <= bytes / 128) pl *= 2;
+    const long long P = (long long)(0.6180339887 * (double)pl) | 1;
+    auto measure = [&](const char *phase, const char *name, int rep, void *p) {
+        f64x2 *c = (f64x2 *)p;
+        const float tw = best([&] { wr<<<4096, 256>>>(c, n2, 1.0); });
+        const float tr = best([&] { rd<<<4096, 256>>>(c, n2, out); });
+        const float ts = best([&] { scat<<<4096, 256>>>((double *)c, pl, P, 2.0); });
+        const float tb2 = best([&] { rd_blocked<<<1024, 256>>>(c, n2, out); });
+        std::printf("{\"phase\": \"%s\", \"method\": \"%s\", \"rep\": %d, \"va\": \"%p\", \"va_mod_1g_mb\": %lld, "
+                    "\"read_gbs\": %.0f, \"write_gbs\": %.0f, \"scatter_gbs\": %.0f, \"blocked1024_gbs\": %.0f}\n",
+                    phase, name, rep, p, (long long)(((uintptr_t)p) & ((1ULL << 30) - 1)) >> 20, bytes / tr / 1e6,
+                    bytes / tw / 1e6, pl * 128.0 / ts / 1e6, bytes / tb2 / 1e6);
+        std::fflush(stdout);
+    };
+    hipMemAllocationProp prop = {};
+    prop.type = hipMemAllocationTypePinned;
+    prop.location.type = hipMemLocationTypeDevice;
+    prop.location.id = 0;
+    struct Vmm {
+        void *va;
+        size_t size;
+        std::vector<hipMemGenericAllocationHandle_t> h;
+        size_t chunk;
+    };
+    std::vector<void *> plain;
+    std::vector<Vmm> vmms;
+    auto vmm = [&](size_t chunk) -> void * {
+        Vmm v;
+        v.size = (size_t)bytes;
+        v.chunk = std::min(chunk, v.size);
+        CHECK(hipMemAddressReserve(&v.va, v.size, 1ULL << 30, nullptr, 0));
+        for (size_t o = 0; o < v.size; o += v.chunk) {
+            hipMemGenericAllocationHandle_t h;
+            CHECK(hipMemCreate(&h, v.chunk, &prop, 0));
+            CHECK(hipMemMap((char *)v.va + o, v.chunk, 0, h, 0));
+            v.h.push_back(h);
+        }
+        hipMemAccessDesc acc = {};
+        acc.location = prop.location;
+        acc.flags = hipMemAccessFlagsProtReadWrite;
+        CHECK(hipMemSetAccess(v.va, v.size, &acc, 1));
+        vmms.push_back(v);
+        return v.va;
+    };
+    auto run = [&](const char *phase, int nr) {
+        for (int r = 0; r < nr; ++r) {
+            void *p = nullptr;
+            CHECK(hipMalloc(&p, bytes));
+            plain.push_back(p);
+            measure(phase, "plain", r, p);
+        }
+        for (int r = 0; r < nr; ++r) measure(phase, "vmm1g_one", r, vmm((size_t)bytes));
+        for (int r = 0; r < nr; ++r) measure(phase, "vmm1g_chunks", r, vmm(512ULL << 20));
+        for (int r = 0; r < nr; ++r) {
+            void *p = nullptr;
+            if (hipExtMallocWithFlags(&p, bytes, hipDeviceMallocContiguous) != hipSuccess) {
+                (void)hipGetLastError();
+                std::printf("{\"phase\": \"%s\", \"method\": \"contig\", \"rep\": %d, \"error\": 1}\n", phase, r);
+                continue;
+            }
+            plain.push_back(p);
+            measure(phase, "contig", r, p);
+        }
+    };
+    run("fresh", 4);
+    // fragment: 20 GB of 2 MB pieces, every other one freed
+    std::vector<void *> pieces, keep;
+    for (int i = 0; i < 10240; ++i) {
+        void *p = nullptr;
+        if (hipMalloc(&p, 2LL << 20) != hipSuccess) {
+            (void)hipGetLastError();
+            break;
+        }
+        pieces.push_back(p);
+    }
+    for (size_t i = 0; i < pieces.size(); ++i) {
+        if (i % 2) CHECK(hipFree(pieces[i]));
+        else keep.push_back(pieces[i]);
+    }
+    run("after_2mb_holes", 4);
+    // squeezed: hold all but 16 GB, fragment those, one buffer per method
+    std::vector<void *> hold;
+    for (;;) {
+        size_t fr = 0, tot = 0;
+        CHECK(hipMemGetInfo(&fr, &tot));
+        if ((long long)fr < (17LL << 30)) break;
+        void *p = nullptr;
+        if (hipMalloc(&p, 1LL << 30) != hipSuccess) {
+            (void)hipGetLastError();
+            break;
+        }
+        hold.push_back(p);
+    }
+    std::vector<void *> p2;
+    for (;;) {
+        size_t fr = 0, tot = 0;
+        CHECK(hipMemGetInfo(&fr, &tot));
+        if ((long long)fr < (256LL << 20)) break;
+        void *p = nullptr;
+        if (hipMalloc(&p, 2LL << 20) != hipSuccess) {
+            (void)hipGetLastError();
+            break;
+        }
+        p2.push_back(p);
+    }
+    for (size_t i = 0; i < p2.size(); ++i) {
+        if (i % 2) CHECK(hipFree(p2[i]));
+        else keep.push_back(p2[i]);
+    }
+    run("squeezed_2mb_holes", 1);
+    for (void *p : hold) CHECK(hipFree(p));
+    for (void *p : keep) CHECK(hipFree(p));
+    for (void *p : plain) CHECK(hipFree(p));
+    for (auto &v : vmms) {
+        for (size_t k = 0; k < v.h.size(); ++k) {
+            CHECK(hipMemUnmap((char *)v.va + k * v.chunk, v.chunk));
+            CHECK(hipMemRelease(v.h[k]));
+        }
+        CHECK(hipMemAddressFree(v.va, v.size));
+    }
     return 0;
 }
