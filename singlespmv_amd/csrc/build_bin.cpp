@@ -688,8 +688,10 @@ static int bin_place_prod(spmv_plan_s *p, int64_t n, size_t prod_bytes, const sp
     if (mode == SPMV_PLACEMENT_VMM) {
         size_t chunk = (size_t)2 << 20;
         if (const char *e = probe_env("SPMV_VMM_CHUNK_MB")) chunk = (size_t)std::max(1, std::atoi(e)) << 20;
+        size_t align = 0;
+        if (const char *e = probe_env("SPMV_VMM_ALIGN_MB")) align = (size_t)std::max(0, std::atoi(e)) << 20;
         void *q = nullptr;
-        SPMV_RETURN_IF(p->arena.alloc_vmm(&q, prod_bytes, chunk, p->device));
+        SPMV_RETURN_IF(p->arena.alloc_vmm(&q, prod_bytes, chunk, p->device, align));
         B.prod = (double *)q;
         return SPMV_SUCCESS;
     }

@@ -34,7 +34,7 @@ int DevArena::alloc(void **p, size_t n) {
 
 // Physical memory in `chunk`-byte handles (hipMemCreate) mapped back to back
 // into one reserved VA range.  chunk is rounded to the allocation granularity.
-int DevArena::alloc_vmm(void **p, size_t n, size_t chunk, int device) {
+int DevArena::alloc_vmm(void **p, size_t n, size_t chunk, int device, size_t align) {
     hipMemAllocationProp prop = {};
     prop.type = hipMemAllocationTypePinned;
     prop.location.type = hipMemLocationTypeDevice;
@@ -56,11 +56,14 @@ int DevArena::alloc_vmm(void **p, size_t n, size_t chunk, int device) {
             (void)hipMemUnmap((char *)m.va + k * chunk, chunk);
             (void)hipMemRelease(m.handles[k]);
         }
-        if (m.va) (void)hipMemAddressFree(m.va, total);
+        if (m.res) (void)hipMemAddressFree(m.res, m.res_bytes);
         return e == hipErrorOutOfMemory ? SPMV_ERROR_OUT_OF_MEMORY : SPMV_ERROR_HIP;
     };
-    hipError_t e = hipMemAddressReserve(&m.va, total, gran, nullptr, 0);
+    align = align > gran ? (align + gran - 1) / gran * gran : 0;
+    m.res_bytes = total + align;
+    hipError_t e = hipMemAddressReserve(&m.res, m.res_bytes, gran, nullptr, 0);
     if (e != hipSuccess) return undo(e, "hipMemAddressReserve");
+    m.va = align ? (void *)(((uintptr_t)m.res + align - 1) / align * align) : m.res;
     // all handles first, then mapped -- in creation order, or (probe build,
     // SPMV_VMM_SHUFFLE) handle k at chunk slot k * P mod count
     const size_t cnt = total / chunk;
@@ -116,7 +119,7 @@ static void vmm_release(const VmmMap &m) {
         (void)hipMemUnmap((char *)m.va + k * m.chunk, m.chunk);
         (void)hipMemRelease(m.handles[k]);
     }
-    (void)hipMemAddressFree(m.va, m.bytes);
+    (void)hipMemAddressFree(m.res, m.res_bytes);
 }
 
 void DevArena::free(void *p) {

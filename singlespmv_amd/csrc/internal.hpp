@@ -76,8 +76,10 @@ inline int placement_mode_check(int mode) {
 // memory API (hipMemCreate + hipMemMap: the BIN product buffer, see
 // build_bin.cpp, placement).
 struct VmmMap {
-    void *va = nullptr;
+    void *va = nullptr;      // mapped range (aligned inside the reservation)
     size_t bytes = 0;
+    void *res = nullptr;     // the reservation, res_bytes long
+    size_t res_bytes = 0;
     std::vector<hipMemGenericAllocationHandle_t> handles;  // one per mapped chunk
     size_t chunk = 0;
 };
@@ -87,7 +89,9 @@ struct DevArena {
     int64_t bytes = 0;
     int alloc(void **p, size_t n);  // hipMalloc, zero-size safe
     // n bytes of physical memory in `chunk`-byte handles mapped at one VA range
-    int alloc_vmm(void **p, size_t n, size_t chunk, int device);
+    // (align > 0: the mapping starts at a multiple of `align` inside a larger
+    // reservation -- hipMemAddressReserve itself honours only the granularity)
+    int alloc_vmm(void **p, size_t n, size_t chunk, int device, size_t align = 0);
     void free(void *p);             // hipFree one allocation of this arena
     void release();
 };

@@ -30,7 +30,7 @@ def main():
     ap.add_argument("--max-len", type=int, default=10000)
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--iters", type=int, default=20)
-    ap.add_argument("--placement", default="search")
+    ap.add_argument("--placement", default="plain", help="default placement (a variant's placement=K overrides)")
     ap.add_argument("--check", action="store_true", help="bit-equality of each variant's y vs the first")
     a = ap.parse_args()
     import torch
@@ -52,7 +52,9 @@ def main():
                 continue
             saved[k] = os.environ.get(k)
             os.environ[k] = v
-        p = sp.Plan.from_csr(m, n, rp, col, val, a.fmt, placement=a.placement, **opts)
+        kw = dict(placement=a.placement)
+        kw.update(opts)
+        p = sp.Plan.from_csr(m, n, rp, col, val, a.fmt, **kw)
         for k, v in saved.items():
             if v is None:
                 os.environ.pop(k, None)
