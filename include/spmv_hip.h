@@ -117,17 +117,18 @@ typedef struct spmv_options {
 } spmv_options_t;
 
 /* Placement of the large scratch/value buffer of BIN and DIA plans (the BIN
- * product buffer, the DIA values).  The same launch runs up to ~15 % slower
- * from some physical HBM regions than from others. */
-#define SPMV_PLACEMENT_AUTO 0   /* = PLAIN                                           */
-#define SPMV_PLACEMENT_PLAIN 1  /* one hipMalloc, nothing timed: create holds no
-                                   device memory beyond the plan's own            */
+ * product buffer, the DIA values).  The BIN Mul ran ~15 % slower with one
+ * plain hipMalloc on most plans than with the same buffer built from 2-MB
+ * physical handles (DESIGN §4a "Placement, round 3"). */
+#define SPMV_PLACEMENT_AUTO 0   /* BIN products >= 32 MB: VMM; everything else: PLAIN */
+#define SPMV_PLACEMENT_PLAIN 1  /* one hipMalloc                                     */
 #define SPMV_PLACEMENT_SEARCH 2 /* experiment (probe build only; the product library
                                    returns SPMV_ERROR_NOT_SUPPORTED): up to 8
                                    candidates spread over all free HBM, each timed
                                    with one launch, the fastest kept              */
-#define SPMV_PLACEMENT_VMM 3    /* experiment (probe build only): hipMemCreate
-                                   handles of 2 MB mapped into one VA range       */
+#define SPMV_PLACEMENT_VMM 3    /* hipMemCreate handles of 2 MB mapped back to back
+                                   into one VA range aligned to 1 GB (no transient
+                                   memory; DIA: the values are copied into it)    */
 
 /* Fill `opt` with defaults (AUTO format, current device, auto tuning). */
 void spmv_options_default(spmv_options_t *opt);

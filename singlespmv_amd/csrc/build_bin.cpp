@@ -673,29 +673,32 @@ static int bin_place_prod(spmv_plan_s *p, int64_t n, size_t prod_bytes, const sp
     int mode = o.placement;
     SPMV_RETURN_IF(placement_mode_check(mode));
     if (const char *e = probe_env("SPMV_PLACEMENT_MODE")) mode = std::atoi(e);
-    // AUTO = one plain allocation: no transient memory beyond the plan.  The
-    // search (probe build only) is the only method that found the Mul's fast
-    // mode reliably, but it briefly holds most of the free HBM; VMM 2-MB
-    // handles were fast on some boxes and not on others
-    // (profiles/round2/placement/, DESIGN §4a "Placement").
-    if (mode == SPMV_PLACEMENT_AUTO) mode = SPMV_PLACEMENT_PLAIN;
+    // AUTO: a product buffer of >= 32 MB is built from 2-MB physical handles
+    // (hipMemCreate) mapped into one VA range aligned to 1 GB; smaller ones
+    // are one plain allocation.  With one plain hipMalloc the Mul ran in a
+    // slow mode on most plans (config 2 Mul 0.61-0.62 vs 0.53 ms; 10 M x 80 M
+    // rank shape 0.84 vs 0.72-0.73), the 2-MB handles were fast in 8 of 8
+    // plans, first plan of a fresh process included, for no transient memory
+    // (profiles/round3/probe/placement_vmm_*.jsonl, DESIGN §4a "Placement,
+    // round 3").
+    if (mode == SPMV_PLACEMENT_AUTO)
+        mode = prod_bytes >= kBinVmmMinBytes ? SPMV_PLACEMENT_VMM : SPMV_PLACEMENT_PLAIN;
     // the Mul of a 184 MB product buffer (config 3 with long rows) varies 0.118-0.151 ms
     // by placement as much as config 2's does: search from 32 MB
     if (mode == SPMV_PLACEMENT_SEARCH && prod_bytes < ((size_t)32 << 20)) mode = SPMV_PLACEMENT_PLAIN;
     B.placement = mode;
 #ifdef SPMV_PROBES
     if (mode == SPMV_PLACEMENT_SEARCH) return bin_place_search(p, n, prod_bytes);
+#endif
     if (mode == SPMV_PLACEMENT_VMM) {
-        size_t chunk = (size_t)2 << 20;
+        size_t chunk = kVmmChunk, align = kVmmAlign;
         if (const char *e = probe_env("SPMV_VMM_CHUNK_MB")) chunk = (size_t)std::max(1, std::atoi(e)) << 20;
-        size_t align = 0;
         if (const char *e = probe_env("SPMV_VMM_ALIGN_MB")) align = (size_t)std::max(0, std::atoi(e)) << 20;
         void *q = nullptr;
         SPMV_RETURN_IF(p->arena.alloc_vmm(&q, prod_bytes, chunk, p->device, align));
         B.prod = (double *)q;
         return SPMV_SUCCESS;
     }
-#endif
     return alloc_prod_plain(p, prod_bytes);
 }
 

@@ -599,21 +599,22 @@ static int dia_placement(spmv_plan_s *p, int64_t m, int64_t n, size_t bytes, con
     if (mode == SPMV_PLACEMENT_SEARCH && bytes < ((size_t)256 << 20)) mode = SPMV_PLACEMENT_PLAIN;
     d.placement = mode;
     if (mode == SPMV_PLACEMENT_PLAIN) return SPMV_SUCCESS;
-#ifndef SPMV_PROBES
-    (void)m;
-    (void)n;
-    return SPMV_SUCCESS;
-#else
     if (mode == SPMV_PLACEMENT_VMM) {  // move the values into a VMM mapping
-        size_t chunk = (size_t)2 << 20;
+        size_t chunk = kVmmChunk, align = kVmmAlign;
         if (const char *e = probe_env("SPMV_VMM_CHUNK_MB")) chunk = (size_t)std::max(1, std::atoi(e)) << 20;
+        if (const char *e = probe_env("SPMV_VMM_ALIGN_MB")) align = (size_t)std::max(0, std::atoi(e)) << 20;
         void *q = nullptr;
-        SPMV_RETURN_IF(p->arena.alloc_vmm(&q, bytes, chunk, p->device));
+        SPMV_RETURN_IF(p->arena.alloc_vmm(&q, bytes, chunk, p->device, align));
         SPMV_HIP_TRY(hipMemcpy(q, d.val, bytes, hipMemcpyDeviceToDevice));
         p->arena.free(d.val);
         d.val = (double *)q;
         return SPMV_SUCCESS;
     }
+#ifndef SPMV_PROBES
+    (void)m;
+    (void)n;
+    return SPMV_SUCCESS;
+#else
     int K = 8;
     if (const char *e = probe_env("SPMV_DIA_PLACEMENT")) K = std::max(1, std::min(8, std::atoi(e)));
     if (K <= 1) return SPMV_SUCCESS;

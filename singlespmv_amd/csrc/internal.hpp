@@ -57,19 +57,24 @@ inline const char *probe_env(const char *name) {
 #endif
 }
 
-// The placement experiments (SPMV_PLACEMENT_SEARCH, _VMM) exist
-// only in the probe build: the product library makes one plain allocation,
-// holds no transient device memory at create and times nothing.
+// The placement search (SPMV_PLACEMENT_SEARCH) exists only in
+// the probe build: the product library holds no transient device memory at
+// create and times nothing.  SPMV_PLACEMENT_VMM (2-MB physical handles mapped
+// into one 1-GB-aligned VA range) is what AUTO uses for large BIN product
+// buffers.
 inline int placement_mode_check(int mode) {
     SPMV_CHECK_ARG(mode >= SPMV_PLACEMENT_AUTO && mode <= SPMV_PLACEMENT_VMM, "unknown placement mode");
 #ifndef SPMV_PROBES
-    if (mode == SPMV_PLACEMENT_SEARCH || mode == SPMV_PLACEMENT_VMM) {
-        set_error("placement search / VMM are experiments of the probe build (make probes)");
+    if (mode == SPMV_PLACEMENT_SEARCH) {
+        set_error("the placement search is an experiment of the probe build (make probes)");
         return SPMV_ERROR_NOT_SUPPORTED;
     }
 #endif
     return SPMV_SUCCESS;
 }
+constexpr size_t kVmmChunk = (size_t)2 << 20;          // physical handle size
+constexpr size_t kVmmAlign = (size_t)1 << 30;          // VA alignment of the mapping
+constexpr size_t kBinVmmMinBytes = (size_t)32 << 20;   // AUTO: VMM from this product-buffer size
 
 // ---- device memory owned by a plan --------------------------------------
 // Plain hipMalloc allocations, plus buffers mapped through the HIP virtual

@@ -665,10 +665,12 @@ def test_bin_long_rows_run_path(long_len, opts):
 
 
 @pytest.mark.parametrize("opts", [{"bin_pad": 8}, {"bin_pad": 16}, {"bin_pad": 32}, {"bin_sum_waves": 2},
-                                  {"bin_sum_waves": 4}, {"bin_sum_waves": 8}, {"placement": "plain"}])
+                                  {"bin_sum_waves": 4}, {"bin_sum_waves": 8}, {"placement": "plain"},
+                                  {"placement": "vmm"}])
 def test_bin_layout_options(opts):
     """The layout options (product-line padding, Sum waves / bin rows) and the
-    explicit plain placement change speed only."""
+    product-buffer placements (plain hipMalloc / 2-MB VMM handles) change
+    speed only."""
     m = 120_000
     rp, col, val = _bin_matrix("powerlaw", m, m, seed=41)
     x = sp.generate_vector(m, seed=43)
@@ -710,21 +712,21 @@ def _create_peak_drop(make):
 def test_plan_create_holds_only_the_plan(fmt, kind):
     """AUTO placement: while a large BIN / DIA plan is created, free device
     memory never drops by more than the plan's own bytes (+128 MB of runtime
-    slack); ten plans built in a row behave the same.  The placement
-    experiments (SEARCH, VMM) are refused by the product library: they exist
-    only in the probe build."""
+    slack); ten plans built in a row behave the same.  The placement search
+    is refused by the product library: it exists only in the probe build
+    (DESIGN §4a)."""
     m = 4_000_000
     spec = sp.gen_spec(kind, m, per_row=16, band_lo=-20, band_hi=20, seed=21)
     rp, col, val = sp.generate_csr(spec)
     for i in range(10 if fmt == "bin" else 2):
         plan, drop = _create_peak_drop(lambda: sp.Plan.from_csr(m, m, rp, col, val, fmt))
         info = plan.info()
-        assert info["format"] == fmt and info["placement"] == "plain"
+        # AUTO: BIN's product buffer (>= 32 MB) from 2-MB VMM handles, DIA plain
+        assert info["format"] == fmt and info["placement"] == ("vmm" if fmt == "bin" else "plain")
         assert drop <= info["device_bytes"] + (128 << 20), (i, drop, info["device_bytes"])
         plan.destroy()
-    for mode in ("search", "vmm"):
-        with pytest.raises(sp.SpmvError, match="probe build"):
-            sp.Plan.from_csr(m, m, rp, col, val, fmt, placement=mode)
+    with pytest.raises(sp.SpmvError, match="probe build"):
+        sp.Plan.from_csr(m, m, rp, col, val, fmt, placement="search")
 
 
 def test_experiment_switches_do_not_reach_the_product_library(monkeypatch):
