@@ -120,7 +120,8 @@ typedef struct spmv_options {
  * product buffer, the DIA values).  The BIN Mul ran ~15 % slower with one
  * plain hipMalloc on most plans than with the same buffer built from 2-MB
  * physical handles (DESIGN §4a "Placement, round 3"). */
-#define SPMV_PLACEMENT_AUTO 0   /* BIN products >= 32 MB: VMM; everything else: PLAIN */
+#define SPMV_PLACEMENT_AUTO 0   /* BIN products >= 32 MB, DIA values >= 256 MB: VMM;
+                                   everything else: PLAIN                         */
 #define SPMV_PLACEMENT_PLAIN 1  /* one hipMalloc                                     */
 #define SPMV_PLACEMENT_SEARCH 2 /* experiment (probe build only; the product library
                                    returns SPMV_ERROR_NOT_SUPPORTED): up to 8
@@ -128,7 +129,7 @@ typedef struct spmv_options {
                                    with one launch, the fastest kept              */
 #define SPMV_PLACEMENT_VMM 3    /* hipMemCreate handles of 2 MB mapped back to back
                                    into one VA range aligned to 1 GB (no transient
-                                   memory; DIA: the values are copied into it)    */
+                                   device memory)                                 */
 
 /* Fill `opt` with defaults (AUTO format, current device, auto tuning). */
 void spmv_options_default(spmv_options_t *opt);

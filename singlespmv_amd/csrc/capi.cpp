@@ -81,6 +81,8 @@ static int create_from_csr(const HostCsr &A, const spmv_options_t *opt_in, spmv_
         return SPMV_ERROR_OUT_OF_MEMORY;
     }
     p->device = dev;
+    p->arena.device = dev;
+    if (const char *e = probe_env("SPMV_ARENA_VMM_MB")) p->arena.vmm_min = (size_t)std::max(0, std::atoi(e)) << 20;
     p->m = A.m;
     p->n = A.n;
     p->nnz = A.nnz;
@@ -212,6 +214,8 @@ int spmv_plan_create_csr_device(int64_t m, int64_t n, int64_t nnz, const int64_t
             return SPMV_ERROR_OUT_OF_MEMORY;
         }
         p->device = dev;
+        p->arena.device = dev;
+        if (const char *e = probe_env("SPMV_ARENA_VMM_MB")) p->arena.vmm_min = (size_t)std::max(0, std::atoi(e)) << 20;
         p->m = m;
         p->n = n;
         p->nnz = nnz;

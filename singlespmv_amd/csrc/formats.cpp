@@ -19,6 +19,7 @@ namespace spmv {
 
 int DevArena::alloc(void **p, size_t n) {
     if (n == 0) n = 16;
+    if (vmm_min > 0 && n >= vmm_min) return alloc_vmm(p, n, kVmmChunk, device, kVmmAlign);
     void *q = nullptr;
     hipError_t e = hipMalloc(&q, n);
     if (e != hipSuccess) {
@@ -721,9 +722,26 @@ int build_dia(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
         }
     SPMV_RETURN_IF(upload(p, &d.off, offs.data(), d.n_diags));
     if (const char *e = probe_env("SPMV_DIA_DEBUG")) d.dbg = std::atoi(e);
-    SPMV_RETURN_IF(upload(p, &d.val, val.data(), slots));
     p->stored_slots = slots;
-    SPMV_RETURN_IF(dia_placement(p, A.m, A.n, (size_t)slots * sizeof(double), o));
+    // AUTO: values of >= 256 MB go straight into 2-MB VMM handles mapped at a
+    // 1-GB-aligned VA (config 4: 1.537-1.61 ms against 1.665-1.677 with one
+    // plain hipMalloc, profiles/round3/probe/dia_placement_vmm.jsonl; the
+    // same placement as BIN's product buffer)
+    const size_t vbytes = (size_t)std::max<int64_t>(slots, 1) * sizeof(double);
+    spmv_options_t oo = o;
+    SPMV_RETURN_IF(placement_mode_check(oo.placement));
+    if (oo.placement == SPMV_PLACEMENT_AUTO)
+        oo.placement = vbytes >= kDiaVmmMinBytes ? SPMV_PLACEMENT_VMM : SPMV_PLACEMENT_PLAIN;
+    if (oo.placement == SPMV_PLACEMENT_VMM && !probe_env("SPMV_PLACEMENT_MODE")) {
+        void *q = nullptr;
+        SPMV_RETURN_IF(p->arena.alloc_vmm(&q, vbytes, kVmmChunk, p->device, kVmmAlign));
+        SPMV_HIP_TRY(hipMemcpy(q, val.data(), vbytes, hipMemcpyHostToDevice));
+        d.val = (double *)q;
+        d.placement = SPMV_PLACEMENT_VMM;
+    } else {
+        SPMV_RETURN_IF(upload(p, &d.val, val.data(), slots));
+        SPMV_RETURN_IF(dia_placement(p, A.m, A.n, vbytes, oo));
+    }
     p->algo_bytes = 8 * A.nnz + 4 * (int64_t)d.n_diags + 8 * A.n + 8 * A.m;
     p->n_kernels = 1;
     p->kernel_name = "dia_kernel";

@@ -75,6 +75,7 @@ inline int placement_mode_check(int mode) {
 constexpr size_t kVmmChunk = (size_t)2 << 20;          // physical handle size
 constexpr size_t kVmmAlign = (size_t)1 << 30;          // VA alignment of the mapping
 constexpr size_t kBinVmmMinBytes = (size_t)32 << 20;   // AUTO: VMM from this product-buffer size
+constexpr size_t kDiaVmmMinBytes = (size_t)256 << 20;  // AUTO: VMM from this DIA value size
 
 // ---- device memory owned by a plan --------------------------------------
 // Plain hipMalloc allocations, plus buffers mapped through the HIP virtual
@@ -92,7 +93,9 @@ struct DevArena {
     std::vector<void *> ptrs;
     std::vector<VmmMap> maps;
     int64_t bytes = 0;
-    int alloc(void **p, size_t n);  // hipMalloc, zero-size safe
+    int device = 0;
+    size_t vmm_min = 0;  // > 0: alloc() of >= vmm_min bytes maps 2-MB VMM handles instead
+    int alloc(void **p, size_t n);  // hipMalloc (or VMM, above), zero-size safe
     // n bytes of physical memory in `chunk`-byte handles mapped at one VA range
     // (align > 0: the mapping starts at a multiple of `align` inside a larger
     // reservation -- hipMemAddressReserve itself honours only the granularity)

@@ -721,8 +721,9 @@ def test_plan_create_holds_only_the_plan(fmt, kind):
     for i in range(10 if fmt == "bin" else 2):
         plan, drop = _create_peak_drop(lambda: sp.Plan.from_csr(m, m, rp, col, val, fmt))
         info = plan.info()
-        # AUTO: BIN's product buffer (>= 32 MB) from 2-MB VMM handles, DIA plain
-        assert info["format"] == fmt and info["placement"] == ("vmm" if fmt == "bin" else "plain")
+        # AUTO: BIN's product buffer (>= 32 MB) and DIA's values (>= 256 MB)
+        # from 2-MB VMM handles
+        assert info["format"] == fmt and info["placement"] == "vmm"
         assert drop <= info["device_bytes"] + (128 << 20), (i, drop, info["device_bytes"])
         plan.destroy()
     with pytest.raises(sp.SpmvError, match="probe build"):
