@@ -278,6 +278,17 @@ static int bin_rows(spmv_plan_s *p, const int64_t *row_ptr, int64_t m, int64_t n
     return SPMV_SUCCESS;
 }
 
+// Mul rotation (B.mul_rot): strip t visits its group's bins starting at
+// position rot(t) of mul_bins, rot(t) = t * 0.618 * bins mod bins, so the
+// workgroups -- each on its own strip at a time -- write their product
+// segments into different bins' runs all over the product buffer instead of
+// all into the same bin's run
+static inline int64_t bin_mul_rot(const BinDev &B, int64_t t, int64_t nbg) {
+    if (!B.mul_rot || nbg <= 1) return 0;
+    const int64_t step = std::max<int64_t>(1, (int64_t)(0.6180339887 * (double)nbg + 0.5));
+    return (int64_t)(((__int128)t * step) % nbg);
+}
+
 // ---- offsets from the counts: row groups, Sum (product) order
 // [block][b][s in block], Mul order [g][s][b]
 static void bin_offsets(spmv_plan_s *p, const spmv_options_t &o, BinLayout &L) {
@@ -386,14 +397,17 @@ static void bin_offsets(spmv_plan_s *p, const spmv_options_t &o, BinLayout &L) {
         }
         for (int64_t i = 0; i < nbg; ++i) L.mul_bins[(size_t)(g0 + i)] = g0 + (int64_t)(((__int128)i * P) % nbg);
     }
+    if (const char *e = probe_env("SPMV_BIN_MUL_ROT")) B.mul_rot = std::atoi(e) != 0;
     L.strip_start.assign((size_t)G * (S + 1), 0);
     if (L.LL > 0) L.lstart.assign((size_t)S, 0);
     for (int g = 0; g < G; ++g) {
         int64_t cur = B.g_prod[(size_t)g];
+        const int64_t g0 = B.g_bin[(size_t)g], nbg = B.g_bin[(size_t)g + 1] - g0;
         for (int64_t t = 0; t < S; ++t) {
             L.strip_start[(size_t)(g * (S + 1) + t)] = cur;
-            for (int64_t i = B.g_bin[(size_t)g]; i < B.g_bin[(size_t)g + 1]; ++i) {
-                const int64_t b = L.mul_bins[(size_t)i];
+            const int64_t rot = bin_mul_rot(B, t, nbg);
+            for (int64_t j = 0; j < nbg; ++j) {
+                const int64_t b = L.mul_bins[(size_t)(g0 + (j + rot) % nbg)];
                 L.off1[(size_t)(b * S + t)] = cur;
                 cur += L.rpad(L.cnt[(size_t)(b * S + t)]);
             }
@@ -668,6 +682,50 @@ static int bin_place_search(spmv_plan_s *p, int64_t n, size_t prod_bytes) {
 }
 #endif  // SPMV_PROBES
 
+// The product buffer in 2-MB VMM handles; with K > 1 candidates, each timed
+// with one Mul pass over a zero x (results never depend on it), the fastest
+// kept and the others freed: transient device memory K - 1 buffers + x.
+static int bin_place_vmm(spmv_plan_s *p, int64_t n, size_t prod_bytes, size_t chunk, size_t align, int K) {
+    BinDev &B = p->bin;
+    if (K <= 1) {
+        void *q = nullptr;
+        SPMV_RETURN_IF(p->arena.alloc_vmm(&q, prod_bytes, chunk, p->device, align));
+        B.prod = (double *)q;
+        return SPMV_SUCCESS;
+    }
+    double *xz = nullptr;
+    const size_t xb = sizeof(double) * (size_t)std::max<int64_t>(n, 1);
+    SPMV_HIP_TRY(hipMalloc(&xz, xb));
+    int st = hipMemset(xz, 0, xb) == hipSuccess ? SPMV_SUCCESS : SPMV_ERROR_HIP;
+    std::vector<double *> cand;
+    std::vector<float> t;
+    for (int k = 0; k < K && st == SPMV_SUCCESS; ++k) {
+        void *q = nullptr;
+        if (p->arena.alloc_vmm(&q, prod_bytes, chunk, p->device, align) != SPMV_SUCCESS) {
+            (void)hipGetLastError();
+            if (cand.empty()) st = SPMV_ERROR_OUT_OF_MEMORY;
+            break;  // rank the candidates that fit
+        }
+        cand.push_back((double *)q);
+        B.prod = (double *)q;
+        float ms = 0;
+        st = bin_time_mul(p, xz, &ms);
+        t.push_back(ms);
+    }
+    (void)hipFree(xz);
+    if (st != SPMV_SUCCESS || t.empty()) {
+        for (double *c : cand) p->arena.free(c);
+        B.prod = nullptr;
+        return st != SPMV_SUCCESS ? st : SPMV_ERROR_OUT_OF_MEMORY;
+    }
+    const size_t best = (size_t)(std::min_element(t.begin(), t.end()) - t.begin());
+    for (size_t k = 0; k < cand.size(); ++k)
+        if (k != best) p->arena.free(cand[k]);
+    B.prod = cand[best];
+    B.placement_ms.assign(t.begin(), t.end());
+    return SPMV_SUCCESS;
+}
+
 static int bin_place_prod(spmv_plan_s *p, int64_t n, size_t prod_bytes, const spmv_options_t &o) {
     BinDev &B = p->bin;
     int mode = o.placement;
@@ -694,10 +752,9 @@ static int bin_place_prod(spmv_plan_s *p, int64_t n, size_t prod_bytes, const sp
         size_t chunk = kVmmChunk, align = kVmmAlign;
         if (const char *e = probe_env("SPMV_VMM_CHUNK_MB")) chunk = (size_t)std::max(1, std::atoi(e)) << 20;
         if (const char *e = probe_env("SPMV_VMM_ALIGN_MB")) align = (size_t)std::max(0, std::atoi(e)) << 20;
-        void *q = nullptr;
-        SPMV_RETURN_IF(p->arena.alloc_vmm(&q, prod_bytes, chunk, p->device, align));
-        B.prod = (double *)q;
-        return SPMV_SUCCESS;
+        int K = 1;
+        if (const char *e = probe_env("SPMV_BIN_PROD_CAND")) K = std::max(1, std::min(8, std::atoi(e)));
+        return bin_place_vmm(p, n, prod_bytes, chunk, align, K);
     }
     return alloc_prod_plain(p, prod_bytes);
 }

@@ -315,6 +315,7 @@ struct BinDev {
     int64_t prod_cap = 0;
     int placement = 0;            // how prod was allocated (spmv_options_t.placement, resolved)
     bool mul_perm = false;        // Mul visits a strip's bins in scrambled order (build_bin.cpp)
+    bool mul_rot = false;         // ... starting at a per-strip rotation (build_bin.cpp bin_mul_rot)
     int64_t long_len = 0;         // rows with >= long_len entries take the run path (0: none)
     int64_t long_rows = 0, long_pieces = 0, long_entries = 0;
     int64_t mul_entries = 0;      // Mul-order length (segments + voids + long blocks)
