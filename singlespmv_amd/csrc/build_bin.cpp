@@ -278,17 +278,6 @@ static int bin_rows(spmv_plan_s *p, const int64_t *row_ptr, int64_t m, int64_t n
     return SPMV_SUCCESS;
 }
 
-// Mul rotation (B.mul_rot): strip t visits its group's bins starting at
-// position rot(t) of mul_bins, rot(t) = t * 0.618 * bins mod bins, so the
-// workgroups -- each on its own strip at a time -- write their product
-// segments into different bins' runs all over the product buffer instead of
-// all into the same bin's run
-static inline int64_t bin_mul_rot(const BinDev &B, int64_t t, int64_t nbg) {
-    if (!B.mul_rot || nbg <= 1) return 0;
-    const int64_t step = std::max<int64_t>(1, (int64_t)(0.6180339887 * (double)nbg + 0.5));
-    return (int64_t)(((__int128)t * step) % nbg);
-}
-
 // ---- offsets from the counts: row groups, Sum (product) order
 // [block][b][s in block], Mul order [g][s][b]
 static void bin_offsets(spmv_plan_s *p, const spmv_options_t &o, BinLayout &L) {
@@ -397,7 +386,6 @@ static void bin_offsets(spmv_plan_s *p, const spmv_options_t &o, BinLayout &L) {
         }
         for (int64_t i = 0; i < nbg; ++i) L.mul_bins[(size_t)(g0 + i)] = g0 + (int64_t)(((__int128)i * P) % nbg);
     }
-    if (const char *e = probe_env("SPMV_BIN_MUL_ROT")) B.mul_rot = std::atoi(e) != 0;
     L.strip_start.assign((size_t)G * (S + 1), 0);
     if (L.LL > 0) L.lstart.assign((size_t)S, 0);
     for (int g = 0; g < G; ++g) {
@@ -405,9 +393,8 @@ static void bin_offsets(spmv_plan_s *p, const spmv_options_t &o, BinLayout &L) {
         const int64_t g0 = B.g_bin[(size_t)g], nbg = B.g_bin[(size_t)g + 1] - g0;
         for (int64_t t = 0; t < S; ++t) {
             L.strip_start[(size_t)(g * (S + 1) + t)] = cur;
-            const int64_t rot = bin_mul_rot(B, t, nbg);
             for (int64_t j = 0; j < nbg; ++j) {
-                const int64_t b = L.mul_bins[(size_t)(g0 + (j + rot) % nbg)];
+                const int64_t b = L.mul_bins[(size_t)(g0 + j)];
                 L.off1[(size_t)(b * S + t)] = cur;
                 cur += L.rpad(L.cnt[(size_t)(b * S + t)]);
             }

@@ -193,6 +193,12 @@ struct CooDev {
 // (0 where absent / outside), offsets ascending -- each workgroup streams one
 // contiguous n_diags*B*8-byte block.
 constexpr int kDiaBlockRows = 512;
+// rotation of block b's diagonal slots (DiaDev::rot): concurrent workgroups
+// read different 4-KB slots of their blocks instead of the same offset of
+// blocks 256 KB apart
+__host__ __device__ inline int dia_rot(int64_t blk, int nd) {
+    return nd > 1 ? (int)(((uint64_t)blk * 2654435761ull) % (uint64_t)nd) : 0;
+}
 struct DiaDev {
     int n_diags = 0;
     int32_t *off = nullptr;  // device copy of offsets
@@ -200,6 +206,7 @@ struct DiaDev {
     double *val = nullptr;   // [n_diags * mp]
     int64_t mp = 0;          // m rounded up to kDiaBlockRows
     int dbg = 0;             // SPMV_DIA_DEBUG (internal): 1 = x from global memory, no LDS window
+    int rot = 0;             // 1: block b stores diagonal d at slot (d + dia_rot(b)) % n_diags
     int placement = 0;       // SPMV_PLACEMENT_* used for val
     std::vector<float> placement_ms;
 };
@@ -315,7 +322,6 @@ struct BinDev {
     int64_t prod_cap = 0;
     int placement = 0;            // how prod was allocated (spmv_options_t.placement, resolved)
     bool mul_perm = false;        // Mul visits a strip's bins in scrambled order (build_bin.cpp)
-    bool mul_rot = false;         // ... starting at a per-strip rotation (build_bin.cpp bin_mul_rot)
     int64_t long_len = 0;         // rows with >= long_len entries take the run path (0: none)
     int64_t long_rows = 0, long_pieces = 0, long_entries = 0;
     int64_t mul_entries = 0;      // Mul-order length (segments + voids + long blocks)

@@ -213,7 +213,6 @@ int main() {
                     B.pad_log = pl;
                     B.nwg1 = B.nwg2 = 256;
                     B.mul_perm = (si + wi + pl) % 2 == 0;  // both Mul bin orders
-                    B.mul_rot = (si + pl) % 2 == 1;        // with and without per-strip rotation
                     spmv_options_t o;
                     std::memset(&o, 0, sizeof(o));
                     BinLayout L;
@@ -251,9 +250,8 @@ int main() {
                     cur = 0;
                     for (int64_t t = 0; t < S; ++t) {
                         if (L.strip_start[(size_t)t] != cur) return fail("strip_start", t, cur);
-                        const int64_t rot = bin_mul_rot(B, t, NB);
                         for (int64_t i = 0; i < NB; ++i) {
-                            const int64_t b = L.mul_bins[(size_t)((i + rot) % NB)];
+                            const int64_t b = L.mul_bins[(size_t)i];
                             if (L.off1[(size_t)(b * S + t)] != cur) return fail("off1", b * S + t, cur);
                             cur += L.rpad(L.cnt[(size_t)(b * S + t)]);
                         }
