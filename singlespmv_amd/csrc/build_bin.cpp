@@ -669,50 +669,6 @@ static int bin_place_search(spmv_plan_s *p, int64_t n, size_t prod_bytes) {
 }
 #endif  // SPMV_PROBES
 
-// The product buffer in 2-MB VMM handles; with K > 1 candidates, each timed
-// with one Mul pass over a zero x (results never depend on it), the fastest
-// kept and the others freed: transient device memory K - 1 buffers + x.
-static int bin_place_vmm(spmv_plan_s *p, int64_t n, size_t prod_bytes, size_t chunk, size_t align, int K) {
-    BinDev &B = p->bin;
-    if (K <= 1) {
-        void *q = nullptr;
-        SPMV_RETURN_IF(p->arena.alloc_vmm(&q, prod_bytes, chunk, p->device, align));
-        B.prod = (double *)q;
-        return SPMV_SUCCESS;
-    }
-    double *xz = nullptr;
-    const size_t xb = sizeof(double) * (size_t)std::max<int64_t>(n, 1);
-    SPMV_HIP_TRY(hipMalloc(&xz, xb));
-    int st = hipMemset(xz, 0, xb) == hipSuccess ? SPMV_SUCCESS : SPMV_ERROR_HIP;
-    std::vector<double *> cand;
-    std::vector<float> t;
-    for (int k = 0; k < K && st == SPMV_SUCCESS; ++k) {
-        void *q = nullptr;
-        if (p->arena.alloc_vmm(&q, prod_bytes, chunk, p->device, align) != SPMV_SUCCESS) {
-            (void)hipGetLastError();
-            if (cand.empty()) st = SPMV_ERROR_OUT_OF_MEMORY;
-            break;  // rank the candidates that fit
-        }
-        cand.push_back((double *)q);
-        B.prod = (double *)q;
-        float ms = 0;
-        st = bin_time_mul(p, xz, &ms);
-        t.push_back(ms);
-    }
-    (void)hipFree(xz);
-    if (st != SPMV_SUCCESS || t.empty()) {
-        for (double *c : cand) p->arena.free(c);
-        B.prod = nullptr;
-        return st != SPMV_SUCCESS ? st : SPMV_ERROR_OUT_OF_MEMORY;
-    }
-    const size_t best = (size_t)(std::min_element(t.begin(), t.end()) - t.begin());
-    for (size_t k = 0; k < cand.size(); ++k)
-        if (k != best) p->arena.free(cand[k]);
-    B.prod = cand[best];
-    B.placement_ms.assign(t.begin(), t.end());
-    return SPMV_SUCCESS;
-}
-
 static int bin_place_prod(spmv_plan_s *p, int64_t n, size_t prod_bytes, const spmv_options_t &o) {
     BinDev &B = p->bin;
     int mode = o.placement;
@@ -739,9 +695,10 @@ static int bin_place_prod(spmv_plan_s *p, int64_t n, size_t prod_bytes, const sp
         size_t chunk = kVmmChunk, align = kVmmAlign;
         if (const char *e = probe_env("SPMV_VMM_CHUNK_MB")) chunk = (size_t)std::max(1, std::atoi(e)) << 20;
         if (const char *e = probe_env("SPMV_VMM_ALIGN_MB")) align = (size_t)std::max(0, std::atoi(e)) << 20;
-        int K = 1;
-        if (const char *e = probe_env("SPMV_BIN_PROD_CAND")) K = std::max(1, std::min(8, std::atoi(e)));
-        return bin_place_vmm(p, n, prod_bytes, chunk, align, K);
+        void *q = nullptr;
+        SPMV_RETURN_IF(p->arena.alloc_vmm(&q, prod_bytes, chunk, p->device, align));
+        B.prod = (double *)q;
+        return SPMV_SUCCESS;
     }
     return alloc_prod_plain(p, prod_bytes);
 }

@@ -193,12 +193,7 @@ struct CooDev {
 // (0 where absent / outside), offsets ascending -- each workgroup streams one
 // contiguous n_diags*B*8-byte block.
 constexpr int kDiaBlockRows = 512;
-// rotation of block b's diagonal slots (DiaDev::rot): concurrent workgroups
-// read different 4-KB slots of their blocks instead of the same offset of
-// blocks 256 KB apart
-__host__ __device__ inline int dia_rot(int64_t blk, int nd) {
-    return nd > 1 ? (int)(((uint64_t)blk * 2654435761ull) % (uint64_t)nd) : 0;
-}
+
 struct DiaDev {
     int n_diags = 0;
     int32_t *off = nullptr;  // device copy of offsets
@@ -206,7 +201,6 @@ struct DiaDev {
     double *val = nullptr;   // [n_diags * mp]
     int64_t mp = 0;          // m rounded up to kDiaBlockRows
     int dbg = 0;             // SPMV_DIA_DEBUG (internal): 1 = x from global memory, no LDS window
-    int rot = 0;             // 1: block b stores diagonal d at slot (d + dia_rot(b)) % n_diags
     int placement = 0;       // SPMV_PLACEMENT_* used for val
     std::vector<float> placement_ms;
 };

@@ -215,11 +215,7 @@ __global__ __launch_bounds__(kBinMulThreads) void bin_mul_kernel(
         __syncthreads();
         const int64_t first = e0 + (int64_t)w * 64 * U;
         const int64_t nit = first < e1 ? (e1 - first + STEP - 1) / STEP : 0;
-        // MODE 256 (probe): the workgroups start their pieces at staggered
-        // batches (rotation by blockIdx), so their entry streams do not
-        // advance in lockstep at a fixed stride
-        const int64_t rot = (MODE & 256) && nit > 1 ? (int64_t)(((uint64_t)blockIdx.x * 2654435761u) % (uint64_t)nit) : 0;
-        auto bat = [&](int64_t j) { return first + (rot ? (j + rot) % nit : j) * STEP; };
+        auto bat = [&](int64_t j) { return first + j * STEP; };
         MulBatch<U> A, B;
         if (nit > 0) mul_load<U, PL, MODE, LONG>(A, bat(0), e0, e1, lane, val1, cs1, dst1, ls, lsh, lcode);
         for (int64_t it = 0; it < nit; it += 2) {
@@ -501,8 +497,7 @@ static void launch_mul_p(const spmv_plan_s *p, int g, const double *x) {
             // long-block partial stores: 2048 nontemporal, 4096 none (ablations);
             // 16384: loads clamped at the piece's end (A/B); 131072 / 262144:
             // x strips staged serially / in bursts (A/B, build_bin.cpp xburst)
-            if (p->bin.dbg & (1 << 20)) launch_mul_t<257, PL>(p, g, x);  // staggered batch order
-            else if (p->bin.dbg & 16384) launch_mul_t<65, PL>(p, g, x);
+            if (p->bin.dbg & 16384) launch_mul_t<65, PL>(p, g, x);
             else if (p->bin.dbg & 2048) launch_mul_t<17, PL>(p, g, x);
             else if (p->bin.dbg & 4096) launch_mul_t<33, PL>(p, g, x);
             else launch_mul_t<1, PL>(p, g, x);

@@ -30,15 +30,11 @@ __global__ __launch_bounds__(256) void dia_kernel(int64_t m, int64_t mp, int64_t
                                                   const int32_t *__restrict__ off, int32_t off_min, int32_t win,
                                                   const double *__restrict__ val,
                                                   const double *__restrict__ x,
-                                                  double *__restrict__ y, int rot_on) {
+                                                  double *__restrict__ y) {
     extern __shared__ double xs[];
     const int64_t r0 = 2 * (int64_t)blockIdx.x * blockDim.x;
     const int64_t r = r0 + 2 * threadIdx.x;
     const double *vb = val + (int64_t)blockIdx.x * n_diags * kDiaBlockRows + 2 * threadIdx.x;
-    // the block's diagonal slots may be rotated (DiaDev::rot): diagonal d at
-    // slot (d + rot) mod n_diags; summed in d order either way
-    const int rot = rot_on ? dia_rot(blockIdx.x, n_diags) : 0;
-    auto slot = [&](int dd) { const int q = dd + rot; return q >= n_diags ? q - n_diags : q; };
     auto xat = [&](int64_t c) { return x[c < 0 ? 0 : (c >= n ? n - 1 : c)]; };
     if (LDSX) {
         // out-of-range columns only meet zero-filled slots: any finite x works
@@ -54,7 +50,7 @@ __global__ __launch_bounds__(256) void dia_kernel(int64_t m, int64_t mp, int64_t
         f64x2 v[UNROLL];
         double g0[UNROLL], g1[UNROLL];
 #pragma unroll
-        for (int u = 0; u < UNROLL; ++u) v[u] = ld_stream2(vb + (int64_t)slot(d + u) * kDiaBlockRows);
+        for (int u = 0; u < UNROLL; ++u) v[u] = ld_stream2(vb + (int64_t)(d + u) * kDiaBlockRows);
 #pragma unroll
         for (int u = 0; u < UNROLL; ++u) {
             if (LDSX) {
@@ -74,7 +70,7 @@ __global__ __launch_bounds__(256) void dia_kernel(int64_t m, int64_t mp, int64_t
         }
     }
     for (; d < n_diags; ++d) {
-        const f64x2 v = ld_stream2(vb + (int64_t)slot(d) * kDiaBlockRows);
+        const f64x2 v = ld_stream2(vb + (int64_t)d * kDiaBlockRows);
         double a, b;
         if (LDSX) {
             const int li = lbase + off[d];
@@ -117,10 +113,10 @@ int launch_dia(const spmv_plan_s *p, const double *x, double *y) {
     const int64_t win = 512 + (int64_t)off_max - off_min + 1;
     if (win <= kDiaMaxWin && !(p->dia.dbg & 1))
         hipLaunchKernelGGL((dia_kernel<8, true>), dim3((unsigned)blocks), dim3(256), sizeof(double) * (size_t)win,
-                           p->stream, p->m, d.mp, p->n, d.n_diags, d.off, off_min, (int32_t)win, d.val, x, y, d.rot);
+                           p->stream, p->m, d.mp, p->n, d.n_diags, d.off, off_min, (int32_t)win, d.val, x, y);
     else
         hipLaunchKernelGGL((dia_kernel<8, false>), dim3((unsigned)blocks), dim3(256), 0, p->stream, p->m, d.mp,
-                           p->n, d.n_diags, d.off, off_min, 0, d.val, x, y, d.rot);
+                           p->n, d.n_diags, d.off, off_min, 0, d.val, x, y);
     SPMV_HIP_TRY(hipGetLastError());
     return SPMV_SUCCESS;
 }
