@@ -197,7 +197,10 @@ __global__ __launch_bounds__(kBinMulThreads) void bin_mul_kernel(
         // instead of 20); else, and always with long rows (their run path's
         // live registers would spill), one load per round trip
         constexpr int XL = 8;
-        if (LONG || !xburst) {
+        if constexpr ((MODE & 512) != 0) {
+            // ablation (probe, wrong results): no x strip loads -- the cost of
+            // staging x, in the Mul's time
+        } else if (LONG || !xburst) {
             for (int i = threadIdx.x; i < cw; i += kBinMulThreads) xs[i] = x[c0 + i];
         } else for (int i0 = threadIdx.x; i0 < cw; i0 += XL * kBinMulThreads) {
             double t[XL];
@@ -497,7 +500,8 @@ static void launch_mul_p(const spmv_plan_s *p, int g, const double *x) {
             // long-block partial stores: 2048 nontemporal, 4096 none (ablations);
             // 16384: loads clamped at the piece's end (A/B); 131072 / 262144:
             // x strips staged serially / in bursts (A/B, build_bin.cpp xburst)
-            if (p->bin.dbg & 16384) launch_mul_t<65, PL>(p, g, x);
+            if (p->bin.dbg & (1 << 21)) launch_mul_t<513, PL>(p, g, x);  // ablation: no x staging
+            else if (p->bin.dbg & 16384) launch_mul_t<65, PL>(p, g, x);
             else if (p->bin.dbg & 2048) launch_mul_t<17, PL>(p, g, x);
             else if (p->bin.dbg & 4096) launch_mul_t<33, PL>(p, g, x);
             else launch_mul_t<1, PL>(p, g, x);
