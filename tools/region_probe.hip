@@ -78,10 +78,13 @@ __global__ __launch_bounds__(256) void rd_blocked(const f64x2 *__restrict__ a, l
 // from A to C; a bandwidth-bound one does not.
 static int frag_mode(int reps);
 static int alloc_mode(int reps);
+static int dia_mode(int nalloc, long long gb);
 
 int main(int argc, char **argv) {
     if (argc > 1 && std::string(argv[1]) == "frag") return frag_mode(argc > 2 ? std::atoi(argv[2]) : 3);
     if (argc > 1 && std::string(argv[1]) == "alloc") return alloc_mode(argc > 2 ? std::atoi(argv[2]) : 3);
+    if (argc > 1 && std::string(argv[1]) == "dia")
+        return dia_mode(argc > 2 ? std::atoi(argv[2]) : 6, argc > 3 ? std::atoll(argv[3]) : 10);
     const long long chunk = (argc > 1 ? std::atoll(argv[1]) : 1024) << 20;
     const long long keep = (argc > 2 ? std::atoll(argv[2]) : 16) << 30;
     const int reps = argc > 3 ? std::atoi(argv[3]) : 3;
@@ -395,5 +398,67 @@ static int alloc_mode(int reps) {
         }
         CHECK(hipMemAddressFree(v.va, v.size));
     }
+    return 0;
+}
+
+// "dia" mode: the DIA kernel's value stream alone -- workgroup b (256
+// threads, 16-byte loads, 8 in flight per lane) streams its own contiguous
+// 256 KB block (the blocked layout, 64 diagonals x 512 rows) -- over
+// `nalloc` separate allocations of `gb` GB each, kept (so each is new
+// memory), three times each; next to the same bytes read grid-stride.
+// Does the rate vary from allocation to allocation like dia_kernel's
+// (1.51-1.68 ms at config 4), and which pattern is immune?
+__global__ __launch_bounds__(256) void rd_dia(const f64x2 *__restrict__ a, long long blk2, double *__restrict__ out) {
+    const f64x2 *b = a + (long long)blockIdx.x * blk2 + threadIdx.x;
+    double s = 0;
+    for (long long i = 0; i < blk2; i += 256 * 8) {
+        f64x2 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = __builtin_nontemporal_load(b + i + u * 256);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s += v[u].x + v[u].y;
+    }
+    if (s == 1.2345) out[0] = s;
+}
+
+static int dia_mode(int nalloc, long long gb) {
+    double *out;
+    CHECK(hipMalloc(&out, 64));
+    hipEvent_t a, b;
+    CHECK(hipEventCreate(&a));
+    CHECK(hipEventCreate(&b));
+    const long long bytes = gb << 30, n2 = bytes / 16, blk2 = (256LL << 10) / 16, nblk = n2 / blk2;
+    auto time = [&](auto launch) {
+        launch();
+        CHECK(hipDeviceSynchronize());
+        float bms = 1e30f;
+        for (int r = 0; r < 3; ++r) {
+            CHECK(hipEventRecord(a));
+            launch();
+            CHECK(hipEventRecord(b));
+            CHECK(hipEventSynchronize(b));
+            float ms;
+            CHECK(hipEventElapsedTime(&ms, a, b));
+            if (ms < bms) bms = ms;
+        }
+        return bms;
+    };
+    std::vector<void *> keep;
+    for (int k = 0; k < nalloc; ++k) {
+        void *p = nullptr;
+        if (hipMalloc(&p, bytes) != hipSuccess) {
+            (void)hipGetLastError();
+            break;
+        }
+        keep.push_back(p);
+        CHECK(hipMemset(p, 0, bytes));
+        const float td = time([&] { rd_dia<<<(unsigned)nblk, 256>>>((const f64x2 *)p, blk2, out); });
+        const float tg = time([&] { rd<<<4096, 256>>>((const f64x2 *)p, n2, out); });
+        std::printf("{\"alloc\": %d, \"gb\": %lld, \"va\": \"%p\", \"dia_blocked_ms\": %.4f, \"dia_blocked_gbs\": %.0f, "
+                    "\"gridstride_ms\": %.4f, \"gridstride_gbs\": %.0f}\n",
+                    k, gb, p, td, bytes / td / 1e6, tg, bytes / tg / 1e6);
+        std::fflush(stdout);
+    }
+    for (void *p : keep) CHECK(hipFree(p));
     return 0;
 }
