@@ -25,7 +25,7 @@ namespace spmv {
 // coalesced loads and every diagonal reads its pair x[c], x[c+1] from there,
 // so the only HBM stream left is val (and x once).  Without LDSX (diagonal
 // span too wide for the window) x is read from global memory per diagonal.
-template <int UNROLL, bool LDSX>
+template <int UNROLL, bool LDSX, int YMODE = 0>
 __global__ __launch_bounds__(256) void dia_kernel(int64_t m, int64_t mp, int64_t n, int n_diags,
                                                   const int32_t *__restrict__ off, int32_t off_min, int32_t win,
                                                   const double *__restrict__ val,
@@ -90,7 +90,9 @@ __global__ __launch_bounds__(256) void dia_kernel(int64_t m, int64_t mp, int64_t
         f64x2 yv;
         yv.x = acc0;
         yv.y = acc1;
-        __builtin_nontemporal_store(yv, reinterpret_cast<f64x2 *>(y + r));
+        // YMODE 1 (probe A/B): ordinary 16-byte stores (y lines stay in L2)
+        if constexpr (YMODE == 1) *reinterpret_cast<f64x2 *>(y + r) = yv;
+        else __builtin_nontemporal_store(yv, reinterpret_cast<f64x2 *>(y + r));
     } else {
         y[r] = acc0;
         if (r + 1 < m) y[r + 1] = acc1;
@@ -111,7 +113,10 @@ int launch_dia(const spmv_plan_s *p, const double *x, double *y) {
     const int64_t blocks = (pairs + 255) / 256;
     const int32_t off_min = d.off_host.front(), off_max = d.off_host.back();
     const int64_t win = 512 + (int64_t)off_max - off_min + 1;
-    if (win <= kDiaMaxWin && !(p->dia.dbg & 1))
+    if (win <= kDiaMaxWin && (p->dia.dbg & 2))  // probe A/B: ordinary y stores
+        hipLaunchKernelGGL((dia_kernel<8, true, 1>), dim3((unsigned)blocks), dim3(256), sizeof(double) * (size_t)win,
+                           p->stream, p->m, d.mp, p->n, d.n_diags, d.off, off_min, (int32_t)win, d.val, x, y);
+    else if (win <= kDiaMaxWin && !(p->dia.dbg & 1))
         hipLaunchKernelGGL((dia_kernel<8, true>), dim3((unsigned)blocks), dim3(256), sizeof(double) * (size_t)win,
                            p->stream, p->m, d.mp, p->n, d.n_diags, d.off, off_min, (int32_t)win, d.val, x, y);
     else
