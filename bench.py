@@ -302,10 +302,17 @@ def time_formats(ctx, args, M, fmts, trials_head: int):
     results, headline, y_head = {}, None, None
     for fi, fmt in enumerate(fmts):
         tp = time.time()
+        plan, err = None, None
         try:
             plan = sp.Plan.from_csr(M["rows"], M["n"], M["rp"], M["col"], M["val"], fmt=fmt, device=ctx.local)
         except sp.SpmvError as e:
-            results[fmt] = {"error": str(e)}
+            err = str(e)
+        # every rank skips a format that failed on any rank (the timed trials
+        # below are collective: one rank skipping them alone would hang)
+        if ctx.sdist.sum_over_ranks([0.0 if plan is None else 1.0], ctx.dev)[0] < ctx.world:
+            results[fmt] = {"error": err or "failed on another rank"}
+            if plan is not None:
+                plan.destroy()
             continue
         t_plan = time.time() - tp
         info = plan.info()
