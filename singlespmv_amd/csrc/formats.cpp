@@ -722,6 +722,7 @@ int build_dia(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
         }
     SPMV_RETURN_IF(upload(p, &d.off, offs.data(), d.n_diags));
     if (const char *e = probe_env("SPMV_DIA_DEBUG")) d.dbg = std::atoi(e);
+    if (const char *e = probe_env("SPMV_DIA_LDS_KB")) d.lds_kb = std::atoi(e);
     p->stored_slots = slots;
     // AUTO: values of >= 256 MB go straight into 2-MB VMM handles mapped at a
     // 1-GB-aligned VA (config 4: 1.537-1.61 ms against 1.665-1.677 with one

@@ -201,6 +201,7 @@ struct DiaDev {
     double *val = nullptr;   // [n_diags * mp]
     int64_t mp = 0;          // m rounded up to kDiaBlockRows
     int dbg = 0;             // SPMV_DIA_DEBUG (internal): 1 = x from global memory, no LDS window
+    int lds_kb = -1;         // SPMV_DIA_LDS_KB (probe): LDS per workgroup (0: window only); -1: kDiaLdsKb
     int placement = 0;       // SPMV_PLACEMENT_* used for val
     std::vector<float> placement_ms;
 };
