@@ -713,11 +713,18 @@ int build_dia(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
     const int64_t slots = (int64_t)d.n_diags * d.mp;
     std::vector<double> val((size_t)std::max<int64_t>(slots, 1), 0.0);
     const int64_t nd = d.n_diags;
+    if (const char *e = probe_env("SPMV_DIA_GROUP")) d.group = std::max(0, std::atoi(e));
+    const int64_t G = d.group, nblk = d.mp / kDiaBlockRows;
 #pragma omp parallel for schedule(static)
     for (int64_t r = 0; r < A.m; ++r)
         for (int64_t j = A.row_ptr[r]; j < A.row_ptr[r + 1]; ++j) {
             const int di = idx[(size_t)(A.col[j] - r + A.m - 1)];
-            const int64_t at = ((r / kDiaBlockRows) * nd + di) * kDiaBlockRows + r % kDiaBlockRows;
+            const int64_t b = r / kDiaBlockRows;
+            int64_t at = (b * nd + di) * kDiaBlockRows + r % kDiaBlockRows;
+            if (G > 0) {  // interleaved groups (k_dia.hip)
+                const int64_t t = b / G, g = b - t * G, gt = std::min(G, nblk - t * G);
+                at = (t * G * nd + di * gt + g) * kDiaBlockRows + r % kDiaBlockRows;
+            }
             val[(size_t)at] += A.val[j];  // duplicates are summed
         }
     SPMV_RETURN_IF(upload(p, &d.off, offs.data(), d.n_diags));

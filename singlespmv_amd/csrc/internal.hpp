@@ -57,6 +57,14 @@ inline const char *probe_env(const char *name) {
 #endif
 }
 
+// Probe build: SPMV_LAUNCH_DEBUG, read at every launch, replaces a plan's
+// SPMV_*_DEBUG kernel-selection bits -- launch-time variants A/B'd on ONE
+// plan, so on one placement (tools/bin_phase_ab.py --launch-variants).
+inline int launch_dbg(int plan_dbg) {
+    if (const char *e = probe_env("SPMV_LAUNCH_DEBUG")) return std::atoi(e);
+    return plan_dbg;
+}
+
 // The placement search (SPMV_PLACEMENT_SEARCH) exists only in
 // the probe build: the product library holds no transient device memory at
 // create and times nothing.  SPMV_PLACEMENT_VMM (2-MB physical handles mapped
@@ -201,6 +209,7 @@ struct DiaDev {
     double *val = nullptr;   // [n_diags * mp]
     int64_t mp = 0;          // m rounded up to kDiaBlockRows
     int dbg = 0;             // SPMV_DIA_DEBUG (internal): 1 = x from global memory, no LDS window
+    int group = 0;           // > 0: value blocks interleaved per group of blocks (k_dia.hip)
     int lds_kb = -1;         // SPMV_DIA_LDS_KB (probe): LDS per workgroup (0: window only); -1: kDiaLdsKb
     int placement = 0;       // SPMV_PLACEMENT_* used for val
     std::vector<float> placement_ms;

@@ -489,21 +489,22 @@ static void launch_mul_p(const spmv_plan_s *p, int g, const double *x) {
 #ifndef SPMV_PROBES
     launch_mul_t<1, PL>(p, g, x);
 #else
-    switch (p->bin.dbg & 3) {
+    const int dbg = launch_dbg(p->bin.dbg);
+    switch (dbg & 3) {
         case 1: launch_mul_t<0, PL>(p, g, x); break;
         case 2: launch_mul_t<2, PL>(p, g, x); break;
         case 3:  // ablations: sequential NT writes (+256: no cs1 loads either)
-            if (p->bin.dbg & 256) launch_mul_t<13, PL>(p, g, x);
+            if (dbg & 256) launch_mul_t<13, PL>(p, g, x);
             else launch_mul_t<5, PL>(p, g, x);
             break;
         default:
             // long-block partial stores: 2048 nontemporal, 4096 none (ablations);
             // 16384: loads clamped at the piece's end (A/B); 131072 / 262144:
             // x strips staged serially / in bursts (A/B, build_bin.cpp xburst)
-            if (p->bin.dbg & (1 << 21)) launch_mul_t<513, PL>(p, g, x);  // ablation: no x staging
-            else if (p->bin.dbg & 16384) launch_mul_t<65, PL>(p, g, x);
-            else if (p->bin.dbg & 2048) launch_mul_t<17, PL>(p, g, x);
-            else if (p->bin.dbg & 4096) launch_mul_t<33, PL>(p, g, x);
+            if (dbg & (1 << 21)) launch_mul_t<513, PL>(p, g, x);  // ablation: no x staging
+            else if (dbg & 16384) launch_mul_t<65, PL>(p, g, x);
+            else if (dbg & 2048) launch_mul_t<17, PL>(p, g, x);
+            else if (dbg & 4096) launch_mul_t<33, PL>(p, g, x);
             else launch_mul_t<1, PL>(p, g, x);
     }
 #endif
@@ -535,27 +536,28 @@ static void launch_sum_w(const spmv_plan_s *p, int g, double *y) {
     launch_sum_t<W2, U, 1 | 512>(p, g, y);
 #else
     // probe build: SPMV_BIN_DEBUG bits 2-3 -> Sum MODE
-    if (p->bin.dbg & 512) {  // ablation: no slot loads
+    const int dbg = launch_dbg(p->bin.dbg);
+    if (dbg & 512) {  // ablation: no slot loads
         launch_sum_t<W2, U, 4>(p, g, y);
         return;
     }
-    if (p->bin.dbg & 1024) {  // ablation: 16-byte product loads (wrong sums)
+    if (dbg & 1024) {  // ablation: 16-byte product loads (wrong sums)
         launch_sum_t<W2, U, 17>(p, g, y);
         return;
     }
-    if (p->bin.dbg & 8192) {  // A/B: product loads clamped at the run's end, masked adds
+    if (dbg & 8192) {  // A/B: product loads clamped at the run's end, masked adds
         launch_sum_t<W2, U, 33>(p, g, y);
         return;
     }
-    if (p->bin.dbg & 32768) {  // ablation: no LDS zeroing / y write-back (wrong y)
+    if (dbg & 32768) {  // ablation: no LDS zeroing / y write-back (wrong y)
         launch_sum_t<W2, U, 129>(p, g, y);
         return;
     }
-    if (p->bin.dbg & 524288) {  // A/B: ordinary y stores (the default's are nontemporal)
+    if (dbg & 524288) {  // A/B: ordinary y stores (the default's are nontemporal)
         launch_sum_t<W2, U, 1>(p, g, y);
         return;
     }
-    if (p->bin.dbg & 65536) {  // A/B: one bin at a time
+    if (dbg & 65536) {  // A/B: one bin at a time
         launch_sum_t<W2, U, 257>(p, g, y);
         return;
     }
@@ -566,7 +568,7 @@ static void launch_sum_w(const spmv_plan_s *p, int g, double *y) {
         launch_sum_t<W2, U, 9>(p, g, y);
         return;
     }
-    switch ((p->bin.dbg >> 2) & 3) {
+    switch ((dbg >> 2) & 3) {
         case 1: launch_sum_t<W2, U, 0>(p, g, y); break;
         case 2: launch_sum_t<W2, U, 2>(p, g, y); break;
         default: launch_sum_t<W2, U, 1 | 512>(p, g, y);

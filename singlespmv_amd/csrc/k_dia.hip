@@ -30,11 +30,21 @@ __global__ __launch_bounds__(256) void dia_kernel(int64_t m, int64_t mp, int64_t
                                                   const int32_t *__restrict__ off, int32_t off_min, int32_t win,
                                                   const double *__restrict__ val,
                                                   const double *__restrict__ x,
-                                                  double *__restrict__ y) {
+                                                  double *__restrict__ y, int32_t group) {
     extern __shared__ double xs[];
     const int64_t r0 = 2 * (int64_t)blockIdx.x * blockDim.x;
     const int64_t r = r0 + 2 * threadIdx.x;
-    const double *vb = val + (int64_t)blockIdx.x * n_diags * kDiaBlockRows + 2 * threadIdx.x;
+    // group > 0 (DiaDev::group): blocks interleaved per group of `group`
+    // consecutive blocks, diagonal by diagonal (the block's diagonal d at
+    // stride gt*512); else one contiguous n_diags*4 KB block
+    int64_t vbase = (int64_t)blockIdx.x * n_diags * kDiaBlockRows, dstride = kDiaBlockRows;
+    if (group > 0) {
+        const int64_t t = blockIdx.x / group, g = blockIdx.x - t * group;
+        const int64_t rest = mp / kDiaBlockRows - t * group;
+        vbase = (t * group * n_diags + g) * kDiaBlockRows;
+        dstride = (rest < group ? rest : group) * kDiaBlockRows;
+    }
+    const double *vb = val + vbase + 2 * threadIdx.x;
     auto xat = [&](int64_t c) { return x[c < 0 ? 0 : (c >= n ? n - 1 : c)]; };
     if (LDSX) {
         // out-of-range columns only meet zero-filled slots: any finite x works
@@ -50,7 +60,7 @@ __global__ __launch_bounds__(256) void dia_kernel(int64_t m, int64_t mp, int64_t
         f64x2 v[UNROLL];
         double g0[UNROLL], g1[UNROLL];
 #pragma unroll
-        for (int u = 0; u < UNROLL; ++u) v[u] = ld_stream2(vb + (int64_t)(d + u) * kDiaBlockRows);
+        for (int u = 0; u < UNROLL; ++u) v[u] = ld_stream2(vb + (int64_t)(d + u) * dstride);
 #pragma unroll
         for (int u = 0; u < UNROLL; ++u) {
             if (LDSX) {
@@ -70,7 +80,7 @@ __global__ __launch_bounds__(256) void dia_kernel(int64_t m, int64_t mp, int64_t
         }
     }
     for (; d < n_diags; ++d) {
-        const f64x2 v = ld_stream2(vb + (int64_t)d * kDiaBlockRows);
+        const f64x2 v = ld_stream2(vb + (int64_t)d * dstride);
         double a, b;
         if (LDSX) {
             const int li = lbase + off[d];
@@ -120,17 +130,19 @@ int launch_dia(const spmv_plan_s *p, const double *x, double *y) {
     // keep the HBM channels out of the oversubscribed mode some placements
     // fall into (config 4, 18 plans: 1.517 against 1.584-1.617 ms mean,
     // profiles/round3/probe/dia_occupancy_c4.jsonl)
-    const int kb = d.lds_kb >= 0 ? d.lds_kb : kDiaLdsKb;
+    int kb = d.lds_kb >= 0 ? d.lds_kb : kDiaLdsKb;
+    if (const char *e = probe_env("SPMV_LAUNCH_DIA_LDS_KB")) kb = std::atoi(e);
+    const int dbg = launch_dbg(d.dbg);
     const size_t lds = std::max(sizeof(double) * (size_t)win, (size_t)kb * 1024);
-    if (win <= kDiaMaxWin && (p->dia.dbg & 2))  // probe A/B: ordinary y stores
+    if (win <= kDiaMaxWin && (dbg & 2))  // probe A/B: ordinary y stores
         hipLaunchKernelGGL((dia_kernel<8, true, 1>), dim3((unsigned)blocks), dim3(256), lds,
-                           p->stream, p->m, d.mp, p->n, d.n_diags, d.off, off_min, (int32_t)win, d.val, x, y);
-    else if (win <= kDiaMaxWin && !(p->dia.dbg & 1))
+                           p->stream, p->m, d.mp, p->n, d.n_diags, d.off, off_min, (int32_t)win, d.val, x, y, d.group);
+    else if (win <= kDiaMaxWin && !(dbg & 1))
         hipLaunchKernelGGL((dia_kernel<8, true>), dim3((unsigned)blocks), dim3(256), lds,
-                           p->stream, p->m, d.mp, p->n, d.n_diags, d.off, off_min, (int32_t)win, d.val, x, y);
+                           p->stream, p->m, d.mp, p->n, d.n_diags, d.off, off_min, (int32_t)win, d.val, x, y, d.group);
     else
         hipLaunchKernelGGL((dia_kernel<8, false>), dim3((unsigned)blocks), dim3(256), 0, p->stream, p->m, d.mp,
-                           p->n, d.n_diags, d.off, off_min, 0, d.val, x, y);
+                           p->n, d.n_diags, d.off, off_min, 0, d.val, x, y, d.group);
     SPMV_HIP_TRY(hipGetLastError());
     return SPMV_SUCCESS;
 }

@@ -11,6 +11,7 @@ in interleaved rounds (cdna_hip_programming.md rule 24).  One JSON line per
       --variants 'base:;ld16:SPMV_BIN_DEBUG=1024' --rows 10000000
 """
 import argparse
+import itertools
 import json
 import os
 import sys
@@ -32,6 +33,10 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--placement", default="plain", help="default placement (a variant's placement=K overrides)")
     ap.add_argument("--check", action="store_true", help="bit-equality of each variant's y vs the first")
+    ap.add_argument("--launch-variants", default="",
+                    help="name:VAR=v,...;... environment set around each timing (probe build: "
+                         "SPMV_LAUNCH_DEBUG, SPMV_LAUNCH_DIA_LDS_KB are read at every launch): "
+                         "every plan is timed under every launch variant, so they share placements")
     a = ap.parse_args()
     import torch
     import singlespmv_amd as sp
@@ -70,18 +75,25 @@ def main():
             if yref is None:
                 yref = y.clone()
             print(json.dumps({"variant": name, "bit_equal_to_first": bool(torch.equal(y, yref))}), flush=True)
+    lvars = []
+    for part in filter(None, a.launch_variants.split(";")):
+        lname, _, envs = part.partition(":")
+        lvars.append((lname, dict(kv.split("=") for kv in filter(None, envs.split(",")))))
     for r in range(a.rounds):
-        for name, p, info in plans:
+        for (name, p, info), (lname, lenv) in itertools.product(plans, lvars or [("", {})]):
+            for k, v in lenv.items():
+                os.environ[k] = v
             ph = p.profile(x, y, a.iters)
             tot = p.time(x, y, a.iters) / a.iters
-            print(json.dumps({"round": r, "variant": name, "ms": round(tot, 4),
+            for k in lenv:
+                os.environ.pop(k, None)
+            print(json.dumps({"round": r, "variant": name, "launch": lname, "ms": round(tot, 4),
                               "long_rows": info.get("bin_long_rows"), "pieces": info.get("bin_long_pieces"),
                               "products": info.get("bin_products"), "stored": info.get("stored_slots"),
                               **{k: round(v, 4) for k, v in ph.items()},
                               "placement_ms": [round(info.get("placement_best_ms", 0), 4),
                                                round(info.get("placement_worst_ms", 0), 4)],
                               "m": m, "n": n}), flush=True)
-
 
 if __name__ == "__main__":
     main()
