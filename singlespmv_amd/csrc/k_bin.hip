@@ -466,16 +466,16 @@ __global__ __launch_bounds__(64 * W2) void bin_sum_kernel(
     }
 }
 
-template <int MODE, int PL>
+template <int MODE, int PL, int U = 8>
 static void launch_mul_t(const spmv_plan_s *p, int g, const double *x) {
     const BinDev &B = p->bin;
     if (B.long_len > 0)
-        hipLaunchKernelGGL((bin_mul_kernel<8, MODE, PL, true>), dim3((unsigned)B.nwg1), dim3(kBinMulThreads), 0,
+        hipLaunchKernelGGL((bin_mul_kernel<U, MODE, PL, true>), dim3((unsigned)B.nwg1), dim3(kBinMulThreads), 0,
                            p->stream, B.piece_off, (int64_t)g * B.nwg1, B.piece_strip, B.piece_begin, B.piece_end,
                            B.val1, B.cs1, B.dst1, x, p->n, (int32_t)B.strip, B.prod, B.lstart, B.lshift, B.lcode,
                            B.xburst);
     else
-        hipLaunchKernelGGL((bin_mul_kernel<8, MODE, PL, false>), dim3((unsigned)B.nwg1), dim3(kBinMulThreads), 0,
+        hipLaunchKernelGGL((bin_mul_kernel<U, MODE, PL, false>), dim3((unsigned)B.nwg1), dim3(kBinMulThreads), 0,
                            p->stream, B.piece_off, (int64_t)g * B.nwg1, B.piece_strip, B.piece_begin, B.piece_end,
                            B.val1, B.cs1, B.dst1, x, p->n, (int32_t)B.strip, B.prod, nullptr, nullptr, nullptr,
                            B.xburst);
@@ -502,6 +502,7 @@ static void launch_mul_p(const spmv_plan_s *p, int g, const double *x) {
             // 16384: loads clamped at the piece's end (A/B); 131072 / 262144:
             // x strips staged serially / in bursts (A/B, build_bin.cpp xburst)
             if (dbg & (1 << 21)) launch_mul_t<513, PL>(p, g, x);  // ablation: no x staging
+            else if (dbg & (1 << 23)) launch_mul_t<1, PL, 4>(p, g, x);  // A/B: 4-entry batches (half in flight)
             else if (dbg & 16384) launch_mul_t<65, PL>(p, g, x);
             else if (dbg & 2048) launch_mul_t<17, PL>(p, g, x);
             else if (dbg & 4096) launch_mul_t<33, PL>(p, g, x);

@@ -111,8 +111,8 @@ __global__ __launch_bounds__(256) void dia_kernel(int64_t m, int64_t mp, int64_t
 
 // LDS x window of a 512-row workgroup: 512 rows + diagonal span + 1
 constexpr int kDiaMaxWin = 8192;  // doubles (64 KB)
-// LDS requested per workgroup (KB), at least the window: caps occupancy
-constexpr int kDiaLdsKb = 64;
+// LDS requested per workgroup (KB), at least the window: > 80 KB = one per CU
+constexpr int kDiaLdsKb = 96;
 
 int launch_dia(const spmv_plan_s *p, const double *x, double *y) {
     const DiaDev &d = p->dia;
@@ -125,15 +125,29 @@ int launch_dia(const spmv_plan_s *p, const double *x, double *y) {
     const int64_t blocks = (pairs + 255) / 256;
     const int32_t off_min = d.off_host.front(), off_max = d.off_host.back();
     const int64_t win = 512 + (int64_t)off_max - off_min + 1;
-    // The LDS request caps the workgroups per CU (kDiaLdsKb: 2 of them, 8
-    // waves; the x window alone would allow 8): fewer value streams in flight
-    // keep the HBM channels out of the oversubscribed mode some placements
-    // fall into (config 4, 18 plans: 1.517 against 1.584-1.617 ms mean,
-    // profiles/round3/probe/dia_occupancy_c4.jsonl)
+    // The LDS request caps the workgroups per CU (kDiaLdsKb: one, 4 waves,
+    // 32 KB of values in flight; the x window alone would allow 8): fewer
+    // value streams keep the HBM channels out of the oversubscribed mode some
+    // placements fall into.  Config 4, launch variants on the same plans:
+    // 1.476-1.527 ms at 1 per CU, 1.500-1.594 at 2, 1.537-1.641 at 8
+    // (profiles/round3/probe/dia_occupancy_paired_c4.jsonl,
+    // dia_unroll_occupancy_c4.jsonl)
     int kb = d.lds_kb >= 0 ? d.lds_kb : kDiaLdsKb;
     if (const char *e = probe_env("SPMV_LAUNCH_DIA_LDS_KB")) kb = std::atoi(e);
     const int dbg = launch_dbg(d.dbg);
     const size_t lds = std::max(sizeof(double) * (size_t)win, (size_t)kb * 1024);
+#ifdef SPMV_PROBES
+    if (win <= kDiaMaxWin && (dbg & 12)) {  // probe A/B: 4 (dbg 4) / 16 (dbg 8) diagonals in flight per lane
+        if (dbg & 4)
+            hipLaunchKernelGGL((dia_kernel<4, true>), dim3((unsigned)blocks), dim3(256), lds, p->stream, p->m, d.mp,
+                               p->n, d.n_diags, d.off, off_min, (int32_t)win, d.val, x, y, d.group);
+        else
+            hipLaunchKernelGGL((dia_kernel<16, true>), dim3((unsigned)blocks), dim3(256), lds, p->stream, p->m, d.mp,
+                               p->n, d.n_diags, d.off, off_min, (int32_t)win, d.val, x, y, d.group);
+        SPMV_HIP_TRY(hipGetLastError());
+        return SPMV_SUCCESS;
+    }
+#endif
     if (win <= kDiaMaxWin && (dbg & 2))  // probe A/B: ordinary y stores
         hipLaunchKernelGGL((dia_kernel<8, true, 1>), dim3((unsigned)blocks), dim3(256), lds,
                            p->stream, p->m, d.mp, p->n, d.n_diags, d.off, off_min, (int32_t)win, d.val, x, y, d.group);
