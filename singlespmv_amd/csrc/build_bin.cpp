@@ -231,6 +231,8 @@ static int bin_rows(spmv_plan_s *p, const int64_t *row_ptr, int64_t m, int64_t n
     L.S = std::max<int64_t>(1, (n + B.strip - 1) / B.strip);
     L.PAD = (int64_t)1 << B.pad_log;
     B.n_strips = L.S;
+    // (Register staging only: the Mul stages x by LDS-DMA wherever x is
+    // 16-byte aligned, k_bin.hip launch_mul_p.)
     // x strips staged with several loads in flight per thread when each Mul
     // workgroup walks many strips (the N = 4, 8 rank shapes: 7.6 / 15 per
     // workgroup): N = 8 shape Mul 0.738 -> 0.719 ms; with ~2 strips per

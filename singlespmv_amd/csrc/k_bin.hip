@@ -200,6 +200,17 @@ __global__ __launch_bounds__(kBinMulThreads) void bin_mul_kernel(
         if constexpr ((MODE & 512) != 0) {
             // ablation (probe, wrong results): no x strip loads -- the cost of
             // staging x, in the Mul's time
+        } else if constexpr ((MODE & 256) != 0) {
+            // LDS-DMA (global_load_lds_dwordx4): each wave instruction copies
+            // 1 KB of x straight into the strip, no VGPRs, all in flight at
+            // once (the barrier below waits for them); the launch checks that
+            // x + c0 is 16-byte aligned.  The tail past whole KB: plain loads.
+            const int full = cw & ~127;
+            for (int k = w; k * 128 < full; k += NW)
+                __builtin_amdgcn_global_load_lds(
+                    (const __attribute__((address_space(1))) void *)(x + c0 + k * 128 + lane * 2),
+                    (__attribute__((address_space(3))) void *)(xs + k * 128), 16, 0, 0);
+            for (int i = full + threadIdx.x; i < cw; i += kBinMulThreads) xs[i] = x[c0 + i];
         } else if (LONG || !xburst) {
             for (int i = threadIdx.x; i < cw; i += kBinMulThreads) xs[i] = x[c0 + i];
         } else for (int i0 = threadIdx.x; i0 < cw; i0 += XL * kBinMulThreads) {
@@ -484,10 +495,16 @@ static void launch_mul_t(const spmv_plan_s *p, int g, const double *x) {
 template <int PL>
 static void launch_mul_p(const spmv_plan_s *p, int g, const double *x) {
     // default: nontemporal stores (measured 0.81 -> 0.71 ms at config 2,
-    // profiles/round1/probe/bin_probe_c2.jsonl).  The ablation MODEs exist
-    // only in the probe build (SPMV_BIN_DEBUG bits 0-1, -DSPMV_PROBES).
+    // profiles/round1/probe/bin_probe_c2.jsonl), x strips staged by LDS-DMA
+    // wherever x + c0 is 16-byte aligned (MODE 256: config 2 Mul 0.536 ->
+    // 0.520 ms, N = 8 rank shape 0.738 -> 0.717, config 3 -1 %, same plans,
+    // profiles/round3/probe/mul_glds_*.jsonl), else through registers.  The
+    // ablation MODEs exist only in the probe build (SPMV_BIN_DEBUG bits 0-1,
+    // -DSPMV_PROBES).
+    const bool dma = (reinterpret_cast<uintptr_t>(x) & 15) == 0 && p->bin.strip % 2 == 0;
 #ifndef SPMV_PROBES
-    launch_mul_t<1, PL>(p, g, x);
+    if (dma) launch_mul_t<257, PL>(p, g, x);
+    else launch_mul_t<1, PL>(p, g, x);
 #else
     const int dbg = launch_dbg(p->bin.dbg);
     switch (dbg & 3) {
@@ -500,12 +517,14 @@ static void launch_mul_p(const spmv_plan_s *p, int g, const double *x) {
         default:
             // long-block partial stores: 2048 nontemporal, 4096 none (ablations);
             // 16384: loads clamped at the piece's end (A/B); 131072 / 262144:
-            // x strips staged serially / in bursts (A/B, build_bin.cpp xburst)
+            // x strips staged serially / in bursts (A/B, build_bin.cpp xburst);
+            // 1 << 24: x strips through registers instead of LDS-DMA (A/B)
             if (dbg & (1 << 21)) launch_mul_t<513, PL>(p, g, x);  // ablation: no x staging
             else if (dbg & (1 << 23)) launch_mul_t<1, PL, 4>(p, g, x);  // A/B: 4-entry batches (half in flight)
             else if (dbg & 16384) launch_mul_t<65, PL>(p, g, x);
             else if (dbg & 2048) launch_mul_t<17, PL>(p, g, x);
             else if (dbg & 4096) launch_mul_t<33, PL>(p, g, x);
+            else if (dma && !(dbg & (1 << 24))) launch_mul_t<257, PL>(p, g, x);
             else launch_mul_t<1, PL>(p, g, x);
     }
 #endif

@@ -321,6 +321,30 @@ def test_device_pointers_and_streams():
         assert ms > 0
 
 
+@pytest.mark.parametrize("long_len", [-1, 64])
+def test_bin_x_staging_paths_agree(long_len):
+    """The Mul stages x strips by LDS-DMA when x is 16-byte aligned and
+    through registers when it is not (a device x at an 8-byte offset): both
+    paths give the same y bit for bit, with and without long rows."""
+    import torch
+    m, n = 50_000, 90_001
+    rp, col, val = _bin_matrix("powerlaw", m, n, seed=5)
+    x = sp.generate_vector(n, seed=8)
+    plan = sp.Plan.from_csr(m, n, rp, col, val, "bin", bin_long_len=long_len)
+    buf = torch.zeros(n + 2, dtype=torch.float64, device="cuda")
+    assert buf.data_ptr() % 16 == 0
+    out = []
+    for off in (0, 1):
+        xd = buf[off:off + n]
+        xd.copy_(torch.from_numpy(x))
+        yd = torch.full((m,), float("nan"), dtype=torch.float64, device="cuda")
+        plan.execute(xd, yd)
+        torch.cuda.synchronize()
+        out.append(yd.cpu().numpy())
+    assert np.array_equal(out[0], out[1])
+    assert_bin_rows(plan, out[0], rp, col, val, x, what=f"x staging long_len {long_len}")
+
+
 @pytest.mark.parametrize("fmt,gpus", [("", ""), ("bin", ""), ("css", ""), ("bin", "1"), ("", "1")])
 def test_dropin_optimizeproblem_spmv(fmt, gpus, monkeypatch):
     """The reference-signature drop-in (include/opt_hip.h) via libopt_hip.so

@@ -67,18 +67,23 @@ def main():
                 os.environ[k] = v
         info = p.info()
         plans.append((name, p, info))
-    yref = None
-    if a.check:
-        for name, p, _ in plans:
-            p.execute(x, y)
-            torch.cuda.synchronize()
-            if yref is None:
-                yref = y.clone()
-            print(json.dumps({"variant": name, "bit_equal_to_first": bool(torch.equal(y, yref))}), flush=True)
     lvars = []
     for part in filter(None, a.launch_variants.split(";")):
         lname, _, envs = part.partition(":")
         lvars.append((lname, dict(kv.split("=") for kv in filter(None, envs.split(",")))))
+    yref = None
+    if a.check:  # every plan under every launch variant against the first
+        for (name, p, _), (lname, lenv) in itertools.product(plans, lvars or [("", {})]):
+            os.environ.update(lenv)
+            y.fill_(float("nan"))
+            p.execute(x, y)
+            torch.cuda.synchronize()
+            for k in lenv:
+                os.environ.pop(k, None)
+            if yref is None:
+                yref = y.clone()
+            print(json.dumps({"variant": name, "launch": lname,
+                              "bit_equal_to_first": bool(torch.equal(y, yref))}), flush=True)
     for r in range(a.rounds):
         for (name, p, info), (lname, lenv) in itertools.product(plans, lvars or [("", {})]):
             for k, v in lenv.items():
