@@ -90,7 +90,11 @@ bin/region_probe: tools/region_probe.hip Makefile
 	mkdir -p bin
 	$(HIPCC) $(HIPFLAGS) -o $@ $<
 
-probes: $(PROBEDIR)/libspmv_hip.so bin/region_probe
+bin/mulorder_probe: tools/mulorder_probe.hip Makefile
+	mkdir -p bin
+	$(HIPCC) $(HIPFLAGS) -o $@ $<
+
+probes: $(PROBEDIR)/libspmv_hip.so bin/region_probe bin/mulorder_probe
 
 # host-code sanitizer build (CPU only): build/asan/libspmv_hip.so
 # with AddressSanitizer + UBSan on every host object (the device code of the

@@ -72,9 +72,18 @@ def streamed_bytes(info) -> dict:
     E = info["stored_slots"]  # Mul entries (segments, voids, long blocks)
     EL = info.get("bin_long_entries", 0)  # long blocks: 4 B lcode instead of a destination per group
     P = info.get("bin_products") or E  # products + run partials (+ the trash line)
-    mul_read = E * (8 + 2) + (E - EL) // max(1, info["bin_pad"]) * 4 + 4 * EL + 8 * info["n"]
-    mul_write = 8 * P
-    sum_read = P * (8 + 2)
+    if info.get("bin_product_order") == 2:
+        # Mul-ordered products: the Mul streams its unpadded entries and writes
+        # them in place; the Sum walks the padded Sum order (8 B product + 2 B
+        # slot per position, a 4-B chunk base per 8 positions)
+        V = info.get("bin_sum_entries") or E
+        mul_read = E * (8 + 2) + 8 * info["n"]
+        mul_write = 8 * P
+        sum_read = V * (8 + 2) + V // 2
+    else:
+        mul_read = E * (8 + 2) + (E - EL) // max(1, info["bin_pad"]) * 4 + 4 * EL + 8 * info["n"]
+        mul_write = 8 * P
+        sum_read = P * (8 + 2)
     sum_write = 8 * info["m"]
     return {"mul": mul_read + mul_write, "sum": sum_read + sum_write,
             "total": mul_read + mul_write + sum_read + sum_write,
@@ -290,7 +299,8 @@ def build_matrix(ctx, args, config: str, rows_override: int = 0):
 RELEVANT = {"csr": ("csr_lanes",), "ss": ("ss_sigma",), "ell": ("ell_width",),
             "hyb": ("ell_width",), "dia": ("n_diags",), "css": ("css_passes", "css_slabs"),
             "bin": ("bin_bins", "bin_strips", "bin_strip_cols", "bin_pad", "bin_sum_waves",
-                    "bin_long_len", "bin_long_rows", "bin_long_pieces", "bin_products")}
+                    "bin_long_len", "bin_long_rows", "bin_long_pieces", "bin_products",
+                    "bin_product_order", "bin_sum_entries")}
 
 
 def time_formats(ctx, args, M, fmts, trials_head: int):

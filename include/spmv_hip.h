@@ -53,11 +53,13 @@ extern "C" {
 
 /* Version 2 changed the layout of spmv_options_t (the bin_* / placement
  * fields, round 2) and spmv_plan_info_t: a caller built against a version-1
- * header passes structs of the wrong size and must be rebuilt.  Callers may
+ * header passes structs of the wrong size and must be rebuilt.  Version 3
+ * (round 3) took bin_product_order from spmv_options_t's reserved words (same
+ * size) and appended bin_sum_entries to spmv_plan_info_t.  Callers may
  * check spmv_api_version() == SPMV_HIP_API_VERSION once at startup; the
  * structs are only ever filled by spmv_options_default / spmv_plan_info of a
  * library with the same version. */
-#define SPMV_HIP_API_VERSION 2
+#define SPMV_HIP_API_VERSION 3
 int spmv_api_version(void);
 
 /* ---- status codes -------------------------------------------------------- */
@@ -113,7 +115,9 @@ typedef struct spmv_options {
                                 the sequential sum); 0 = auto (max(128, strips)
                                 when such rows hold >= 5 % of nnz), -1 = never
                                 (every row bit-exact)                         */
-    int32_t reserved[3];
+    int32_t bin_product_order; /* BIN: where the Mul writes its products
+                                (SPMV_BIN_ORDER_*; 0 = auto)                   */
+    int32_t reserved[2];
 } spmv_options_t;
 
 /* Placement of the large scratch/value buffer of BIN and DIA plans (the BIN
@@ -130,6 +134,19 @@ typedef struct spmv_options {
 #define SPMV_PLACEMENT_VMM 3    /* hipMemCreate handles of 2 MB mapped back to back
                                    into one VA range aligned to 1 GB (no transient
                                    device memory)                                 */
+
+/* Product order of a BIN plan (spmv_options_t.bin_product_order).  Either
+ * way each row is summed in column order (bit-identical y). */
+#define SPMV_BIN_ORDER_AUTO 0  /* MUL where the layout allows it (no long rows,
+                                  one row group, < 2^31 entries), else SUM     */
+#define SPMV_BIN_ORDER_SUM 1   /* the Mul scatters each product into its (bin,
+                                  strip) segment of the Sum's order; the Sum
+                                  streams each bin as one contiguous run       */
+#define SPMV_BIN_ORDER_MUL 2   /* the Mul writes its products contiguously in
+                                  its own order (no segment padding, no
+                                  destination array); the Sum gathers each
+                                  bin's segments in 8-entry chunks through a
+                                  chunk table                                  */
 
 /* Fill `opt` with defaults (AUTO format, current device, auto tuning). */
 void spmv_options_default(spmv_options_t *opt);
@@ -296,11 +313,12 @@ typedef struct spmv_plan_info {
     float placement_best_ms;  /* SEARCH: fastest / slowest candidate launch    */
     float placement_worst_ms;
     int32_t bin_long_len;     /* BIN: long-row threshold in use (0 = none)      */
-    int32_t bin_reserved;
+    int32_t bin_product_order; /* BIN: SPMV_BIN_ORDER_SUM or _MUL (resolved)   */
     int64_t bin_long_rows;    /* BIN: rows on the run path, their run pieces    */
     int64_t bin_long_pieces;
     int64_t bin_products;     /* BIN: products + partials the Sum reads         */
     int64_t bin_long_entries; /* BIN: Mul entries in long blocks (with padding) */
+    int64_t bin_sum_entries;  /* BIN: Sum-order positions (segments padded)     */
 } spmv_plan_info_t;
 
 int spmv_plan_info(spmv_plan_t plan, spmv_plan_info_t *info);

@@ -41,7 +41,7 @@ FORMATS = {"auto": 0, "csr": 1, "crs": 1, "ell": 2, "ss": 3, "dia": 4, "hyb": 5,
 FORMAT_NAMES = {0: "auto", 1: "csr", 2: "ell", 3: "ss", 4: "dia", 5: "hyb", 6: "css", 7: "coo", 8: "jds", 9: "bin"}
 X_DEVICE, Y_DEVICE, ASYNC, X_STAGED = 0x1, 0x2, 0x4, 0x8
 GEN_UNIFORM, GEN_POWERLAW, GEN_BANDED = 1, 2, 3
-API_VERSION = 2  # SPMV_HIP_API_VERSION of the structs mirrored here
+API_VERSION = 3  # SPMV_HIP_API_VERSION of the structs mirrored here
 
 _I32P = np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")
 _I64P = np.ctypeslib.ndpointer(np.int64, flags="C_CONTIGUOUS")
@@ -58,7 +58,8 @@ class Options(C.Structure):
                 ("dia_max_fill", C.c_double), ("css_slab_shift", C.c_int32), ("css_lag", C.c_int32),
                 ("css_pace", C.c_int32), ("bin_strip_cols", C.c_int32), ("bin_groups", C.c_int32),
                 ("bin_sum_waves", C.c_int32), ("bin_pad", C.c_int32), ("csr_row_ptr64", C.c_int32),
-                ("placement", C.c_int32), ("bin_long_len", C.c_int32), ("reserved", C.c_int32 * 3)]
+                ("placement", C.c_int32), ("bin_long_len", C.c_int32), ("bin_product_order", C.c_int32),
+                ("reserved", C.c_int32 * 2)]
 
 
 PLACEMENTS = {"auto": 0, "plain": 1, "search": 2, "vmm": 3}
@@ -75,9 +76,9 @@ class PlanInfo(C.Structure):
                 ("bin_pad", C.c_int32), ("bin_sum_waves", C.c_int32), ("bin_groups", C.c_int32),
                 ("placement", C.c_int32), ("placement_candidates", C.c_int32),
                 ("placement_best_ms", C.c_float), ("placement_worst_ms", C.c_float),
-                ("bin_long_len", C.c_int32), ("bin_reserved", C.c_int32), ("bin_long_rows", C.c_int64),
+                ("bin_long_len", C.c_int32), ("bin_product_order", C.c_int32), ("bin_long_rows", C.c_int64),
                 ("bin_long_pieces", C.c_int64), ("bin_products", C.c_int64),
-                ("bin_long_entries", C.c_int64)]
+                ("bin_long_entries", C.c_int64), ("bin_sum_entries", C.c_int64)]
 
     def as_dict(self):
         d = {k: getattr(self, k) for k, _ in self._fields_}
@@ -359,7 +360,7 @@ def make_options(fmt="auto", device: int = -1, csr_lanes: int = 0, ell_width: in
                  css_slab_shift: int = 0, css_lag: int = 0, css_pace: int = 0,
                  bin_strip_cols: int = 0, bin_groups: int = 0, bin_sum_waves: int = 0,
                  bin_pad: int = 0, csr_row_ptr64: bool = False, placement="auto",
-                 bin_long_len: int = 0) -> Options:
+                 bin_long_len: int = 0, bin_product_order: int = 0) -> Options:
     o = Options()
     lib().spmv_options_default(C.byref(o))
     o.format = FORMATS[fmt] if isinstance(fmt, str) else int(fmt)
@@ -370,6 +371,7 @@ def make_options(fmt="auto", device: int = -1, csr_lanes: int = 0, ell_width: in
     o.bin_sum_waves, o.bin_pad, o.csr_row_ptr64 = bin_sum_waves, bin_pad, 1 if csr_row_ptr64 else 0
     o.placement = PLACEMENTS[placement] if isinstance(placement, str) else int(placement)
     o.bin_long_len = bin_long_len
+    o.bin_product_order = bin_product_order
     return o
 
 

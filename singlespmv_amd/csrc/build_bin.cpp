@@ -127,6 +127,12 @@ static int bin_params(spmv_plan_s *p, const spmv_options_t &o, int64_t m, int64_
         const int w = std::atoi(e);
         B.sum_waves = w == 2 || w == 4 ? w : 8;
     }
+    // product order: Mul order unless the caller asks for the Sum's (resolved
+    // against the layout in bin_mo_resolve)
+    SPMV_CHECK_ARG(o.bin_product_order >= SPMV_BIN_ORDER_AUTO && o.bin_product_order <= SPMV_BIN_ORDER_MUL,
+                   "bin_product_order must be 0, 1 or 2");
+    B.order_req = o.bin_product_order;
+    if (const char *e = probe_env("SPMV_BIN_ORDER")) B.order_req = std::atoi(e);
     B.max_rows = bin_max_rows(B.sum_waves);
     B.sum_u = B.sum_waves == 8 ? 8 : 32;  // must match launch_sum's <W2, U> pairs
     B.slot_linear = false;
@@ -221,6 +227,18 @@ static void bin_long_count(BinLayout &L) {
         }
         L.lpad[(size_t)t] = (nt + 63) & ~(int64_t)63;
     }
+}
+
+// ---- product order.  Mul order (BinDev::mo) needs the plain layout: no run
+// path (its partials have Sum positions), one row group, one strip block,
+// grouped slots with 32-entry Sum batches, and Mul positions that fit the
+// int32 chunk table.  Its Sum reads 8-entry chunks, so the segments' padding
+// in the Sum order is 8 entries unless the caller set bin_pad.
+static void bin_mo_resolve(BinDev &B, const spmv_options_t &o, int64_t LL, int64_t nnz) {
+    // AUTO: Sum order until the Mul order is measured on the GPU
+    B.mo = B.order_req == SPMV_BIN_ORDER_MUL && LL == 0 && o.bin_groups <= 1 && !B.reuse && !B.slot_linear &&
+           B.sum_u == 32 && nnz + kBinProdSlack < ((int64_t)1 << 31);
+    if (B.mo && !o.bin_pad && !probe_env("SPMV_BIN_PADLOG")) B.pad_log = 3;
 }
 
 // ---- row bins: <= max_rows rows, cut at cumulative nnz targets; a multiple
@@ -325,7 +343,7 @@ static void bin_offsets(spmv_plan_s *p, const spmv_options_t &o, BinLayout &L) {
     // block, the plain bin-major layout.
     int64_t SB = S;
     if (const char *e = probe_env("SPMV_BIN_SB")) SB = std::max<int64_t>(1, std::atoll(e));
-    if (B.reuse || SB > S) SB = S;
+    if (B.reuse || B.mo || SB > S) SB = S;
     const int64_t NBK = (S + SB - 1) / SB;
     // long rows: one more run per bin (its run pieces, [strip][row][piece])
     const int64_t NR = NBK + (L.LL > 0 ? 1 : 0);
@@ -398,7 +416,8 @@ static void bin_offsets(spmv_plan_s *p, const spmv_options_t &o, BinLayout &L) {
             for (int64_t j = 0; j < nbg; ++j) {
                 const int64_t b = L.mul_bins[(size_t)(g0 + j)];
                 L.off1[(size_t)(b * S + t)] = cur;
-                cur += L.rpad(L.cnt[(size_t)(b * S + t)]);
+                // Mul-ordered products: the Mul's segments are not padded
+                cur += B.mo ? L.cnt[(size_t)(b * S + t)] : L.rpad(L.cnt[(size_t)(b * S + t)]);
             }
             if (L.LL > 0) {  // G == 1: void up to a 64-entry boundary, then the long blocks
                 cur = (cur + 63) & ~(int64_t)63;
@@ -426,9 +445,29 @@ static void bin_offsets(spmv_plan_s *p, const spmv_options_t &o, BinLayout &L) {
 struct BinHostArrays {
     std::vector<double> val1;
     std::vector<uint16_t> cs1, slot2;
-    std::vector<int32_t> dst1, lcode;
+    std::vector<int32_t> dst1, lcode, mtab;
     std::vector<int64_t> lshift;
 };
+
+// Mul order: the chunk table (internal.hpp bin_mo_tab_at) from the layout
+// alone -- every segment's 8-entry chunks, Sum position -> Mul position;
+// chunks past a run's end keep base 0 (their slots are the dummy slot)
+static void bin_mo_table(const BinDev &B, const BinLayout &L, std::vector<int32_t> &tab) {
+    const int64_t S = L.S, NB = L.NB, U = B.sum_u, step = 64 * U;
+    tab.assign((size_t)(L.ES / 8), 0);
+#pragma omp parallel for schedule(static)
+    for (int64_t b = 0; b < NB; ++b) {
+        const int64_t r0 = L.run_off[(size_t)b], s0 = L.srun_off[(size_t)b];
+        for (int64_t t = 0; t < S; ++t) {
+            const int64_t o1 = L.off1[(size_t)(b * S + t)], o2 = L.off2[(size_t)(b * S + t)];
+            const int64_t c = L.cnt[(size_t)(b * S + t)];
+            for (int64_t k = 0; k < c; k += 8) {
+                const int64_t rel = o2 + k - r0, i = rel / step, w = rel - i * step;
+                tab[(size_t)((s0 + i * step) / 8 + bin_mo_tab_at(w >> 3, (int)U))] = (int32_t)(o1 + k);
+            }
+        }
+    }
+}
 
 static void bin_fill_arrays(const BinDev &B, const HostCsr &A, const BinLayout &L, BinHostArrays &H) {
     const int64_t S = L.S, NB = L.NB, E1 = L.E1, C = B.strip, PAD = L.PAD;
@@ -441,7 +480,8 @@ static void bin_fill_arrays(const BinDev &B, const HostCsr &A, const BinLayout &
     val1.assign((size_t)(E1 + kBinMulSlack), 0.0);
     cs1.assign((size_t)(E1 + kBinMulSlack), 0);
     slot2.assign((size_t)L.ES, (uint16_t)max_rows);
-    dst1.assign((size_t)((E1 + kBinMulSlack) >> B.pad_log), (int32_t)(L.TRASH >> B.pad_log));
+    if (B.mo) dst1.clear();  // Mul order: no destinations, no Mul-side padding
+    else dst1.assign((size_t)((E1 + kBinMulSlack) >> B.pad_log), (int32_t)(L.TRASH >> B.pad_log));
     std::vector<int> gof((size_t)NB);
     for (int g = 0; g < B.G; ++g)
         for (int64_t b = B.g_bin[(size_t)g]; b < B.g_bin[(size_t)g + 1]; ++b) gof[(size_t)b] = g;
@@ -497,12 +537,15 @@ static void bin_fill_arrays(const BinDev &B, const HostCsr &A, const BinLayout &
             for (int64_t s = 0; s < S; ++s) {
                 const int64_t n0 = L.cnt[(size_t)(b * S + s)], n8 = L.rpad(n0);
                 for (int64_t k = n0; k < n8; ++k) {
-                    val1[(size_t)(o1[s] + k)] = 0.0;
-                    cs1[(size_t)(o1[s] + k)] = 0;
+                    if (!B.mo) {
+                        val1[(size_t)(o1[s] + k)] = 0.0;
+                        cs1[(size_t)(o1[s] + k)] = 0;
+                    }
                     slot2[sidx(s, o2[s] + k)] = (uint16_t)max_rows;
                 }
-                for (int64_t t = 0; t < n8; t += PAD)
-                    dst1[(size_t)((o1[s] + t) >> B.pad_log)] = (int32_t)((o2[s] + t - pb) >> B.pad_log);
+                if (!B.mo)
+                    for (int64_t t = 0; t < n8; t += PAD)
+                        dst1[(size_t)((o1[s] + t) >> B.pad_log)] = (int32_t)((o2[s] + t - pb) >> B.pad_log);
             }
         }
     }
@@ -545,6 +588,7 @@ static void bin_fill_arrays(const BinDev &B, const HostCsr &A, const BinLayout &
         H.lshift.resize((size_t)S);
         for (int64_t t = 0; t < S; ++t) H.lshift[(size_t)t] = L.lcode_off[(size_t)t] - L.lstart[(size_t)t];
     }
+    if (B.mo) bin_mo_table(B, L, H.mtab);
 }
 
 static int bin_fill_host(spmv_plan_s *p, const HostCsr &A, const BinLayout &L) {
@@ -558,7 +602,8 @@ static int bin_fill_host(spmv_plan_s *p, const HostCsr &A, const BinLayout &L) {
     }
     SPMV_RETURN_IF(upload_vec(p, &B.val1, H.val1));
     SPMV_RETURN_IF(upload_vec(p, &B.cs1, H.cs1));
-    SPMV_RETURN_IF(upload_vec(p, &B.dst1, H.dst1));
+    if (B.mo) SPMV_RETURN_IF(upload_vec(p, &B.mtab, H.mtab));
+    else SPMV_RETURN_IF(upload_vec(p, &B.dst1, H.dst1));
     SPMV_RETURN_IF(upload_vec(p, &B.slot2, H.slot2));
     return SPMV_SUCCESS;
 }
@@ -729,7 +774,8 @@ static void bin_pieces(const BinDev &B, const BinLayout &L, BinPieces &P) {
     for (int g = 0; g < B.G; ++g) {
         // Mul-order range of the group (with long rows, G == 1: segments,
         // voids and long blocks)
-        const int64_t g0 = B.g_prod[(size_t)g], g1 = L.LL > 0 ? L.E1 : B.g_prod[(size_t)g + 1];
+        // (Mul-ordered products: G == 1, the unpadded entries [0, E1))
+        const int64_t g0 = B.g_prod[(size_t)g], g1 = L.LL > 0 || B.mo ? L.E1 : B.g_prod[(size_t)g + 1];
         const int64_t *ss = L.strip_start.data() + (size_t)g * (S + 1);
         int64_t s = 0;
         for (int k = 0; k < B.nwg1; ++k) {
@@ -748,7 +794,7 @@ static int bin_finish(spmv_plan_s *p, int64_t n, const BinLayout &L, const spmv_
     bin_pieces(B, L, P);
     std::vector<int64_t> &piece_off = P.off, &pbeg = P.beg, &pend = P.end;
     std::vector<int32_t> &pstrip = P.strip;
-    B.prod_cap = B.reuse ? 0 : (L.LL > 0 ? L.TRASH + L.PAD : E);
+    B.prod_cap = B.reuse ? 0 : (L.LL > 0 ? L.TRASH + L.PAD : B.mo ? L.E1 : E);
     if (B.reuse)
         for (int g = 0; g < B.G; ++g) B.prod_cap = std::max(B.prod_cap, B.g_prod[(size_t)g + 1] - B.g_prod[(size_t)g]);
     const size_t prod_bytes = sizeof(double) * (size_t)(std::max<int64_t>(B.prod_cap, 1) + kBinProdSlack);
@@ -800,6 +846,7 @@ static int bin_layout(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o,
             bin_long_prep(A, B.strip, L);
             for (int64_t r = 0; r < A.m; ++r) B.long_rows += L.is_long(A.row_ptr, r) ? 1 : 0;
         }
+        bin_mo_resolve(B, o, L.LL, A.nnz);
         SPMV_RETURN_IF(bin_rows(p, A.row_ptr, A.m, A.n, L));
         // segment sizes (bin b, strip s); long rows are not in the segments
         const int64_t S = L.S, NB = L.NB, C = B.strip;
@@ -849,6 +896,7 @@ int build_bin_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, 
     if (bin_long_threshold(o, rp.data(), p->m, p->nnz, std::max<int64_t>(1, (p->n + B.strip - 1) / B.strip)) > 0)
         return kBinNeedHostBuild;
     BinLayout L;
+    bin_mo_resolve(B, o, 0, p->nnz);
     SPMV_RETURN_IF(bin_rows(p, rp.data(), p->m, p->n, L));
     std::vector<int64_t> bstart((size_t)L.NB + 1);
     for (int64_t b = 0; b <= L.NB; ++b) bstart[(size_t)b] = rp[(size_t)L.row0[(size_t)b]];
@@ -858,6 +906,11 @@ int build_bin_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, 
     bin_offsets(p, o, L);
     SPMV_RETURN_IF(bin_fill_device(p, d_rp, d_col, d_val, L.row0, bstart, L.cnt, L.off1, L.off2, L.run_off,
                                    L.srun_off, L.S, L.E, L.ES));
+    if (B.mo) {  // the chunk table needs only the layout
+        std::vector<int32_t> tab;
+        bin_mo_table(B, L, tab);
+        SPMV_RETURN_IF(upload_vec(p, &B.mtab, tab));
+    }
     return bin_finish(p, p->n, L, o);
 }
 

@@ -635,10 +635,12 @@ int spmv_plan_info(spmv_plan_t p, spmv_plan_info_t *info) {
         info->bin_sum_waves = p->bin.sum_waves;
         info->bin_groups = p->bin.G;
         info->bin_long_len = (int32_t)p->bin.long_len;
+        info->bin_product_order = p->bin.mo ? SPMV_BIN_ORDER_MUL : SPMV_BIN_ORDER_SUM;
         info->bin_long_rows = p->bin.long_rows;
         info->bin_long_pieces = p->bin.long_pieces;
         info->bin_products = p->bin.prod_cap;
         info->bin_long_entries = p->bin.long_entries;
+        info->bin_sum_entries = p->bin.n_entries;
     }
     const std::vector<float> *pm = nullptr;
     if (p->format == SPMV_FORMAT_BIN) {

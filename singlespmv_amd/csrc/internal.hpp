@@ -288,6 +288,17 @@ __host__ __device__ inline int64_t bin_slot_index(int64_t e, int64_t r0, int64_t
     const int64_t u = w >> 6, lane = w & 63;
     return s0 + i * step + (u >> 3) * 512 + lane * 8 + (u & 7);
 }
+// Mul-ordered products (BinDev::mo, SPMV_BIN_ORDER_MUL): the Mul writes entry
+// e's product to prod[e] (its own order, segments unpadded), and the Sum
+// reads the Sum order's positions through a chunk table.  Entry (u, lane) of
+// a Sum batch lies in chunk c = 8u + lane/8 of the batch: 8 consecutive Sum
+// positions of one segment = 8 consecutive Mul positions (segment padding in
+// the Sum order reads on into the next segment's products, to the dummy
+// slot).  A batch's 8U chunk bases sit at table index sbase/8 (sbase = the
+// batch's slot block) in the order below: word r of lane l is chunk 64r + l,
+// so a lane loads its U/8 words at once and ds_bpermute hands chunk c to the
+// 8 lanes reading it.
+__host__ __device__ inline int64_t bin_mo_tab_at(int64_t c, int U) { return (c & 63) * (U / 8) + (c >> 6); }
 // The Sum reads whole batches of 64*U products without clamping at a run's
 // end (the padded slot batches send those lanes to the dummy slot), so the
 // product buffer carries one batch of slack past its last run.
@@ -313,7 +324,10 @@ struct BinDev {
     int64_t *piece_begin = nullptr, *piece_end = nullptr;
     double *val1 = nullptr;
     uint16_t *cs1 = nullptr;
-    int32_t *dst1 = nullptr;       // per 2^pad_log entries
+    int32_t *dst1 = nullptr;       // per 2^pad_log entries (Sum-ordered products only)
+    int order_req = 0;             // spmv_options_t.bin_product_order (SPMV_BIN_ORDER_*)
+    bool mo = false;               // products in Mul order (SPMV_BIN_ORDER_MUL, bin_mo_tab_at)
+    int32_t *mtab = nullptr;       // mo: [ES / 8] Mul position of every 8-entry Sum chunk
     uint16_t *slot2 = nullptr;
     int64_t n_blocks = 1;         // strip blocks of the product layout
     int64_t *run_off = nullptr;   // [n_blocks*n_bins + 1]: run (blk, b) of bin b's products

@@ -78,9 +78,10 @@ __device__ __forceinline__ void mul_load(MulBatch<U> &B, int64_t base, int64_t e
             // its e may lie beyond the strip's long blocks
             const int64_t e = base + u * 64 + lane;
             if (LONG && base + u * 64 >= ls) B.d[u] = ld_stream(lcode + (e < e1 ? e + lsh : 0));
-            else B.d[u] = ld_stream(db + u * (64 >> PL));
+            else if constexpr ((MODE & 4) == 0) B.d[u] = ld_stream(db + u * (64 >> PL));
         }
         (void)e0;
+        (void)db;
     } else {  // LONG, or MODE 64 (A/B): every load clamped at the piece's end
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -89,7 +90,7 @@ __device__ __forceinline__ void mul_load(MulBatch<U> &B, int64_t base, int64_t e
             B.v[u] = ld_stream(val1 + ee);
             B.c[u] = (MODE & 8) ? (uint32_t)((ee * 2654435761u) & 16383) : (uint32_t)__builtin_nontemporal_load(cs1 + ee);
             if (LONG && base + u * 64 >= ls) B.d[u] = ld_stream(lcode + (e < e1 ? e + lsh : 0));
-            else B.d[u] = ld_stream(dst1 + (ee >> PL));
+            else if constexpr ((MODE & 4) == 0) B.d[u] = ld_stream(dst1 + (ee >> PL));
         }
     }
 }
@@ -154,7 +155,8 @@ __device__ __forceinline__ void mul_store(const MulBatch<U> &B, int64_t base, in
             mul_long_block<MODE>(__dmul_rn(B.v[u], xs[B.c[u]]), B.d[u], e < e1, lane, prod);
         } else if (e < e1) {
             const double pr = __dmul_rn(B.v[u], xs[B.c[u]]);
-            // MODE 4 (ablation): write in Mul order (sequential) instead of Sum order
+            // MODE 4: products in Mul order (BinDev::mo: contiguous, no
+            // destinations) instead of the Sum order's segments
             double *dp = (MODE & 4) ? prod + e : prod + ((int64_t)B.d[u] << PL) + (e & ((1 << PL) - 1));
             if (MODE & 2) {
                 if (pr == 1.2345e300) *dp = pr;
@@ -167,9 +169,10 @@ __device__ __forceinline__ void mul_store(const MulBatch<U> &B, int64_t base, in
     }
 }
 
-// MODE (SPMV_BIN_DEBUG, internal ablations): 1 nontemporal product stores,
-// 2 no product stores (value kept alive), 4 products written in Mul order
-// (sequential; wrong results -- measures the cost of the scattered layout).  PL: segments padded to 2^PL entries.
+// MODE: 1 nontemporal product stores, 4 products in Mul order (BinDev::mo;
+// on a Sum-ordered plan an ablation with wrong results), 256 x strips by
+// LDS-DMA; probe ablations: 2 no product stores (value kept alive), 8 no cs1
+// loads, 512 no x staging.  PL: segments padded to 2^PL entries.
 template <int U, int MODE, int PL, bool LONG>
 __global__ __launch_bounds__(kBinMulThreads) void bin_mul_kernel(
     const int64_t *__restrict__ piece_off, int64_t q_base, const int32_t *__restrict__ piece_strip,
@@ -477,8 +480,145 @@ __global__ __launch_bounds__(64 * W2) void bin_sum_kernel(
     }
 }
 
+// Mul-ordered plans (BinDev::mo) take every variant with MODE 4
+// ---- Mul-ordered products (BinDev::mo, internal.hpp bin_mo_tab_at) -------
+// The Sum's walk is bin_sum_kernel's (one cursor over a wave's bins, the next
+// batch loading while the current one is added, y written per bin), but a
+// batch's products are gathered in 8-entry chunks: lane l loads the batch's
+// table words r = 0..U/8-1 (chunks 64r + l) with one 16-byte load, and load
+// instruction u takes chunk 8u + l/8's base from lane 8(u%8) + l/8 by
+// ds_bpermute.  Each wave instruction still reads 64 products -- 8 runs of
+// 64 B.  The table is loaded one batch ahead of the products it addresses,
+// so waiting for it never drains the batch of products in flight (loads
+// complete in issue order).
+template <int U>
+struct SumTab {
+    int32_t t[U / 8];
+};
+
+template <int U>
+__device__ __forceinline__ void sum_mo_tab(SumTab<U> &T, int64_t sb, int lane, const int32_t *__restrict__ mtab) {
+    static_assert(U == 32, "one 16-byte table load per lane");
+    const bin_u32x4 w = __builtin_nontemporal_load(reinterpret_cast<const bin_u32x4 *>(mtab + (sb >> 3)) + lane);
+#pragma unroll
+    for (int h = 0; h < 4; ++h) T.t[h] = (int32_t)w[h];
+}
+
+template <int U, int MODE>
+__device__ __forceinline__ void sum_mo_load(SumBatch<U, MODE> &B, const SumTab<U> &T, int64_t sb, int lane,
+                                            const uint16_t *__restrict__ slot2, const double *__restrict__ prod) {
+    const bin_u32x4 *sp = reinterpret_cast<const bin_u32x4 *>(slot2 + sb + (int64_t)lane * 8);
+#pragma unroll
+    for (int q = 0; q < U / 8; ++q) {
+        const bin_u32x4 w = __builtin_nontemporal_load(sp + q * 64);
+#pragma unroll
+        for (int h = 0; h < 4; ++h) B.w[4 * q + h] = w[h];
+    }
+    const double *pl = prod + (lane & 7);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int c0 = __builtin_amdgcn_ds_bpermute((((u & 7) << 3) + (lane >> 3)) << 2, T.t[u >> 3]);
+        B.v[u] = ld_stream(pl + c0);
+    }
+}
+
+template <int W2, int U, int MODE>
+__global__ __launch_bounds__(64 * W2) void bin_sum_mo_kernel(
+    int64_t nbins, const int64_t *__restrict__ run_off, const int64_t *__restrict__ srun_off,
+    const int32_t *__restrict__ bin_row0, const uint16_t *__restrict__ slot2, const int32_t *__restrict__ mtab,
+    const double *__restrict__ prod, double *__restrict__ y) {
+    constexpr int SLICE = kBinLdsDoubles / W2;
+    constexpr int64_t STEP = 64 * U;
+    __shared__ double ylds[kBinLdsDoubles];
+    const int w = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    double *ys = ylds + w * SLICE;
+    const int64_t bfirst = (int64_t)blockIdx.x * W2 + w, bstride = (int64_t)gridDim.x * W2;
+    if (bfirst >= nbins) return;
+    // one cursor over the wave's bins: bin cb, batch at pos of its run;
+    // the batch's slot block (and table block) from ss
+    int64_t cb = bfirst, pos = run_off[cb], end = run_off[cb + 1], rs = pos, ss = srun_off[cb];
+    auto next = [&](int64_t &sb, int64_t &bb) -> bool {
+        while (pos >= end) {
+            cb += bstride;
+            if (cb >= nbins) return false;
+            pos = rs = run_off[cb];
+            end = run_off[cb + 1];
+            ss = srun_off[cb];
+        }
+        sb = ss + (pos - rs);
+        bb = cb;
+        pos += STEP;
+        return true;
+    };
+    int64_t acc = -1, done = bfirst;
+    auto write_zero = [&](int64_t bz) {
+        const int64_t r0 = bin_row0[bz];
+        const int rows = (int)(bin_row0[bz + 1] - r0);
+        for (int i = lane; i < rows; i += 64) __builtin_nontemporal_store(0.0, y + r0 + i);
+    };
+    auto finish = [&]() {
+        const int64_t r0 = bin_row0[acc];
+        const int rows = (int)(bin_row0[acc + 1] - r0);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        for (int i = lane; i < rows; i += 64) __builtin_nontemporal_store(ys[i], y + r0 + i);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        done = acc + bstride;
+    };
+    auto begin = [&](int64_t nb) {
+        if (nb == acc) return;
+        if (acc >= 0) finish();
+        for (; done < nb; done += bstride) write_zero(done);
+        const int rows = (int)(bin_row0[nb + 1] - bin_row0[nb]);
+        for (int i = lane; i < rows; i += 64) ys[i] = 0.0;
+        acc = nb;
+        done = nb + bstride;
+    };
+    double sink = 0.0;
+    SumBatch<U, MODE> PA, PB;
+    SumTab<U> TA, TB;
+    int64_t s0 = 0, n0 = 0, s1 = 0, n1 = 0, s2 = 0, n2 = 0, s3 = 0, n3 = 0;
+    bool h0 = next(s0, n0);
+    bool h1 = h0 && next(s1, n1);
+    if (h0) sum_mo_tab<U>(TA, s0, lane, mtab);
+    if (h1) sum_mo_tab<U>(TB, s1, lane, mtab);
+    if (h0) sum_mo_load<U, MODE>(PA, TA, s0, lane, slot2, prod);
+    while (h0) {
+        // batch k in PA is added while k+1's products (table TB) and k+2's
+        // table (into TA, free since PA's loads were issued) are in flight
+        const bool h2 = h1 && next(s2, n2);
+        if (h2) sum_mo_tab<U>(TA, s2, lane, mtab);
+        if (h1) sum_mo_load<U, MODE>(PB, TB, s1, lane, slot2, prod);
+        begin(n0);
+        sum_add<U, MODE, SLICE - 1>(PA, 0, 0, lane, ys, sink);
+        if (!h1) break;
+        const bool h3 = h2 && next(s3, n3);
+        if (h3) sum_mo_tab<U>(TB, s3, lane, mtab);
+        if (h2) sum_mo_load<U, MODE>(PA, TA, s2, lane, slot2, prod);
+        begin(n1);
+        sum_add<U, MODE, SLICE - 1>(PB, 0, 0, lane, ys, sink);
+        h0 = h2;
+        s0 = s2;
+        n0 = n2;
+        h1 = h3;
+        s1 = s3;
+        n1 = n3;
+    }
+    if (acc >= 0) finish();
+    for (; done < nbins; done += bstride) write_zero(done);
+}
+
+template <int W2>
+static void launch_sum_mo(const spmv_plan_s *p, double *y) {
+    const BinDev &B = p->bin;
+    hipLaunchKernelGGL((bin_sum_mo_kernel<W2, 32, 1 | 512>), dim3((unsigned)B.nwg2), dim3(64 * W2), 0, p->stream,
+                       B.n_bins, B.run_off, B.srun_off, B.bin_row0, B.slot2, B.mtab, B.prod, y);
+}
+
 template <int MODE, int PL, int U = 8>
-static void launch_mul_t(const spmv_plan_s *p, int g, const double *x) {
+static void launch_mul_t(const spmv_plan_s *p, int g, const double *x);
+template <int MODE, int PL, int U = 8>
+static void launch_mul_tt(const spmv_plan_s *p, int g, const double *x) {
     const BinDev &B = p->bin;
     if (B.long_len > 0)
         hipLaunchKernelGGL((bin_mul_kernel<U, MODE, PL, true>), dim3((unsigned)B.nwg1), dim3(kBinMulThreads), 0,
@@ -490,6 +630,11 @@ static void launch_mul_t(const spmv_plan_s *p, int g, const double *x) {
                            p->stream, B.piece_off, (int64_t)g * B.nwg1, B.piece_strip, B.piece_begin, B.piece_end,
                            B.val1, B.cs1, B.dst1, x, p->n, (int32_t)B.strip, B.prod, nullptr, nullptr, nullptr,
                            B.xburst);
+}
+template <int MODE, int PL, int U>
+static void launch_mul_t(const spmv_plan_s *p, int g, const double *x) {
+    if (p->bin.mo) launch_mul_tt<MODE | 4, PL, U>(p, g, x);
+    else launch_mul_tt<MODE, PL, U>(p, g, x);
 }
 
 template <int PL>
@@ -623,6 +768,11 @@ int launch_bin(const spmv_plan_s *p, const double *x, double *y) {
         return SPMV_SUCCESS;
     }
     auto sum = [&](int g) {
+        if (B.mo) {  // Mul-ordered products (G == 1, 32-entry batches)
+            if (B.sum_waves == 2) launch_sum_mo<2>(p, y);
+            else launch_sum_mo<4>(p, y);
+            return;
+        }
         if (B.sum_waves == 2) launch_sum_w<2, 32>(p, g, y);
         // 4 waves: 32-entry batches per lane (0.313 -> 0.295 ms against 16,
         // profiles/round1/probe/bin_sum_depth.jsonl; 231 VGPRs, 1 wave/SIMD)

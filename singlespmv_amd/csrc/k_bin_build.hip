@@ -108,8 +108,10 @@ __global__ __launch_bounds__(256) void bin_place_kernel(
         cs1[o1 + pos] = (uint16_t)(c - t * C);
         const int64_t run = (t / SB) * NB + e.b;
         slot2[bin_slot_index(o2 + pos, run_off[run], srun_off[run], sum_u)] = (uint16_t)(e.r - row0[e.b]);
-        // every 2^pad_log group of a segment starts with a real entry
-        if ((pos & ((1 << pad_log) - 1)) == 0) dst1[(o1 + pos) >> pad_log] = (int32_t)((o2 + pos - pbb[e.b]) >> pad_log);
+        // every 2^pad_log group of a segment starts with a real entry (Mul
+        // order, dst1 == nullptr: no destinations)
+        if (dst1 && (pos & ((1 << pad_log) - 1)) == 0)
+            dst1[(o1 + pos) >> pad_log] = (int32_t)((o2 + pos - pbb[e.b]) >> pad_log);
     }
 }
 
@@ -211,17 +213,21 @@ int bin_fill_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, c
             for (int64_t b = B.g_bin[(size_t)g]; b < B.g_bin[(size_t)g + 1]; ++b) pbb[(size_t)b] = B.g_prod[(size_t)g];
     void *q;
     // val1 / cs1 / dst1 with the Mul's unclamped-batch slack (kBinMulSlack), zeroed
+    // (Mul order: the entries fill [0, nnz) unpadded, the rest is slack)
+    const int64_t Ez = B.mo ? p->nnz : E;
     SPMV_RETURN_IF(p->arena.alloc(&q, sizeof(double) * (size_t)(E + kBinMulSlack)));
     B.val1 = (double *)q;
-    SPMV_HIP_TRY(hipMemsetAsync(B.val1 + E, 0, sizeof(double) * (size_t)kBinMulSlack, st));
+    SPMV_HIP_TRY(hipMemsetAsync(B.val1 + Ez, 0, sizeof(double) * (size_t)(E - Ez + kBinMulSlack), st));
     SPMV_RETURN_IF(p->arena.alloc(&q, sizeof(uint16_t) * (size_t)(E + kBinMulSlack)));
     B.cs1 = (uint16_t *)q;
-    SPMV_HIP_TRY(hipMemsetAsync(B.cs1 + E, 0, sizeof(uint16_t) * (size_t)kBinMulSlack, st));
+    SPMV_HIP_TRY(hipMemsetAsync(B.cs1 + Ez, 0, sizeof(uint16_t) * (size_t)(E - Ez + kBinMulSlack), st));
     SPMV_RETURN_IF(p->arena.alloc(&q, sizeof(uint16_t) * (size_t)std::max<int64_t>(ES, 1)));
     B.slot2 = (uint16_t *)q;
-    SPMV_RETURN_IF(p->arena.alloc(&q, sizeof(int32_t) * (size_t)std::max<int64_t>((E + kBinMulSlack) >> B.pad_log, 1)));
-    B.dst1 = (int32_t *)q;
-    SPMV_HIP_TRY(hipMemsetAsync(B.dst1 + (E >> B.pad_log), 0, sizeof(int32_t) * (size_t)(kBinMulSlack >> B.pad_log), st));
+    if (!B.mo) {  // Mul-ordered products need no destinations
+        SPMV_RETURN_IF(p->arena.alloc(&q, sizeof(int32_t) * (size_t)std::max<int64_t>((E + kBinMulSlack) >> B.pad_log, 1)));
+        B.dst1 = (int32_t *)q;
+        SPMV_HIP_TRY(hipMemsetAsync(B.dst1 + (E >> B.pad_log), 0, sizeof(int32_t) * (size_t)(kBinMulSlack >> B.pad_log), st));
+    }
     Scratch sc{st, {}};
     int32_t *d_row0, *d_cnt;
     int64_t *d_bstart, *d_off1, *d_off2, *d_pbb, *d_ks, *d_run, *d_srun;
@@ -249,8 +255,9 @@ int bin_fill_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, c
                        d_row0, (int32_t)C, S, d_off1, d_off2, d_ks, d_kh, d_pbb, B.pad_log, d_run, d_srun,
                        B.strip_block, B.slot_linear ? 0 : B.sum_u, B.val1, B.cs1, B.slot2,
                        B.dst1);
-    hipLaunchKernelGGL(bin_pad_kernel, dim3(grid_of(NB * S)), dim3(256), 0, st, d_cnt, NB * S, d_off1, B.pad_log,
-                       B.val1, B.cs1);
+    if (!B.mo)  // (Mul order: the Mul's segments are not padded)
+        hipLaunchKernelGGL(bin_pad_kernel, dim3(grid_of(NB * S)), dim3(256), 0, st, d_cnt, NB * S, d_off1, B.pad_log,
+                           B.val1, B.cs1);
     return finish(st, "fill");
 }
 

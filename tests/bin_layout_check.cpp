@@ -38,7 +38,7 @@ static int fail(const char *what, long long a = 0, long long b = 0) {
 static int emulate(const BinDev &B, const HostCsr &A, const BinLayout &L, const BinHostArrays &H,
                    const std::vector<double> &x) {
     const int64_t S = L.S, NB = L.NB, C = B.strip, PL = B.pad_log, PADE = (int64_t)1 << PL;
-    const int64_t prod_cap = L.LL > 0 ? L.TRASH + L.PAD : L.E;
+    const int64_t prod_cap = L.LL > 0 ? L.TRASH + L.PAD : B.mo ? L.E1 : L.E;
     std::vector<double> prod((size_t)prod_cap, 0.0);
     std::vector<char> written((size_t)prod_cap, 0);
     BinPieces P;
@@ -76,7 +76,7 @@ static int emulate(const BinDev &B, const HostCsr &A, const BinLayout &L, const 
                                 const int64_t i = e < e1 ? e + lsh : 0;
                                 if (i < 0 || i >= (int64_t)H.lcode.size()) return fail("mul lcode index", i, H.lcode.size());
                                 d[lane] = H.lcode[(size_t)i];
-                            } else {
+                            } else if (!B.mo) {
                                 const int64_t i = ee >> PL;
                                 if (i < 0 || i >= (int64_t)H.dst1.size()) return fail("mul dst1 index", i, H.dst1.size());
                                 d[lane] = H.dst1[(size_t)i];
@@ -118,7 +118,8 @@ static int emulate(const BinDev &B, const HostCsr &A, const BinLayout &L, const 
                         } else {
                             for (int lane = 0; lane < 64; ++lane) {
                                 if (!ok[lane]) continue;
-                                const int64_t pos = ((int64_t)d[lane] << PL) + ((bs + lane) & (PADE - 1));
+                                // Mul order (B.mo): the product of entry e goes to prod[e]
+                                const int64_t pos = B.mo ? bs + lane : ((int64_t)d[lane] << PL) + ((bs + lane) & (PADE - 1));
                                 if (pos < 0 || pos >= prod_cap) return fail("product position", pos, prod_cap);
                                 prod[(size_t)pos] = v[lane];
                                 written[(size_t)pos] = 1;
@@ -145,19 +146,32 @@ static int emulate(const BinDev &B, const HostCsr &A, const BinLayout &L, const 
                         const int64_t e = pos + u * 64 + lane;
                         const int64_t si = sbase + (u / 8) * 512 + lane * 8 + (u % 8);
                         if (si >= L.ES) return fail("slot index", si, L.ES);
+                        // the product read: position e, or (Mul order) lane
+                        // l/8's chunk base from the table + l % 8 (sum_mo_load)
+                        int64_t pe = e;
+                        if (B.mo) {
+                            const int64_t ti = sbase / 8 + bin_mo_tab_at((u * 64 + lane) >> 3, U2);
+                            if (sbase % 8 || ti >= (int64_t)H.mtab.size()) return fail("chunk table index", ti, H.mtab.size());
+                            pe = H.mtab[(size_t)ti] + (lane & 7);
+                        }
+                        if (pe < 0) return fail("negative product position", pe);
                         if (e >= bhi) {
                             // sum_load reads the whole batch unclamped: past the
                             // run it must stay inside the buffer (with its slack)
                             // and hit the dummy slot
-                            if (e >= prod_cap + kBinProdSlack) return fail("sum reads past the product buffer", e, prod_cap);
+                            if (pe >= prod_cap + kBinProdSlack) return fail("sum reads past the product buffer", pe, prod_cap);
                             if (H.slot2[(size_t)si] != SLICE - 1) return fail("slot past a run is not the dummy", e, H.slot2[(size_t)si]);
                             continue;
                         }
-                        if (e >= prod_cap || !written[(size_t)e]) return fail("sum reads an unwritten product", e);
                         const int slot = H.slot2[(size_t)si];
+                        if (B.mo && slot == SLICE - 1) {  // segment padding: the next segment's products
+                            if (pe >= prod_cap + kBinProdSlack) return fail("padding read past the product buffer", pe, prod_cap);
+                            continue;
+                        }
+                        if (pe >= prod_cap || !written[(size_t)pe]) return fail("sum reads an unwritten product", pe);
                         if (slot > SLICE - 1) return fail("slot past the dummy", slot);
                         if (slot < SLICE - 1 && slot >= rows) return fail("slot past the bin", slot, rows);
-                        ys[(size_t)slot] += prod[(size_t)e];
+                        ys[(size_t)slot] += prod[(size_t)pe];
                     }
             }
         }
@@ -203,9 +217,11 @@ int main() {
         const int waves[] = {2, 4, 8};
         for (int si = 0; si < 3; ++si)
             for (int wi = 0; wi < 3; ++wi)
-                for (int pl = 3; pl <= 4; ++pl) {
+                for (int pl = 3; pl <= 4; ++pl)
+                for (int mo = 0; mo < (waves[wi] == 8 ? 1 : 2); ++mo) {
                     spmv_plan_s p;
                     BinDev &B = p.bin;
+                    B.mo = mo == 1;  // products in Mul order (build_bin.cpp bin_mo_resolve)
                     B.strip = strips[si];
                     B.sum_waves = waves[wi];
                     B.max_rows = bin_max_rows(B.sum_waves);
@@ -240,6 +256,7 @@ int main() {
                     if (cur != E) return fail("E", cur, E);
                     // Mul order: strip-major, the bins of a strip in L.mul_bins
                     // order (a permutation of the bins), same padded sizes
+                    // (Mul-ordered products: unpadded, nnz in all)
                     {
                         std::vector<char> hit((size_t)NB, 0);
                         for (int64_t i = 0; i < NB; ++i) {
@@ -253,10 +270,10 @@ int main() {
                         for (int64_t i = 0; i < NB; ++i) {
                             const int64_t b = L.mul_bins[(size_t)i];
                             if (L.off1[(size_t)(b * S + t)] != cur) return fail("off1", b * S + t, cur);
-                            cur += L.rpad(L.cnt[(size_t)(b * S + t)]);
+                            cur += B.mo ? L.cnt[(size_t)(b * S + t)] : L.rpad(L.cnt[(size_t)(b * S + t)]);
                         }
                     }
-                    if (cur != E) return fail("Mul E", cur, E);
+                    if (cur != (B.mo ? nnz : E) || L.E1 != cur) return fail("Mul E", cur, E);
                     // slots: padded runs, bijective index, kernel formula
                     const int U = B.sum_u;
                     const int64_t step = 64 * (int64_t)U;
@@ -276,14 +293,14 @@ int main() {
                         }
                     }
                     ++cases;
-                    if (emu && wi == 1) {  // emulate the kernels on the exact (no long rows) layout
+                    if (emu && (wi == 1 || mo)) {  // emulate the kernels on the exact (no long rows) layout
                         HostCsr A0{m, n, nnz, rp.data(), col.data(), val.data()};
                         BinHostArrays H0;
                         bin_fill_arrays(B, A0, L, H0);
                         if (emulate(B, A0, L, H0, x)) return fail("emulation (exact layout)", trial, si);
                         ++cases;
                     }
-                    if (kind == 0 || (kind == 2 && !emu) || si == 0) continue;
+                    if (mo || kind == 0 || (kind == 2 && !emu) || si == 0) continue;
                     // ---- the same CSR with long rows on the run path: the
                     // auto threshold (long-row CSRs), or 6 entries (many short
                     // long rows, pieces cut at block boundaries)

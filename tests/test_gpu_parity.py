@@ -707,6 +707,34 @@ def test_bin_layout_options(opts):
     assert_bin_rows(plan, run_plan(plan, x, m), rp, col, val, x, what=str(opts))
 
 
+@pytest.mark.parametrize("kind", ["uniform", "powerlaw", "banded", "empty_rows"])
+@pytest.mark.parametrize("opts", [{}, {"bin_pad": 16}, {"bin_sum_waves": 4}, {"bin_strip_cols": 3001}])
+def test_bin_product_orders(kind, opts):
+    """Products in Mul order (the Mul writes its entries' products in place,
+    unpadded; the Sum gathers each bin's segments in 8-entry chunks through
+    the chunk table, k_bin.hip bin_sum_mo_kernel) and in Sum order (the Mul
+    scatters them into padded segments) give the same y, bit for bit: the
+    sequential opt_crs row sums."""
+    m, n = 150_000, 170_003
+    rp, col, val = _bin_matrix(kind, m, n, seed=5)
+    x = sp.generate_vector(n, seed=6)
+    ys = {}
+    for order in (1, 2):
+        plan = sp.Plan.from_csr(m, n, rp, col, val, "bin", bin_product_order=order, bin_long_len=-1, **opts)
+        info = plan.info()
+        assert info["bin_product_order"] == order
+        if order == 2:  # the Mul's entries are not padded
+            assert info["stored_slots"] == len(val) == info["bin_products"]
+            assert info["bin_sum_entries"] >= len(val)
+        ys[order] = run_plan(plan, x, m)
+        assert_bin_rows(plan, ys[order], rp, col, val, x, what=f"order {order} {kind} {opts}")
+    assert np.array_equal(ys[1], ys[2])
+    # Mul order falls back to Sum order with long rows
+    if kind == "powerlaw":
+        lr = sp.Plan.from_csr(m, n, rp, col, val, "bin", bin_long_len=64, bin_product_order=2, **opts)
+        assert lr.info()["bin_long_rows"] > 0 and lr.info()["bin_product_order"] == 1
+
+
 def _create_peak_drop(make):
     """(plan, peak drop of free device memory while `make()` runs): a thread
     polls hipMemGetInfo (torch.cuda.mem_get_info) during the create call."""
@@ -762,7 +790,7 @@ def test_experiment_switches_do_not_reach_the_product_library(monkeypatch):
            "SPMV_BIN_REUSE": "1", "SPMV_BIN_SB": "2", "SPMV_BIN_CUS": "3", "SPMV_BIN_PLACEMENT": "3",
            "SPMV_BIN_HOST_BUILD": "1", "SPMV_CSS_DEBUG": "3", "SPMV_CSS_LAYOUT": "0", "SPMV_CSS_PIECE_DIV": "7",
            "SPMV_CSS_WGS": "5", "SPMV_DIA_DEBUG": "1", "SPMV_DIA_PLACEMENT": "2", "SPMV_ELL_UNROLL": "3",
-           "SPMV_CSR_FORCE_RP64": "1", "SPMV_PLACEMENT_MODE": "9", "SPMV_VMM_CHUNK_MB": "1"}
+           "SPMV_CSR_FORCE_RP64": "1", "SPMV_PLACEMENT_MODE": "9", "SPMV_VMM_CHUNK_MB": "1", "SPMV_BIN_ORDER": "1"}
     for k, v in bad.items():
         monkeypatch.setenv(k, v)
     m = 60_000
@@ -878,7 +906,7 @@ def test_bin_empty_bins_between_full_ones(sum_waves):
     assert not y[:100_000].any() and not y[4_000_000:4_040_000].any()
 
 
-@pytest.mark.parametrize("opts", [{}, {"bin_strip_cols": 3001}, {"bin_groups": 3}])
+@pytest.mark.parametrize("opts", [{}, {"bin_strip_cols": 3001}, {"bin_groups": 3}, {"bin_product_order": 1}])
 def test_bin_device_build(opts, monkeypatch):
     """spmv_plan_create_csr_device with BIN: the segments are counted, laid
     out and filled on the GPU (k_bin_build.hip).  Same bins / strips / slots
@@ -895,7 +923,8 @@ def test_bin_device_build(opts, monkeypatch):
         pd = sp.Plan.from_device_csr(m, n, torch.from_numpy(rp).cuda(), torch.from_numpy(col).cuda(),
                                      torch.from_numpy(val).cuda(), "bin", **opts)
         ih, idv = ph.info(), pd.info()
-        for k in ("format", "stored_slots", "bin_bins", "bin_strips", "bin_pad", "bin_groups"):
+        for k in ("format", "stored_slots", "bin_bins", "bin_strips", "bin_pad", "bin_groups", "bin_product_order",
+                  "bin_sum_entries"):
             assert ih[k] == idv[k], (kind, m, n, k, ih[k], idv[k])
         yd = run_plan(pd, x, m)
         assert np.array_equal(yd, run_plan(ph, x, m)), f"{kind} {m}x{n} {opts}"

@@ -28,7 +28,7 @@ CSRC = os.path.join(ROOT, "singlespmv_amd", "csrc")
 PROBE_VARS = ["SPMV_BIN_DEBUG", "SPMV_BIN_PADLOG", "SPMV_BIN_SUMWAVES", "SPMV_BIN_SLOT_LINEAR", "SPMV_BIN_REUSE",
               "SPMV_BIN_SB", "SPMV_BIN_CUS", "SPMV_BIN_PLACEMENT", "SPMV_BIN_HOST_BUILD", "SPMV_CSS_DEBUG",
               "SPMV_CSS_LAYOUT", "SPMV_CSS_PIECE_DIV", "SPMV_CSS_WGS", "SPMV_DIA_DEBUG", "SPMV_DIA_PLACEMENT",
-              "SPMV_ELL_UNROLL", "SPMV_CSR_FORCE_RP64", "SPMV_PLACEMENT_MODE", "SPMV_VMM_CHUNK_MB"]
+              "SPMV_ELL_UNROLL", "SPMV_CSR_FORCE_RP64", "SPMV_PLACEMENT_MODE", "SPMV_VMM_CHUNK_MB", "SPMV_BIN_ORDER"]
 
 
 def _strings(path):
