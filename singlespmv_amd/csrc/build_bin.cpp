@@ -239,6 +239,8 @@ static void bin_mo_resolve(BinDev &B, const spmv_options_t &o, int64_t LL, int64
     B.mo = B.order_req == SPMV_BIN_ORDER_MUL && LL == 0 && o.bin_groups <= 1 && !B.reuse && !B.slot_linear &&
            B.sum_u == 32 && nnz + kBinProdSlack < ((int64_t)1 << 31);
     if (B.mo && !o.bin_pad && !probe_env("SPMV_BIN_PADLOG")) B.pad_log = 3;
+    B.mo_probe = 0;
+    if (const char *e = probe_env("SPMV_BIN_MO_PROBE")) B.mo_probe = B.mo ? std::atoi(e) : 0;
 }
 
 // ---- row bins: <= max_rows rows, cut at cumulative nnz targets; a multiple
@@ -417,7 +419,7 @@ static void bin_offsets(spmv_plan_s *p, const spmv_options_t &o, BinLayout &L) {
                 const int64_t b = L.mul_bins[(size_t)(g0 + j)];
                 L.off1[(size_t)(b * S + t)] = cur;
                 // Mul-ordered products: the Mul's segments are not padded
-                cur += B.mo ? L.cnt[(size_t)(b * S + t)] : L.rpad(L.cnt[(size_t)(b * S + t)]);
+                cur += B.mo && !(B.mo_probe & 1) ? L.cnt[(size_t)(b * S + t)] : L.rpad(L.cnt[(size_t)(b * S + t)]);
             }
             if (L.LL > 0) {  // G == 1: void up to a 64-entry boundary, then the long blocks
                 cur = (cur + 63) & ~(int64_t)63;
@@ -463,7 +465,8 @@ static void bin_mo_table(const BinDev &B, const BinLayout &L, std::vector<int32_
             const int64_t c = L.cnt[(size_t)(b * S + t)];
             for (int64_t k = 0; k < c; k += 8) {
                 const int64_t rel = o2 + k - r0, i = rel / step, w = rel - i * step;
-                tab[(size_t)((s0 + i * step) / 8 + bin_mo_tab_at(w >> 3, (int)U))] = (int32_t)(o1 + k);
+                const int64_t at = (B.mo_probe & 2) ? bin_mo_tab_at_grouped(w >> 3, (int)U) : bin_mo_tab_at(w >> 3, (int)U);
+                tab[(size_t)((s0 + i * step) / 8 + at)] = (int32_t)(o1 + k);
             }
         }
     }
@@ -537,7 +540,7 @@ static void bin_fill_arrays(const BinDev &B, const HostCsr &A, const BinLayout &
             for (int64_t s = 0; s < S; ++s) {
                 const int64_t n0 = L.cnt[(size_t)(b * S + s)], n8 = L.rpad(n0);
                 for (int64_t k = n0; k < n8; ++k) {
-                    if (!B.mo) {
+                    if (!B.mo || (B.mo_probe & 1)) {
                         val1[(size_t)(o1[s] + k)] = 0.0;
                         cs1[(size_t)(o1[s] + k)] = 0;
                     }

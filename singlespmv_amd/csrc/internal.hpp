@@ -299,6 +299,9 @@ __host__ __device__ inline int64_t bin_slot_index(int64_t e, int64_t r0, int64_t
 // so a lane loads its U/8 words at once and ds_bpermute hands chunk c to the
 // 8 lanes reading it.
 __host__ __device__ inline int64_t bin_mo_tab_at(int64_t c, int U) { return (c & 63) * (U / 8) + (c >> 6); }
+// probe variant (mo_probe & 2): lane group g = l/8 reads its U bases (chunks
+// 8u + g) as U/4 16-byte loads, no ds_bpermute
+__host__ __device__ inline int64_t bin_mo_tab_at_grouped(int64_t c, int U) { return (c & 7) * U + (c >> 3); }
 // The Sum reads whole batches of 64*U products without clamping at a run's
 // end (the padded slot batches send those lanes to the dummy slot), so the
 // product buffer carries one batch of slack past its last run.
@@ -327,6 +330,8 @@ struct BinDev {
     int32_t *dst1 = nullptr;       // per 2^pad_log entries (Sum-ordered products only)
     int order_req = 0;             // spmv_options_t.bin_product_order (SPMV_BIN_ORDER_*)
     bool mo = false;               // products in Mul order (SPMV_BIN_ORDER_MUL, bin_mo_tab_at)
+    int mo_probe = 0;              // probe build (SPMV_BIN_MO_PROBE): 1 Mul order padded like the Sum's
+                                   // (64-B aligned chunks), 2 per-lane chunk tables (no ds_bpermute)
     int32_t *mtab = nullptr;       // mo: [ES / 8] Mul position of every 8-entry Sum chunk
     uint16_t *slot2 = nullptr;
     int64_t n_blocks = 1;         // strip blocks of the product layout

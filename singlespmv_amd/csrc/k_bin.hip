@@ -184,7 +184,10 @@ __global__ __launch_bounds__(kBinMulThreads) void bin_mul_kernel(
     __shared__ double xs[kBinMaxStrip];
     constexpr int NW = kBinMulThreads / 64;
     constexpr int64_t STEP = (int64_t)NW * 64 * U;
-    const int w = threadIdx.x >> 6;
+    // the wave index as a wave-uniform (SGPR) value: the compiler cannot
+    // prove threadIdx.x >> 6 uniform, and the cursor's table loads then
+    // become vector loads whose s_waitcnt vmcnt(0) drains the batch in flight
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const int64_t q0 = piece_off[q_base + blockIdx.x], q1 = piece_off[q_base + blockIdx.x + 1];
     for (int64_t q = q0; q < q1; ++q) {
@@ -355,7 +358,10 @@ __global__ __launch_bounds__(64 * W2) void bin_sum_kernel(
     constexpr int SLICE = kBinLdsDoubles / W2;
     constexpr int64_t STEP = 64 * U;
     __shared__ double ylds[kBinLdsDoubles];
-    const int w = threadIdx.x >> 6;
+    // the wave index as a wave-uniform (SGPR) value: the compiler cannot
+    // prove threadIdx.x >> 6 uniform, and the cursor's table loads then
+    // become vector loads whose s_waitcnt vmcnt(0) drains the batch in flight
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     double *ys = ylds + w * SLICE;
     const int64_t bfirst = b0 + (int64_t)blockIdx.x * W2 + w, bstride = (int64_t)gridDim.x * W2;
@@ -491,21 +497,34 @@ __global__ __launch_bounds__(64 * W2) void bin_sum_kernel(
 // 64 B.  The table is loaded one batch ahead of the products it addresses,
 // so waiting for it never drains the batch of products in flight (loads
 // complete in issue order).
-template <int U>
+// MODE 8192 (probe, mo_probe 2): per-lane tables (bin_mo_tab_at_grouped),
+// U words per lane, no ds_bpermute; MODE 2048 (probe ablation, wrong y): the
+// table and ds_bpermute as usual, but the products read contiguously
+template <int U, int MODE>
 struct SumTab {
-    int32_t t[U / 8];
+    int32_t t[(MODE & 8192) ? U : U / 8];
 };
 
-template <int U>
-__device__ __forceinline__ void sum_mo_tab(SumTab<U> &T, int64_t sb, int lane, const int32_t *__restrict__ mtab) {
+template <int U, int MODE>
+__device__ __forceinline__ void sum_mo_tab(SumTab<U, MODE> &T, int64_t sb, int lane, const int32_t *__restrict__ mtab) {
     static_assert(U == 32, "one 16-byte table load per lane");
-    const bin_u32x4 w = __builtin_nontemporal_load(reinterpret_cast<const bin_u32x4 *>(mtab + (sb >> 3)) + lane);
+    if constexpr ((MODE & 8192) != 0) {
+        const bin_u32x4 *tp = reinterpret_cast<const bin_u32x4 *>(mtab + (sb >> 3) + (lane >> 3) * U);
 #pragma unroll
-    for (int h = 0; h < 4; ++h) T.t[h] = (int32_t)w[h];
+        for (int q = 0; q < U / 4; ++q) {
+            const bin_u32x4 w = __builtin_nontemporal_load(tp + q);
+#pragma unroll
+            for (int h = 0; h < 4; ++h) T.t[4 * q + h] = (int32_t)w[h];
+        }
+    } else {
+        const bin_u32x4 w = __builtin_nontemporal_load(reinterpret_cast<const bin_u32x4 *>(mtab + (sb >> 3)) + lane);
+#pragma unroll
+        for (int h = 0; h < 4; ++h) T.t[h] = (int32_t)w[h];
+    }
 }
 
 template <int U, int MODE>
-__device__ __forceinline__ void sum_mo_load(SumBatch<U, MODE> &B, const SumTab<U> &T, int64_t sb, int lane,
+__device__ __forceinline__ void sum_mo_load(SumBatch<U, MODE> &B, const SumTab<U, MODE> &T, int64_t sb, int lane,
                                             const uint16_t *__restrict__ slot2, const double *__restrict__ prod) {
     const bin_u32x4 *sp = reinterpret_cast<const bin_u32x4 *>(slot2 + sb + (int64_t)lane * 8);
 #pragma unroll
@@ -517,102 +536,118 @@ __device__ __forceinline__ void sum_mo_load(SumBatch<U, MODE> &B, const SumTab<U
     const double *pl = prod + (lane & 7);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-        const int c0 = __builtin_amdgcn_ds_bpermute((((u & 7) << 3) + (lane >> 3)) << 2, T.t[u >> 3]);
-        B.v[u] = ld_stream(pl + c0);
+        if constexpr ((MODE & 8192) != 0) {
+            B.v[u] = ld_stream(pl + T.t[u]);
+        } else {
+            const int c0 = __builtin_amdgcn_ds_bpermute((((u & 7) << 3) + (lane >> 3)) << 2, T.t[u >> 3]);
+            if constexpr ((MODE & 2048) != 0) B.v[u] = ld_stream(prod + (sb >> 1) + u * 64 + lane + (c0 >> 31));
+            else B.v[u] = ld_stream(pl + c0);
+        }
     }
 }
 
-template <int W2, int U, int MODE>
-__global__ __launch_bounds__(64 * W2) void bin_sum_mo_kernel(
-    int64_t nbins, const int64_t *__restrict__ run_off, const int64_t *__restrict__ srun_off,
-    const int32_t *__restrict__ bin_row0, const uint16_t *__restrict__ slot2, const int32_t *__restrict__ mtab,
-    const double *__restrict__ prod, double *__restrict__ y) {
+// ---- the Sum with its pipeline kept inside one bin --------------------------
+// (the Mul-ordered Sum, and the Sum order's A/B against bin_sum_kernel's flat
+// walk).  LLVM's s_waitcnt insertion is conservative around vector stores
+// issued in a loop of unknown trip count (the flat walk writes a finished
+// bin's y and the zeros of empty bins inside its batch loop) and around
+// conditionally issued loads: the ISA of the flat walks waits for vmcnt(0)
+// (or a few) before a batch's adds or table reads, draining the batch in
+// flight.  Here each bin's batch loop issues its loads unconditionally (the
+// batches past the bin's end re-load its last batch and are dropped) and
+// stores nothing, so its waits count only its own pipeline; the bin's y is
+// written after the loop.  A bin's batches walk its runs in order (run 0: its
+// segments; with long rows run 1: its pieces; at most two runs).
+template <int W2, int U, int MODE, bool MO>
+__global__ __launch_bounds__(64 * W2) void bin_sum_bin_kernel(
+    int64_t b0, int64_t b1, int64_t nbins, int64_t nblk, const int64_t *__restrict__ run_off,
+    const int64_t *__restrict__ srun_off, const int32_t *__restrict__ bin_row0, int64_t pbase,
+    const uint16_t *__restrict__ slot2, const int32_t *__restrict__ mtab, const double *__restrict__ prod,
+    double *__restrict__ y) {
     constexpr int SLICE = kBinLdsDoubles / W2;
     constexpr int64_t STEP = 64 * U;
     __shared__ double ylds[kBinLdsDoubles];
-    const int w = threadIdx.x >> 6;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     double *ys = ylds + w * SLICE;
-    const int64_t bfirst = (int64_t)blockIdx.x * W2 + w, bstride = (int64_t)gridDim.x * W2;
-    if (bfirst >= nbins) return;
-    // one cursor over the wave's bins: bin cb, batch at pos of its run;
-    // the batch's slot block (and table block) from ss
-    int64_t cb = bfirst, pos = run_off[cb], end = run_off[cb + 1], rs = pos, ss = srun_off[cb];
-    auto next = [&](int64_t &sb, int64_t &bb) -> bool {
-        while (pos >= end) {
-            cb += bstride;
-            if (cb >= nbins) return false;
-            pos = rs = run_off[cb];
-            end = run_off[cb + 1];
-            ss = srun_off[cb];
-        }
-        sb = ss + (pos - rs);
-        bb = cb;
-        pos += STEP;
-        return true;
-    };
-    int64_t acc = -1, done = bfirst;
-    auto write_zero = [&](int64_t bz) {
-        const int64_t r0 = bin_row0[bz];
-        const int rows = (int)(bin_row0[bz + 1] - r0);
-        for (int i = lane; i < rows; i += 64) __builtin_nontemporal_store(0.0, y + r0 + i);
-    };
-    auto finish = [&]() {
-        const int64_t r0 = bin_row0[acc];
-        const int rows = (int)(bin_row0[acc + 1] - r0);
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        for (int i = lane; i < rows; i += 64) __builtin_nontemporal_store(ys[i], y + r0 + i);
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        done = acc + bstride;
-    };
-    auto begin = [&](int64_t nb) {
-        if (nb == acc) return;
-        if (acc >= 0) finish();
-        for (; done < nb; done += bstride) write_zero(done);
-        const int rows = (int)(bin_row0[nb + 1] - bin_row0[nb]);
-        for (int i = lane; i < rows; i += 64) ys[i] = 0.0;
-        acc = nb;
-        done = nb + bstride;
-    };
     double sink = 0.0;
-    SumBatch<U, MODE> PA, PB;
-    SumTab<U> TA, TB;
-    int64_t s0 = 0, n0 = 0, s1 = 0, n1 = 0, s2 = 0, n2 = 0, s3 = 0, n3 = 0;
-    bool h0 = next(s0, n0);
-    bool h1 = h0 && next(s1, n1);
-    if (h0) sum_mo_tab<U>(TA, s0, lane, mtab);
-    if (h1) sum_mo_tab<U>(TB, s1, lane, mtab);
-    if (h0) sum_mo_load<U, MODE>(PA, TA, s0, lane, slot2, prod);
-    while (h0) {
-        // batch k in PA is added while k+1's products (table TB) and k+2's
-        // table (into TA, free since PA's loads were issued) are in flight
-        const bool h2 = h1 && next(s2, n2);
-        if (h2) sum_mo_tab<U>(TA, s2, lane, mtab);
-        if (h1) sum_mo_load<U, MODE>(PB, TB, s1, lane, slot2, prod);
-        begin(n0);
-        sum_add<U, MODE, SLICE - 1>(PA, 0, 0, lane, ys, sink);
-        if (!h1) break;
-        const bool h3 = h2 && next(s3, n3);
-        if (h3) sum_mo_tab<U>(TB, s3, lane, mtab);
-        if (h2) sum_mo_load<U, MODE>(PA, TA, s2, lane, slot2, prod);
-        begin(n1);
-        sum_add<U, MODE, SLICE - 1>(PB, 0, 0, lane, ys, sink);
-        h0 = h2;
-        s0 = s2;
-        n0 = n2;
-        h1 = h3;
-        s1 = s3;
-        n1 = n3;
+    for (int64_t b = b0 + (int64_t)blockIdx.x * W2 + w; b < b1; b += (int64_t)gridDim.x * W2) {
+        const int64_t r0 = bin_row0[b];
+        const int rows = (int)(bin_row0[b + 1] - r0);
+        for (int i = lane; i < rows; i += 64) ys[i] = 0.0;
+        const int64_t rs0 = run_off[b], ss0 = srun_off[b];
+        const int64_t n0 = (run_off[b + 1] - rs0 + STEP - 1) / STEP;
+        int64_t rs1 = 0, ss1 = 0, n1 = 0;
+        if (!MO && nblk > 1) {
+            rs1 = run_off[nbins + b];
+            ss1 = srun_off[nbins + b];
+            n1 = (run_off[nbins + b + 1] - rs1 + STEP - 1) / STEP;
+        }
+        const int64_t nb = n0 + n1;
+        if (nb > 0) {
+            // batch j's slot block and product base (j clamped to the last)
+            auto sbat = [&](int64_t j) -> int64_t {
+                j = j < nb ? j : nb - 1;
+                return j < n0 ? ss0 + j * STEP : ss1 + (j - n0) * STEP;
+            };
+            auto pbat = [&](int64_t j) -> int64_t {
+                j = j < nb ? j : nb - 1;
+                return j < n0 ? rs0 + j * STEP : rs1 + (j - n0) * STEP;
+            };
+            auto load = [&](SumBatch<U, MODE> &P, const SumTab<U, MODE> &T, int64_t j) {
+                if constexpr (MO) sum_mo_load<U, MODE>(P, T, sbat(j), lane, slot2, prod);
+                else sum_load<U, MODE>(P, pbat(j), 0, 0, lane, pbase, sbat(j), slot2, prod);
+            };
+            SumBatch<U, MODE> PA, PB;
+            SumTab<U, MODE> TA, TB;
+            if constexpr (MO) {
+                sum_mo_tab<U, MODE>(TA, sbat(0), lane, mtab);
+                sum_mo_tab<U, MODE>(TB, sbat(1), lane, mtab);
+            }
+            load(PA, TA, 0);
+            for (int64_t j = 0; j < nb; j += 2) {
+                // batch j (PA) is added while j+1's products (table TB) and
+                // j+2's table (into TA: PA's loads are issued) are in flight
+                if constexpr (MO) sum_mo_tab<U, MODE>(TA, sbat(j + 2), lane, mtab);
+                load(PB, TB, j + 1);
+                sum_add<U, MODE, SLICE - 1>(PA, 0, 0, lane, ys, sink);
+                if (j + 1 >= nb) break;
+                if constexpr (MO) sum_mo_tab<U, MODE>(TB, sbat(j + 3), lane, mtab);
+                load(PA, TA, j + 2);
+                sum_add<U, MODE, SLICE - 1>(PB, 0, 0, lane, ys, sink);
+            }
+        }
+        if ((MODE & 2) && sink == 1.2345e300) ys[0] = sink;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        for (int i = lane; i < rows; i += 64) {
+            if constexpr ((MODE & 512) != 0) __builtin_nontemporal_store(ys[i], y + r0 + i);
+            else y[r0 + i] = ys[i];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     }
-    if (acc >= 0) finish();
-    for (; done < nbins; done += bstride) write_zero(done);
+}
+
+template <int W2, int MODE>
+static void launch_sum_mo_t(const spmv_plan_s *p, double *y) {
+    const BinDev &B = p->bin;
+    hipLaunchKernelGGL((bin_sum_bin_kernel<W2, 32, MODE, true>), dim3((unsigned)B.nwg2), dim3(64 * W2), 0,
+                       p->stream, (int64_t)0, B.n_bins, B.n_bins, (int64_t)1, B.run_off, B.srun_off, B.bin_row0,
+                       (int64_t)0, B.slot2, B.mtab, B.prod, y);
 }
 
 template <int W2>
 static void launch_sum_mo(const spmv_plan_s *p, double *y) {
-    const BinDev &B = p->bin;
-    hipLaunchKernelGGL((bin_sum_mo_kernel<W2, 32, 1 | 512>), dim3((unsigned)B.nwg2), dim3(64 * W2), 0, p->stream,
-                       B.n_bins, B.run_off, B.srun_off, B.bin_row0, B.slot2, B.mtab, B.prod, y);
+#ifdef SPMV_PROBES
+    if (p->bin.mo_probe & 2) {
+        launch_sum_mo_t<W2, 1 | 512 | 8192>(p, y);
+        return;
+    }
+    if (launch_dbg(p->bin.dbg) & (1 << 25)) {  // ablation: contiguous product reads (wrong y)
+        launch_sum_mo_t<W2, 1 | 512 | 2048>(p, y);
+        return;
+    }
+#endif
+    launch_sum_mo_t<W2, 1 | 512>(p, y);
 }
 
 template <int MODE, int PL, int U = 8>
@@ -687,6 +722,15 @@ static void launch_sum_t(const spmv_plan_s *p, int g, double *y) {
     const BinDev &B = p->bin;
     const int64_t b0 = g < 0 ? 0 : B.g_bin[g], b1 = g < 0 ? B.n_bins : B.g_bin[g + 1];
     const int64_t pbase = g < 0 ? 0 : B.g_prod[g];
+#ifdef SPMV_PROBES
+    // A/B (SPMV_LAUNCH_DEBUG bit 26): the pipeline kept inside each bin
+    if (MODE == (1 | 512) && B.n_blocks <= 2 && (launch_dbg(B.dbg) & (1 << 26))) {
+        hipLaunchKernelGGL((bin_sum_bin_kernel<W2, U, MODE, false>), dim3((unsigned)B.nwg2), dim3(64 * W2), 0,
+                           p->stream, b0, b1, B.n_bins, B.n_blocks, B.run_off, B.srun_off, B.bin_row0, pbase,
+                           B.slot2, (const int32_t *)nullptr, B.prod, y);
+        return;
+    }
+#endif
     hipLaunchKernelGGL((bin_sum_kernel<W2, U, MODE>), dim3((unsigned)B.nwg2), dim3(64 * W2), 0, p->stream, b0, b1,
                        B.n_bins, B.n_blocks, B.run_off, B.srun_off, B.bin_row0, pbase, B.slot2, B.prod, y);
 }
