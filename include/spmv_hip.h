@@ -137,8 +137,11 @@ typedef struct spmv_options {
 
 /* Product order of a BIN plan (spmv_options_t.bin_product_order).  Either
  * way each row is summed in column order (bit-identical y). */
-#define SPMV_BIN_ORDER_AUTO 0  /* MUL where the layout allows it (no long rows,
-                                  one row group, < 2^31 entries), else SUM     */
+#define SPMV_BIN_ORDER_AUTO 0  /* MUL for short segments (< 64 entries per
+                                  row bin x column strip: the wide multi-GPU
+                                  rank shapes) where the layout allows it (no
+                                  long rows, one row group, < 2^31 entries),
+                                  else SUM                                    */
 #define SPMV_BIN_ORDER_SUM 1   /* the Mul scatters each product into its (bin,
                                   strip) segment of the Sum's order; the Sum
                                   streams each bin as one contiguous run       */

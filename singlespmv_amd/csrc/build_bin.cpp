@@ -112,6 +112,7 @@ static int bin_params(spmv_plan_s *p, const spmv_options_t &o, int64_t m, int64_
             seg = seg_for(2);
         }
         B.pad_log = seg >= 96.0 ? 4 : 3;
+        B.seg_est = seg;
     }
     if (o.bin_sum_waves) {
         SPMV_CHECK_ARG(o.bin_sum_waves == 2 || o.bin_sum_waves == 4 || o.bin_sum_waves == 8,
@@ -234,9 +235,19 @@ static void bin_long_count(BinLayout &L) {
 // grouped slots with 32-entry Sum batches, and Mul positions that fit the
 // int32 chunk table.  Its Sum reads 8-entry chunks, so the segments' padding
 // in the Sum order is 8 entries unless the caller set bin_pad.
+// AUTO takes it for short segments (expected < 64 entries per (bin, strip)):
+// in-process A/Bs on the same matrices (profiles/round3/probe/mulorder_*),
+// execute ms Sum order -> Mul order: 10 M x 80 M rank shape (40 entries per
+// segment) 1.005 -> 0.975 (Mul 0.70 -> 0.62, Sum 0.314 -> 0.359); 10 M x 40 M
+// (80) 0.891 -> 0.884; 10 M x 20 M (160) 0.8125 -> 0.831; config 2 (320)
+// 0.799 -> 0.827.  The scattered product writes cost the Sum-ordered Mul
+// more the shorter the segments; the chunk gathers cost the Sum about the
+// same at any length.
+constexpr double kBinMulOrderMaxSeg = 64.0;
 static void bin_mo_resolve(BinDev &B, const spmv_options_t &o, int64_t LL, int64_t nnz) {
-    // AUTO: Sum order until the Mul order is measured on the GPU
-    B.mo = B.order_req == SPMV_BIN_ORDER_MUL && LL == 0 && o.bin_groups <= 1 && !B.reuse && !B.slot_linear &&
+    const bool want = B.order_req == SPMV_BIN_ORDER_MUL ||
+                      (B.order_req == SPMV_BIN_ORDER_AUTO && B.seg_est < kBinMulOrderMaxSeg);
+    B.mo = want && LL == 0 && o.bin_groups <= 1 && !B.reuse && !B.slot_linear &&
            B.sum_u == 32 && nnz + kBinProdSlack < ((int64_t)1 << 31);
     if (B.mo && !o.bin_pad && !probe_env("SPMV_BIN_PADLOG")) B.pad_log = 3;
     B.mo_probe = 0;

@@ -329,6 +329,7 @@ struct BinDev {
     uint16_t *cs1 = nullptr;
     int32_t *dst1 = nullptr;       // per 2^pad_log entries (Sum-ordered products only)
     int order_req = 0;             // spmv_options_t.bin_product_order (SPMV_BIN_ORDER_*)
+    double seg_est = 0;            // expected entries per (bin, strip) segment (bin_params)
     bool mo = false;               // products in Mul order (SPMV_BIN_ORDER_MUL, bin_mo_tab_at)
     int mo_probe = 0;              // probe build (SPMV_BIN_MO_PROBE): 1 Mul order padded like the Sum's
                                    // (64-B aligned chunks), 2 per-lane chunk tables (no ds_bpermute)

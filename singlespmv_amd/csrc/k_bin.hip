@@ -534,14 +534,20 @@ __device__ __forceinline__ void sum_mo_load(SumBatch<U, MODE> &B, const SumTab<U
         for (int h = 0; h < 4; ++h) B.w[4 * q + h] = w[h];
     }
     const double *pl = prod + (lane & 7);
+    if constexpr ((MODE & 8192) != 0) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-        if constexpr ((MODE & 8192) != 0) {
-            B.v[u] = ld_stream(pl + T.t[u]);
-        } else {
-            const int c0 = __builtin_amdgcn_ds_bpermute((((u & 7) << 3) + (lane >> 3)) << 2, T.t[u >> 3]);
-            if constexpr ((MODE & 2048) != 0) B.v[u] = ld_stream(prod + (sb >> 1) + u * 64 + lane + (c0 >> 31));
-            else B.v[u] = ld_stream(pl + c0);
+        for (int u = 0; u < U; ++u) B.v[u] = ld_stream(pl + T.t[u]);
+    } else {
+        // all U bases first, then the U loads: a load right behind its own
+        // ds_bpermute waits out the LDS latency, U times per batch
+        int c[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) c[u] = __builtin_amdgcn_ds_bpermute((((u & 7) << 3) + (lane >> 3)) << 2, T.t[u >> 3]);
+        if constexpr ((MODE & 16384) == 0) __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if constexpr ((MODE & 2048) != 0) B.v[u] = ld_stream(prod + (sb >> 1) + u * 64 + lane + (c[u] >> 31));
+            else B.v[u] = ld_stream(pl + c[u]);
         }
     }
 }
@@ -644,6 +650,10 @@ static void launch_sum_mo(const spmv_plan_s *p, double *y) {
     }
     if (launch_dbg(p->bin.dbg) & (1 << 25)) {  // ablation: contiguous product reads (wrong y)
         launch_sum_mo_t<W2, 1 | 512 | 2048>(p, y);
+        return;
+    }
+    if (launch_dbg(p->bin.dbg) & (1 << 27)) {  // A/B: bases and loads interleaved by the scheduler
+        launch_sum_mo_t<W2, 1 | 512 | 16384>(p, y);
         return;
     }
 #endif

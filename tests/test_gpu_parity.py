@@ -735,6 +735,21 @@ def test_bin_product_orders(kind, opts):
         assert lr.info()["bin_long_rows"] > 0 and lr.info()["bin_product_order"] == 1
 
 
+def test_bin_auto_product_order():
+    """AUTO picks the Mul order for short (bin, strip) segments -- a wide
+    matrix like the multi-GPU rank shapes (here 20 K x 60 M, 16 per row:
+    ~55 entries per segment) -- and the Sum order for long ones."""
+    m, n = 20_000, 60_000_000
+    spec = sp.gen_spec("uniform", m, n, per_row=16, seed=9)
+    rp, col, val = sp.generate_csr(spec, 0, m)
+    x = sp.generate_vector(n, seed=10)
+    plan = sp.Plan.from_csr(m, n, rp, col, val, "bin")
+    assert plan.info()["bin_product_order"] == 2
+    assert np.array_equal(run_plan(plan, x, m), oracle_y(rp, col, val, x))
+    rp2, col2, val2 = _bin_matrix("uniform", 150_000, 170_003, seed=5)
+    assert sp.Plan.from_csr(150_000, 170_003, rp2, col2, val2, "bin").info()["bin_product_order"] == 1
+
+
 def _create_peak_drop(make):
     """(plan, peak drop of free device memory while `make()` runs): a thread
     polls hipMemGetInfo (torch.cuda.mem_get_info) during the create call."""
