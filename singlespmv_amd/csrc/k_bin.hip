@@ -562,8 +562,10 @@ __device__ __forceinline__ void sum_mo_load(SumBatch<U, MODE> &B, const SumTab<U
 // flight.  Here each bin's batch loop issues its loads unconditionally (the
 // batches past the bin's end re-load its last batch and are dropped) and
 // stores nothing, so its waits count only its own pipeline; the bin's y is
-// written after the loop.  A bin's batches walk its runs in order (run 0: its
-// segments; with long rows run 1: its pieces; at most two runs).
+// written after the loop, while the next bin's first batches already load
+// (the loop's batches past its bin's end are the next bin's).  A bin's
+// batches walk its runs in order (run 0: its segments; with long rows run 1:
+// its pieces; at most two runs).
 template <int W2, int U, int MODE, bool MO>
 __global__ __launch_bounds__(64 * W2) void bin_sum_bin_kernel(
     int64_t b0, int64_t b1, int64_t nbins, int64_t nblk, const int64_t *__restrict__ run_off,
@@ -577,59 +579,97 @@ __global__ __launch_bounds__(64 * W2) void bin_sum_bin_kernel(
     const int lane = threadIdx.x & 63;
     double *ys = ylds + w * SLICE;
     double sink = 0.0;
-    for (int64_t b = b0 + (int64_t)blockIdx.x * W2 + w; b < b1; b += (int64_t)gridDim.x * W2) {
-        const int64_t r0 = bin_row0[b];
-        const int rows = (int)(bin_row0[b + 1] - r0);
-        for (int i = lane; i < rows; i += 64) ys[i] = 0.0;
-        const int64_t rs0 = run_off[b], ss0 = srun_off[b];
-        const int64_t n0 = (run_off[b + 1] - rs0 + STEP - 1) / STEP;
-        int64_t rs1 = 0, ss1 = 0, n1 = 0;
+    // a bin's rows and runs (run 0: its segments; with long rows run 1: its
+    // pieces), batch j's slot block and product base
+    struct BinRun {
+        int64_t r0 = 0, nb = 0, n0 = 0, rs0 = 0, ss0 = 0, rs1 = 0, ss1 = 0;
+        int rows = 0;
+        __device__ int64_t s(int64_t j) const { return j < n0 ? ss0 + j * STEP : ss1 + (j - n0) * STEP; }
+        __device__ int64_t p(int64_t j) const { return j < n0 ? rs0 + j * STEP : rs1 + (j - n0) * STEP; }
+    };
+    auto bin_at = [&](int64_t b) {
+        BinRun R;
+        R.r0 = bin_row0[b];
+        R.rows = (int)(bin_row0[b + 1] - R.r0);
+        R.rs0 = run_off[b];
+        R.ss0 = srun_off[b];
+        R.n0 = (run_off[b + 1] - R.rs0 + STEP - 1) / STEP;
+        R.nb = R.n0;
         if (!MO && nblk > 1) {
-            rs1 = run_off[nbins + b];
-            ss1 = srun_off[nbins + b];
-            n1 = (run_off[nbins + b + 1] - rs1 + STEP - 1) / STEP;
+            R.rs1 = run_off[nbins + b];
+            R.ss1 = srun_off[nbins + b];
+            R.nb += (run_off[nbins + b + 1] - R.rs1 + STEP - 1) / STEP;
         }
-        const int64_t nb = n0 + n1;
-        if (nb > 0) {
-            // batch j's slot block and product base (j clamped to the last)
-            auto sbat = [&](int64_t j) -> int64_t {
-                j = j < nb ? j : nb - 1;
-                return j < n0 ? ss0 + j * STEP : ss1 + (j - n0) * STEP;
-            };
-            auto pbat = [&](int64_t j) -> int64_t {
-                j = j < nb ? j : nb - 1;
-                return j < n0 ? rs0 + j * STEP : rs1 + (j - n0) * STEP;
-            };
-            auto load = [&](SumBatch<U, MODE> &P, const SumTab<U, MODE> &T, int64_t j) {
-                if constexpr (MO) sum_mo_load<U, MODE>(P, T, sbat(j), lane, slot2, prod);
-                else sum_load<U, MODE>(P, pbat(j), 0, 0, lane, pbase, sbat(j), slot2, prod);
-            };
-            SumBatch<U, MODE> PA, PB;
-            SumTab<U, MODE> TA, TB;
-            if constexpr (MO) {
-                sum_mo_tab<U, MODE>(TA, sbat(0), lane, mtab);
-                sum_mo_tab<U, MODE>(TB, sbat(1), lane, mtab);
+        return R;
+    };
+    const int64_t bstride = (int64_t)gridDim.x * W2;
+    int64_t b = b0 + (int64_t)blockIdx.x * W2 + w;
+    if (b >= b1) return;
+    BinRun R = bin_at(b);
+    for (int i = lane; i < R.rows; i += 64) ys[i] = 0.0;
+    SumBatch<U, MODE> PA, PB;
+    SumTab<U, MODE> TA, TB;
+    bool pre = false;  // R's batch 0 (PA) and batch 1's table (TB) are in flight
+    for (;;) {
+        const int64_t bn = b + bstride;
+        const bool more = bn < b1;
+        const BinRun N = more ? bin_at(bn) : R;
+        // batches past R's end are the next bin's first ones (its pipeline
+        // starts while R's y is written), or R's last batch again (dropped)
+        const bool pfn = more && N.nb > 0;
+        auto sbat = [&](int64_t j) -> int64_t {
+            if (j < R.nb) return R.s(j);
+            return pfn ? N.s(j - R.nb < N.nb ? j - R.nb : N.nb - 1) : R.s(R.nb - 1);
+        };
+        auto pbat = [&](int64_t j) -> int64_t {
+            if (j < R.nb) return R.p(j);
+            return pfn ? N.p(j - R.nb < N.nb ? j - R.nb : N.nb - 1) : R.p(R.nb - 1);
+        };
+        auto load = [&](SumBatch<U, MODE> &P, const SumTab<U, MODE> &T, int64_t j) {
+            if constexpr (MO) sum_mo_load<U, MODE>(P, T, sbat(j), lane, slot2, prod);
+            else sum_load<U, MODE>(P, pbat(j), 0, 0, lane, pbase, sbat(j), slot2, prod);
+        };
+        bool swapped = false;
+        if (R.nb > 0) {
+            if (!pre) {
+                if constexpr (MO) {
+                    sum_mo_tab<U, MODE>(TA, sbat(0), lane, mtab);
+                    sum_mo_tab<U, MODE>(TB, sbat(1), lane, mtab);
+                }
+                load(PA, TA, 0);
             }
-            load(PA, TA, 0);
-            for (int64_t j = 0; j < nb; j += 2) {
+            for (int64_t j = 0;; j += 2) {
                 // batch j (PA) is added while j+1's products (table TB) and
                 // j+2's table (into TA: PA's loads are issued) are in flight
                 if constexpr (MO) sum_mo_tab<U, MODE>(TA, sbat(j + 2), lane, mtab);
                 load(PB, TB, j + 1);
                 sum_add<U, MODE, SLICE - 1>(PA, 0, 0, lane, ys, sink);
-                if (j + 1 >= nb) break;
+                if (j + 1 >= R.nb) {
+                    swapped = true;  // the next bin's batch 0 is in PB, its batch 1's table in TA
+                    break;
+                }
                 if constexpr (MO) sum_mo_tab<U, MODE>(TB, sbat(j + 3), lane, mtab);
                 load(PA, TA, j + 2);
                 sum_add<U, MODE, SLICE - 1>(PB, 0, 0, lane, ys, sink);
+                if (j + 2 >= R.nb) break;
             }
         }
+        pre = R.nb > 0 && pfn;
         if ((MODE & 2) && sink == 1.2345e300) ys[0] = sink;
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        for (int i = lane; i < rows; i += 64) {
-            if constexpr ((MODE & 512) != 0) __builtin_nontemporal_store(ys[i], y + r0 + i);
-            else y[r0 + i] = ys[i];
+        for (int i = lane; i < R.rows; i += 64) {
+            if constexpr ((MODE & 512) != 0) __builtin_nontemporal_store(ys[i], y + R.r0 + i);
+            else y[R.r0 + i] = ys[i];
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        if (!more) break;
+        for (int i = lane; i < N.rows; i += 64) ys[i] = 0.0;
+        if (pre && swapped) {
+            PA = PB;
+            TB = TA;
+        }
+        b = bn;
+        R = N;
     }
 }
 
