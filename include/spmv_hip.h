@@ -137,7 +137,7 @@ typedef struct spmv_options {
 
 /* Product order of a BIN plan (spmv_options_t.bin_product_order).  Either
  * way each row is summed in column order (bit-identical y). */
-#define SPMV_BIN_ORDER_AUTO 0  /* MUL for short segments (< 64 entries per
+#define SPMV_BIN_ORDER_AUTO 0  /* MUL for short segments (< 112 entries per
                                   row bin x column strip: the wide multi-GPU
                                   rank shapes) where the layout allows it (no
                                   long rows, one row group, < 2^31 entries),

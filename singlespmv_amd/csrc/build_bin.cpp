@@ -235,15 +235,15 @@ static void bin_long_count(BinLayout &L) {
 // grouped slots with 32-entry Sum batches, and Mul positions that fit the
 // int32 chunk table.  Its Sum reads 8-entry chunks, so the segments' padding
 // in the Sum order is 8 entries unless the caller set bin_pad.
-// AUTO takes it for short segments (expected < 64 entries per (bin, strip)):
-// in-process A/Bs on the same matrices (profiles/round3/probe/mulorder_*),
-// execute ms Sum order -> Mul order: 10 M x 80 M rank shape (40 entries per
-// segment) 1.005 -> 0.975 (Mul 0.70 -> 0.62, Sum 0.314 -> 0.359); 10 M x 40 M
-// (80) 0.891 -> 0.884; 10 M x 20 M (160) 0.8125 -> 0.831; config 2 (320)
-// 0.799 -> 0.827.  The scattered product writes cost the Sum-ordered Mul
-// more the shorter the segments; the chunk gathers cost the Sum about the
-// same at any length.
-constexpr double kBinMulOrderMaxSeg = 64.0;
+// AUTO takes it for short segments (expected < 112 entries per (bin,
+// strip)): in-process A/Bs on the same matrices (profiles/round3/probe/
+// mulorder_*), execute ms Sum order -> Mul order: 10 M x 80 M rank shape
+// (42 entries per segment) 1.008 -> 0.959 (Mul 0.70 -> 0.61, Sum 0.315 ->
+// 0.352); 10 M x 40 M (84) 0.900 -> 0.880; 10 M x 20 M (168) 0.823 ->
+// 0.832; config 2 (320) 0.809 -> 0.830.  The scattered product writes cost
+// the Sum-ordered Mul more the shorter the segments; the chunk gathers cost
+// the Sum about the same at any length.
+constexpr double kBinMulOrderMaxSeg = 112.0;
 static void bin_mo_resolve(BinDev &B, const spmv_options_t &o, int64_t LL, int64_t nnz) {
     const bool want = B.order_req == SPMV_BIN_ORDER_MUL ||
                       (B.order_req == SPMV_BIN_ORDER_AUTO && B.seg_est < kBinMulOrderMaxSeg);

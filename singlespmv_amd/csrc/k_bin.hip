@@ -47,6 +47,8 @@ namespace spmv {
 // batch of loads in flight while it consumes the other (the single-batch
 // loop drained the memory pipe every iteration: BIN lost 25 % on 160 CUs
 // instead of 256, profiles/round1/probe/bin_cus.jsonl).
+typedef uint32_t bin_u32x4 __attribute__((ext_vector_type(4)));
+
 template <int U>
 struct MulBatch {
     double v[U];
@@ -69,10 +71,19 @@ __device__ __forceinline__ void mul_load(MulBatch<U> &B, int64_t base, int64_t e
         const double *vb = val1 + base + lane;
         const uint16_t *cb = cs1 + base + lane;
         const int32_t *db = dst1 + ((base + lane) >> PL);
+        uint32_t cw[4] = {0, 0, 0, 0};
+        if constexpr ((MODE & 32768) != 0) {
+            // ablation (probe, wrong y): the batch's 1 KB of columns as ONE
+            // 16-byte load per lane (what an 8-entry lane-grouped cs1 would load)
+            static_assert(U == 8, "8 columns per 16-byte load");
+            const bin_u32x4 t = __builtin_nontemporal_load(reinterpret_cast<const bin_u32x4 *>(cs1 + base) + lane);
+            cw[0] = t[0], cw[1] = t[1], cw[2] = t[2], cw[3] = t[3];
+        }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             B.v[u] = ld_stream(vb + u * 64);
-            B.c[u] = (MODE & 8) ? (uint32_t)(((base + u * 64 + lane) * 2654435761u) & 16383)
+            if constexpr ((MODE & 32768) != 0) B.c[u] = (cw[(u >> 1) & 3] >> (16 * (u & 1))) & 16383;
+            else B.c[u] = (MODE & 8) ? (uint32_t)(((base + u * 64 + lane) * 2654435761u) & 16383)
                                 : (uint32_t)__builtin_nontemporal_load(cb + u * 64);
             // a lane past the piece (e >= e1, masked at the store) reads word 0:
             // its e may lie beyond the strip's long blocks
@@ -261,8 +272,6 @@ struct SumBatch {
         else return (w[u >> 1] >> (16 * (u & 1))) & 0xFFFFu;
     }
 };
-
-typedef uint32_t bin_u32x4 __attribute__((ext_vector_type(4)));
 
 // sbase: the batch's slot block (bin_slot_index): this lane's slots u..u+7
 // are one 16-byte word, the wave's word q one contiguous KB
@@ -750,6 +759,7 @@ static void launch_mul_p(const spmv_plan_s *p, int g, const double *x) {
             // x strips staged serially / in bursts (A/B, build_bin.cpp xburst);
             // 1 << 24: x strips through registers instead of LDS-DMA (A/B)
             if (dbg & (1 << 21)) launch_mul_t<513, PL>(p, g, x);  // ablation: no x staging
+            else if ((dbg & (1 << 28)) && dma) launch_mul_t<257 | 32768, PL>(p, g, x);  // ablation: 16-B column loads
             else if (dbg & (1 << 23)) launch_mul_t<1, PL, 4>(p, g, x);  // A/B: 4-entry batches (half in flight)
             else if (dbg & 16384) launch_mul_t<65, PL>(p, g, x);
             else if (dbg & 2048) launch_mul_t<17, PL>(p, g, x);
