@@ -828,6 +828,7 @@ static int bin_finish(spmv_plan_s *p, int64_t n, const BinLayout &L, const spmv_
         for (float tt : B.placement_ms) std::fprintf(stderr, " %.4f", tt);
         std::fprintf(stderr, "\n");
     }
+    if (B.mo) p->kernel_name = "bin_mul_kernel+bin_sum_bin_kernel";  // the Mul-ordered Sum
     p->stored_slots = L.E1;
     B.mul_entries = L.E1;
     B.long_pieces = L.NP;
