@@ -174,7 +174,8 @@ def test_traffic_keys_name_the_shape():
     import bench
     t = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic_calibrated.json")))
     assert bench.traffic_key("c2", 10_000_000, 10_000_000, "bin_mul_kernel+bin_sum_kernel") in t
-    assert bench.traffic_key("c2", 10_000_000, 80_000_000, "bin_mul_kernel+bin_sum_kernel") in t  # N = 8 rank
+    # N = 8 rank shape (AUTO: Mul-ordered products)
+    assert bench.traffic_key("c2", 10_000_000, 80_000_000, "bin_mul_kernel+bin_sum_bin_kernel") in t
     assert bench.traffic_key("c2", 10_000_000, 30_000_000, "bin_mul_kernel+bin_sum_kernel") not in t  # unprofiled
 
 
