@@ -760,6 +760,7 @@ static void launch_mul_p(const spmv_plan_s *p, int g, const double *x) {
             // 1 << 24: x strips through registers instead of LDS-DMA (A/B)
             if (dbg & (1 << 21)) launch_mul_t<513, PL>(p, g, x);  // ablation: no x staging
             else if ((dbg & (1 << 28)) && dma) launch_mul_t<257 | 32768, PL>(p, g, x);  // ablation: 16-B column loads
+            else if ((dbg & (1 << 29)) && dma) launch_mul_t<256, PL>(p, g, x);  // A/B: ordinary product stores
             else if (dbg & (1 << 23)) launch_mul_t<1, PL, 4>(p, g, x);  // A/B: 4-entry batches (half in flight)
             else if (dbg & 16384) launch_mul_t<65, PL>(p, g, x);
             else if (dbg & 2048) launch_mul_t<17, PL>(p, g, x);
