@@ -545,7 +545,7 @@ __device__ __forceinline__ void sum_mo_load(SumBatch<U, MODE> &B, const SumTab<U
     const double *pl = prod + (lane & 7);
     if constexpr ((MODE & 8192) != 0) {
 #pragma unroll
-        for (int u = 0; u < U; ++u) B.v[u] = ld_stream(pl + T.t[u]);
+        for (int u = 0; u < U; ++u) B.v[u] = (MODE & 1) ? ld_stream(pl + T.t[u]) : pl[T.t[u]];
     } else {
         // all U bases first, then the U loads: a load right behind its own
         // ds_bpermute waits out the LDS latency, U times per batch
@@ -556,6 +556,7 @@ __device__ __forceinline__ void sum_mo_load(SumBatch<U, MODE> &B, const SumTab<U
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             if constexpr ((MODE & 2048) != 0) B.v[u] = ld_stream(prod + (sb >> 1) + u * 64 + lane + (c[u] >> 31));
+            else if constexpr ((MODE & 1) == 0) B.v[u] = pl[c[u]];  // the default (launch_sum_mo)
             else B.v[u] = ld_stream(pl + c[u]);
         }
     }
@@ -694,19 +695,28 @@ template <int W2>
 static void launch_sum_mo(const spmv_plan_s *p, double *y) {
 #ifdef SPMV_PROBES
     if (p->bin.mo_probe & 2) {
-        launch_sum_mo_t<W2, 1 | 512 | 8192>(p, y);
+        launch_sum_mo_t<W2, 512 | 8192>(p, y);
         return;
     }
     if (launch_dbg(p->bin.dbg) & (1 << 25)) {  // ablation: contiguous product reads (wrong y)
-        launch_sum_mo_t<W2, 1 | 512 | 2048>(p, y);
+        launch_sum_mo_t<W2, 512 | 2048>(p, y);
+        return;
+    }
+    if (launch_dbg(p->bin.dbg) & (1 << 30)) {  // A/B: nontemporal product loads
+        launch_sum_mo_t<W2, 1 | 512>(p, y);
         return;
     }
     if (launch_dbg(p->bin.dbg) & (1 << 27)) {  // A/B: bases and loads interleaved by the scheduler
-        launch_sum_mo_t<W2, 1 | 512 | 16384>(p, y);
+        launch_sum_mo_t<W2, 512 | 16384>(p, y);
         return;
     }
 #endif
-    launch_sum_mo_t<W2, 1 | 512>(p, y);
+    // ordinary (cached) product loads: a chunk's 64 B start at any 8-byte
+    // offset, so most chunks share a 128-B line with the next one -- kept in
+    // L2 it is read from HBM once.  Nontemporal loads (the Sum order's
+    // choice) cost the rank shape's Sum 0.310 -> 0.342 ms on the same plan
+    // (profiles/round3/probe/mulorder_store_load_policy_*.jsonl)
+    launch_sum_mo_t<W2, 512>(p, y);
 }
 
 template <int MODE, int PL, int U = 8>
