@@ -201,7 +201,10 @@ __global__ __launch_bounds__(kBinMulThreads) void bin_mul_kernel(
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const int64_t q0 = piece_off[q_base + blockIdx.x], q1 = piece_off[q_base + blockIdx.x + 1];
-    for (int64_t q = q0; q < q1; ++q) {
+    for (int64_t qq = q0; qq < q1; ++qq) {
+        // MODE 131072 (probe A/B): each workgroup starts at a different one
+        // of its pieces (breaks the lockstep of the workgroups' streams)
+        const int64_t q = (MODE & 131072) ? q0 + (qq - q0 + blockIdx.x) % (q1 - q0) : qq;
         // consecutive pieces of a workgroup are consecutive strips: stage x
         const int32_t st = piece_strip[q];
         const int64_t c0 = (int64_t)st * strip;
@@ -771,6 +774,7 @@ static void launch_mul_p(const spmv_plan_s *p, int g, const double *x) {
             if (dbg & (1 << 21)) launch_mul_t<513, PL>(p, g, x);  // ablation: no x staging
             else if ((dbg & (1 << 28)) && dma) launch_mul_t<257 | 32768, PL>(p, g, x);  // ablation: 16-B column loads
             else if ((dbg & (1 << 29)) && dma) launch_mul_t<256, PL>(p, g, x);  // A/B: ordinary product stores
+            else if ((dbg & (1 << 20)) && dma) launch_mul_t<257 | 131072, PL>(p, g, x);  // A/B: rotated pieces
             else if (dbg & (1 << 23)) launch_mul_t<1, PL, 4>(p, g, x);  // A/B: 4-entry batches (half in flight)
             else if (dbg & 16384) launch_mul_t<65, PL>(p, g, x);
             else if (dbg & 2048) launch_mul_t<17, PL>(p, g, x);
