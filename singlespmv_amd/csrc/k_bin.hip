@@ -753,10 +753,21 @@ static void launch_mul_p(const spmv_plan_s *p, int g, const double *x) {
     // profiles/round3/probe/mul_glds_*.jsonl), else through registers.  The
     // ablation MODEs exist only in the probe build (SPMV_BIN_DEBUG bits 0-1,
     // -DSPMV_PROBES).
+    // Mul-ordered products (BinDev::mo) are stored with ordinary stores: the
+    // contiguous write streams of all workgroups ran the rank shape's Mul at
+    // 0.593-0.660 instead of 0.642-0.733 ms on two boxes, the Sum after
+    // them (cached loads) 0.307-0.310 -> 0.346-0.363: execute 0.944 -> 0.933
+    // and 1.039 -> 1.017 ms (profiles/round3/probe/mulorder_store_load_policy_*).
     const bool dma = (reinterpret_cast<uintptr_t>(x) & 15) == 0 && p->bin.strip % 2 == 0;
+    const bool mo = p->bin.mo;
 #ifndef SPMV_PROBES
-    if (dma) launch_mul_t<257, PL>(p, g, x);
-    else launch_mul_t<1, PL>(p, g, x);
+    if (dma) {
+        if (mo) launch_mul_t<256, PL>(p, g, x);
+        else launch_mul_t<257, PL>(p, g, x);
+    } else {
+        if (mo) launch_mul_t<0, PL>(p, g, x);
+        else launch_mul_t<1, PL>(p, g, x);
+    }
 #else
     const int dbg = launch_dbg(p->bin.dbg);
     switch (dbg & 3) {
@@ -773,14 +784,22 @@ static void launch_mul_p(const spmv_plan_s *p, int g, const double *x) {
             // 1 << 24: x strips through registers instead of LDS-DMA (A/B)
             if (dbg & (1 << 21)) launch_mul_t<513, PL>(p, g, x);  // ablation: no x staging
             else if ((dbg & (1 << 28)) && dma) launch_mul_t<257 | 32768, PL>(p, g, x);  // ablation: 16-B column loads
-            else if ((dbg & (1 << 29)) && dma) launch_mul_t<256, PL>(p, g, x);  // A/B: ordinary product stores
+            else if ((dbg & (1 << 29)) && dma) {  // A/B: the other product-store policy
+                if (mo) launch_mul_t<257, PL>(p, g, x);
+                else launch_mul_t<256, PL>(p, g, x);
+            }
             else if ((dbg & (1 << 20)) && dma) launch_mul_t<257 | 131072, PL>(p, g, x);  // A/B: rotated pieces
             else if (dbg & (1 << 23)) launch_mul_t<1, PL, 4>(p, g, x);  // A/B: 4-entry batches (half in flight)
             else if (dbg & 16384) launch_mul_t<65, PL>(p, g, x);
             else if (dbg & 2048) launch_mul_t<17, PL>(p, g, x);
             else if (dbg & 4096) launch_mul_t<33, PL>(p, g, x);
-            else if (dma && !(dbg & (1 << 24))) launch_mul_t<257, PL>(p, g, x);
-            else launch_mul_t<1, PL>(p, g, x);
+            else if (dma && !(dbg & (1 << 24))) {
+                if (mo) launch_mul_t<256, PL>(p, g, x);
+                else launch_mul_t<257, PL>(p, g, x);
+            } else {
+                if (mo) launch_mul_t<0, PL>(p, g, x);
+                else launch_mul_t<1, PL>(p, g, x);
+            }
     }
 #endif
 }
