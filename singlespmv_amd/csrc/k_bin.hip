@@ -158,7 +158,8 @@ __device__ __forceinline__ void mul_long_block(double pr, int32_t code, bool ok,
 
 template <int U, int MODE, int PL, bool LONG>
 __device__ __forceinline__ void mul_store(const MulBatch<U> &B, int64_t base, int64_t e1, int lane,
-                                          const double *xs, double *__restrict__ prod, int64_t ls) {
+                                          const double *xs, double *__restrict__ prod, int64_t ls,
+                                          bool nt_tail = false) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const int64_t e = base + u * 64 + lane;
@@ -171,7 +172,7 @@ __device__ __forceinline__ void mul_store(const MulBatch<U> &B, int64_t base, in
             double *dp = (MODE & 4) ? prod + e : prod + ((int64_t)B.d[u] << PL) + (e & ((1 << PL) - 1));
             if (MODE & 2) {
                 if (pr == 1.2345e300) *dp = pr;
-            } else if (MODE & 1) {
+            } else if ((MODE & 1) || ((MODE & 65536) && nt_tail)) {
                 __builtin_nontemporal_store(pr, dp);
             } else {
                 *dp = pr;
@@ -205,6 +206,9 @@ __global__ __launch_bounds__(kBinMulThreads) void bin_mul_kernel(
         // MODE 131072 (probe A/B): each workgroup starts at a different one
         // of its pieces (breaks the lockstep of the workgroups' streams)
         const int64_t q = (MODE & 131072) ? q0 + (qq - q0 + blockIdx.x) % (q1 - q0) : qq;
+        // MODE 65536 (probe A/B): ordinary product stores for the first 70 %
+        // of the workgroup's pieces, nontemporal for the rest
+        const bool nt_tail = (MODE & 65536) && (qq - q0) * 10 >= (q1 - q0) * 7;
         // consecutive pieces of a workgroup are consecutive strips: stage x
         const int32_t st = piece_strip[q];
         const int64_t c0 = (int64_t)st * strip;
@@ -255,11 +259,11 @@ __global__ __launch_bounds__(kBinMulThreads) void bin_mul_kernel(
         for (int64_t it = 0; it < nit; it += 2) {
             const int64_t ba = bat(it), bb = bat(it + 1);
             if (it + 1 < nit) mul_load<U, PL, MODE, LONG>(B, bb, e0, e1, lane, val1, cs1, dst1, ls, lsh, lcode);
-            mul_store<U, MODE, PL, LONG>(A, ba, e1, lane, xs, prod, ls);
+            mul_store<U, MODE, PL, LONG>(A, ba, e1, lane, xs, prod, ls, nt_tail);
             if (it + 1 < nit) {
                 if (it + 2 < nit)
                     mul_load<U, PL, MODE, LONG>(A, bat(it + 2), e0, e1, lane, val1, cs1, dst1, ls, lsh, lcode);
-                mul_store<U, MODE, PL, LONG>(B, bb, e1, lane, xs, prod, ls);
+                mul_store<U, MODE, PL, LONG>(B, bb, e1, lane, xs, prod, ls, nt_tail);
             }
         }
     }
@@ -789,6 +793,7 @@ static void launch_mul_p(const spmv_plan_s *p, int g, const double *x) {
                 else launch_mul_t<256, PL>(p, g, x);
             }
             else if ((dbg & (1 << 20)) && dma) launch_mul_t<257 | 131072, PL>(p, g, x);  // A/B: rotated pieces
+            else if ((dbg & (1 << 22)) && dma) launch_mul_t<256 | 65536, PL>(p, g, x);  // A/B: nontemporal tail
             else if (dbg & (1 << 23)) launch_mul_t<1, PL, 4>(p, g, x);  // A/B: 4-entry batches (half in flight)
             else if (dbg & 16384) launch_mul_t<65, PL>(p, g, x);
             else if (dbg & 2048) launch_mul_t<17, PL>(p, g, x);
