@@ -20,6 +20,10 @@
 //    streams the bin's products -- contiguous, ordered [strip][k, row] -- and
 //    adds them with ds_add_f64 into its own LDS y slice, then writes the
 //    bin's y rows; each wave walks all of its bins with one batch cursor.
+//  * Mul order (BinDev::mo, the wide multi-GPU rank shapes whose segments
+//    are short): the Mul writes entry e's product to prod[e] instead, and
+//    bin_sum_bin_kernel gathers each bin's Sum order back in 8-entry chunks
+//    through a chunk table (same add order, same y).
 //
 // HBM bytes per nnz: Mul 8 (val) + 2 (column in strip) + 0.25-0.5
 // (destination) + 8 (product), Sum 8 (product) + 2 (row in bin): ~28.5 B,
