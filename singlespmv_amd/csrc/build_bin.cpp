@@ -252,6 +252,7 @@ static void bin_mo_resolve(BinDev &B, const spmv_options_t &o, int64_t LL, int64
     if (B.mo && !o.bin_pad && !probe_env("SPMV_BIN_PADLOG")) B.pad_log = 3;
     B.mo_probe = 0;
     if (const char *e = probe_env("SPMV_BIN_MO_PROBE")) B.mo_probe = B.mo ? std::atoi(e) : 0;
+    if (B.mo_probe & 8) B.sum_u = 24;  // probe: 24-entry Sum batches (slot runs padded to 1536)
 }
 
 // ---- row bins: <= max_rows rows, cut at cumulative nnz targets; a multiple

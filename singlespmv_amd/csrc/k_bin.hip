@@ -527,8 +527,12 @@ struct SumTab {
 
 template <int U, int MODE>
 __device__ __forceinline__ void sum_mo_tab(SumTab<U, MODE> &T, int64_t sb, int lane, const int32_t *__restrict__ mtab) {
-    static_assert(U == 32, "one 16-byte table load per lane");
-    if constexpr ((MODE & 8192) != 0) {
+    static_assert(U == 32 || U == 24, "U/8 table words per lane");
+    if constexpr (U == 24) {  // probe (SPMV_BIN_MO_PROBE & 8): 3 words per lane
+        const int32_t *tp = mtab + (sb >> 3) + lane * 3;
+#pragma unroll
+        for (int h = 0; h < 3; ++h) T.t[h] = __builtin_nontemporal_load(tp + h);
+    } else if constexpr ((MODE & 8192) != 0) {
         const bin_u32x4 *tp = reinterpret_cast<const bin_u32x4 *>(mtab + (sb >> 3) + (lane >> 3) * U);
 #pragma unroll
         for (int q = 0; q < U / 4; ++q) {
@@ -694,10 +698,10 @@ __global__ __launch_bounds__(64 * W2) void bin_sum_bin_kernel(
     }
 }
 
-template <int W2, int MODE>
+template <int W2, int MODE, int U = 32>
 static void launch_sum_mo_t(const spmv_plan_s *p, double *y) {
     const BinDev &B = p->bin;
-    hipLaunchKernelGGL((bin_sum_bin_kernel<W2, 32, MODE, true>), dim3((unsigned)B.nwg2), dim3(64 * W2), 0,
+    hipLaunchKernelGGL((bin_sum_bin_kernel<W2, U, MODE, true>), dim3((unsigned)B.nwg2), dim3(64 * W2), 0,
                        p->stream, (int64_t)0, B.n_bins, B.n_bins, (int64_t)1, B.run_off, B.srun_off, B.bin_row0,
                        (int64_t)0, B.slot2, B.mtab, B.prod, y);
 }
@@ -707,6 +711,10 @@ static void launch_sum_mo(const spmv_plan_s *p, double *y) {
 #ifdef SPMV_PROBES
     if (p->bin.mo_probe & 2) {
         launch_sum_mo_t<W2, 512 | 8192>(p, y);
+        return;
+    }
+    if (p->bin.sum_u == 24) {  // probe: 24-entry batches (two batches within the 63 loads in flight)
+        launch_sum_mo_t<W2, 512, 24>(p, y);
         return;
     }
     if (launch_dbg(p->bin.dbg) & (1 << 25)) {  // ablation: contiguous product reads (wrong y)
