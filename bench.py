@@ -47,6 +47,7 @@ import time
 
 import numpy as np
 
+T_START = time.time()  # process start: the rank's setup time is measured from here
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
@@ -59,8 +60,20 @@ CONFIGS = {
     "c4": (dict(kind="banded", band_lo=-32, band_hi=31), "banded 20M rows, 64 diagonals", 20_000_000),
 }
 # the configs the N = 1 line carries beside the headline: (config, formats)
-EXTRA_CONFIGS = (("c3", ["auto"]), ("c4", ["auto", "csr"]))
+EXTRA_CONFIGS = (("c3", ["auto", "hyb", "csr", "ss"]), ("c4", ["auto", "csr", "ell"]))
 KFD_TOPOLOGY = "/sys/class/kfd/kfd/topology/nodes"
+
+
+def model_bytes(fmt: str, m: int, n: int, nnz: int, n_diags: int = 0) -> int:
+    """SURVEY §8(d) algorithmic bytes of one y = A x over an m x n rank shape
+    (x read once, y written once): DIA 8 nnz + 4 nDiag + 8 n + 8 m; every
+    other format is priced as CSR, 12 nnz + 4 (m + 1) + 8 n + 8 m (BASELINE.md
+    §3: 2.120 GB at config 2, 15.76 GB CSR / 10.56 GB DIA at config 4), so the
+    formats of one matrix share one byte model (the format's own model, e.g.
+    BIN's 12 nnz + 8 n + 8 m, is kept beside it as `format_bytes`)."""
+    if fmt == "dia":
+        return 8 * nnz + 4 * n_diags + 8 * n + 8 * m
+    return 12 * nnz + 4 * (m + 1) + 8 * n + 8 * m
 
 
 def streamed_bytes(info) -> dict:
@@ -129,12 +142,15 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--trials", type=int, default=5,
-                    help="timed trials of K steps; value = the fastest (src/main.cpp:58-102)")
+    ap.add_argument("--trials", type=int, default=10,
+                    help="timed trials of K steps of each config's headline plan; value = the fastest "
+                         "(src/main.cpp:58-102: min of 10); the other formats get 3")
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--rows", type=int, default=0, help="rows per GPU (default: the config's)")
-    ap.add_argument("--formats", default="auto,csr,ell,ss,css",
-                    help="first entry is the headline plan; the rest are reported alongside")
+    ap.add_argument("--formats", default=None,
+                    help="first entry is the headline plan; the rest are reported alongside "
+                         "(default: auto,csr,ell,ss,css at N = 1; auto,csr at N > 1, where every rank "
+                         "builds each format of its shard)")
     ap.add_argument("--only-config", action="store_true",
                     help="time --config alone (no configs 3 / 4 beside the N = 1 headline)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
@@ -303,9 +319,16 @@ RELEVANT = {"csr": ("csr_lanes",), "ss": ("ss_sigma",), "ell": ("ell_width",),
                     "bin_product_order", "bin_sum_entries")}
 
 
-def time_formats(ctx, args, M, fmts, trials_head: int):
+def host_rss_peak_gb() -> float:
+    import resource
+    return resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1e6  # KB -> GB
+
+
+def time_formats(ctx, args, M, fmts, trials_head: int, y_check=None, setup_mark=False):
     """Build and time each format on M; the first is the headline (kept, with
-    its y).  Returns (results, headline (plan, info, r) or None, y_head)."""
+    its y).  y_check(y) -> dict, if given, is applied to every format's y
+    (its max_rel_err_vs_cpu).  Returns (results, headline (plan, info, r) or
+    None, y_head)."""
     import singlespmv_amd as sp
     torch = ctx.torch
     y = torch.empty(M["rows"], dtype=torch.float64, device=ctx.dev)
@@ -331,8 +354,14 @@ def time_formats(ctx, args, M, fmts, trials_head: int):
         torch.cuda.synchronize()
         if args.warmup:
             plan.time(M["x"], y, args.warmup)
+        if setup_mark and fi == 0:
+            # the rank's setup (generation, x broadcast, headline plan build),
+            # measured up to its first timed trial (multi-GPU rehearsals)
+            free, total = torch.cuda.mem_get_info(ctx.dev)
+            M["setup"] = {"setup_s": time.time() - T_START, "peak_rss_gb": host_rss_peak_gb(),
+                          "device_used_gb": (total - free) / 1e9, "plan_device_gb": info["device_bytes"] / 1e9}
         trials = []  # (max-over-ranks wall s, this rank's event ms, this rank's wall s)
-        for _ in range(trials_head if fi == 0 else min(trials_head, 2)):
+        for _ in range(trials_head if fi == 0 else min(trials_head, 3)):
             torch.cuda.synchronize()
             if ctx.distributed:
                 ctx.dist.barrier()
@@ -347,6 +376,7 @@ def time_formats(ctx, args, M, fmts, trials_head: int):
             trials.append((wall_max, ev_ms, wall))
         wall_max, ev_ms, wall_own = min(trials)
         launch_s = ev_ms / 1e3 / args.steps
+        algo = model_bytes(info["format"], M["rows"], M["n"], M["nnz_local"], info.get("n_diags", 0))
         r = {
             "format": info["format"], "kernel": info["kernel"],
             "gflops": 2.0 * M["nnz_total"] * args.steps / wall_max / 1e9,
@@ -354,8 +384,8 @@ def time_formats(ctx, args, M, fmts, trials_head: int):
             "trials_ms_per_step": [round(t[0] / args.steps * 1e3, 5) for t in trials],
             "event_ms_per_launch": launch_s * 1e3,
             "own_wall_ms_per_step": wall_own / args.steps * 1e3,
-            "achieved_gbs": info["algo_bytes"] / launch_s / 1e9,
-            "algo_bytes": info["algo_bytes"], "stored_slots": info["stored_slots"],
+            "achieved_gbs": algo / launch_s / 1e9,
+            "algo_bytes": algo, "format_bytes": info["algo_bytes"], "stored_slots": info["stored_slots"],
             "device_bytes": info["device_bytes"], "plan_build_s": round(t_plan, 3),
             "n_kernels": info["n_kernels"], "placement": info["placement"],
         }
@@ -363,6 +393,13 @@ def time_formats(ctx, args, M, fmts, trials_head: int):
             r[k] = info[k]
         if info["n_kernels"] > 1:
             r["phases_ms"] = plan.profile(M["x"], y, 10)  # e.g. BIN Mul / Sum (opt_ss MulPerf / SumPerf)
+        tb, kind = lookup_traffic(M["config"], M["rows"], M["n"], info["kernel"])
+        if tb is not None:
+            r["traffic"], r["traffic_kind"] = tb, kind
+            r["traffic_over_algo"] = tb / algo
+        if y_check is not None:
+            torch.cuda.synchronize()
+            r.update(y_check(y))
         results[fmt if fmt not in results else f"{fmt}_{fi}"] = r
         if fi == 0:
             headline = (plan, info, r)
@@ -397,17 +434,23 @@ def extra_config(ctx, args, config: str, fmts, stream_gbs: float) -> dict:
     others beside it, roofline + PMC traffic, y against the CPU port."""
     import oracle
     M = build_matrix(ctx, args, config)
-    results, head, y_head = time_formats(ctx, args, M, fmts, trials_head=3)
-    if head is None:
-        return {"error": "no plan could be built", "details": results}
-    plan, info, r = head
-    plan.destroy()
+    # the CPU port's y first (untimed for the GPU): every format's y is
+    # checked against it right after that format's timed trials
     x_host = M["x"].cpu().numpy()
     tc = time.perf_counter()
     y_cpu = oracle.csr_spmv(M["rp"], M["col"], M["val"], x_host)
     t_cpu = time.perf_counter() - tc
-    ygpu = y_head.cpu().numpy()
-    max_rel = float(np.max(np.abs(ygpu - y_cpu) / np.maximum(np.abs(y_cpu), 1e-300)))
+    den = np.maximum(np.abs(y_cpu), 1e-300)
+
+    def y_check(y):
+        return {"max_rel_err_vs_cpu": float(np.max(np.abs(y.cpu().numpy() - y_cpu) / den))}
+
+    results, head, y_head = time_formats(ctx, args, M, fmts, trials_head=args.trials, y_check=y_check)
+    if head is None:
+        return {"error": "no plan could be built", "details": results}
+    plan, info, r = head
+    plan.destroy()
+    max_rel = r["max_rel_err_vs_cpu"]
     for fr in results.values():
         if "achieved_gbs" in fr:
             fr["frac_of_stream"] = fr["achieved_gbs"] / stream_gbs
@@ -459,8 +502,9 @@ def main():
     rows, n_glob, m_glob = M["rows"], M["n"], M["m"]
     nnz_local, nnz_total, x = M["nnz_local"], M["nnz_total"], M["x"]
 
-    fmts = [f for f in args.formats.split(",") if f]
-    results, headline, y_head = time_formats(ctx, args, M, fmts, args.trials)
+    fmts_arg = args.formats or ("auto,csr,ell,ss,css" if world == 1 else "auto,csr")
+    fmts = [f for f in fmts_arg.split(",") if f]
+    results, headline, y_head = time_formats(ctx, args, M, fmts, args.trials, setup_mark=True)
     if headline is None:
         if rank == 0:
             print(json.dumps({"error": "no plan could be built", "details": results}))
@@ -471,13 +515,20 @@ def main():
     per_rank = None
     if distributed:
         ph = r.get("phases_ms", {})
+        su = M.get("setup", {})
         rows_all = sdist.gather_floats([float(rank), float(M["row0"]), float(M["row1"]), float(nnz_local),
                                         r["own_wall_ms_per_step"], r["event_ms_per_launch"],
-                                        float(ph.get("mul", -1.0)), float(ph.get("sum", -1.0))], dev)
+                                        float(ph.get("mul", -1.0)), float(ph.get("sum", -1.0)),
+                                        su.get("setup_s", -1.0), su.get("peak_rss_gb", -1.0),
+                                        su.get("device_used_gb", -1.0), su.get("plan_device_gb", -1.0),
+                                        host_rss_peak_gb(), time.time() - T_START], dev)
         per_rank = [{"rank": int(v[0]), "rows": [int(v[1]), int(v[2])], "nnz": int(v[3]),
                      "wall_ms_per_step": v[4], "event_ms_per_launch": v[5],
                      "phases_ms": {"mul": v[6], "sum": v[7]} if v[6] >= 0 else None,
-                     "placement": info["placement"]} for v in rows_all]
+                     "placement": info["placement"],
+                     "setup_s_to_first_trial": v[8], "peak_rss_gb_at_first_trial": v[9],
+                     "device_used_gb_after_build": v[10], "headline_plan_device_gb": v[11],
+                     "peak_rss_gb": v[12], "elapsed_s": v[13]} for v in rows_all]
 
     # y gather (RCCL all_gather over xGMI), timed separately from the kernel
     # (slices padded to the longest rank's rows)
@@ -588,7 +639,7 @@ def main():
                          f"per call (src/main.cpp:58-102), {nthreads} threads = the host cores of this "
                          f"process's affinity",
                "ms_per_call": t_cpu * 1e3,
-               "gbs": (12 * nnz_local + 4 * (rows + 1) + 16 * rows) / t_cpu / 1e9,
+               "gbs": model_bytes("csr", rows, n_glob, nnz_local) / t_cpu / 1e9,
                "value_1thread": 2.0 * e1 / t_cpu1 / 1e9,
                "sample_1thread": f"first {r1} rows ({e1} nnz) of the same matrix, all of x, 1 thread, "
                                  f"same method ({loop1} calls per trial, min of 10)",

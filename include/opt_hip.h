@@ -10,7 +10,8 @@
  *
  * Format: the first of -DOPT_HIP_{CRS,ELL,SS,DIA,HYB,CSS,COO,JDS,BIN} that is defined
  * (default AUTO); the environment variable SPMV_HIP_FORMAT
- * (crs|ell|ss|dia|hyb|auto) overrides it at run time.
+ * (crs|csr|ell|ss|dia|hyb|css|coo|jds|bin|auto, case-insensitive; anything
+ * else means auto) overrides it at run time.
  *
  * x handling follows the reference: x_opt.val aliases the caller's x
  * (src/opt_crs.cpp:11-12) and SpMV uploads it on every call the way

@@ -120,12 +120,22 @@ typedef struct spmv_options {
     int32_t reserved[2];
 } spmv_options_t;
 
-/* Placement of the large scratch/value buffer of BIN and DIA plans (the BIN
- * product buffer, the DIA values).  The BIN Mul ran ~15 % slower with one
+/* Placement of the large buffers of a plan (the BIN product buffer, the DIA
+ * values, the streamed col / val arrays of CSR, ELL, HYB, JDS, SS, COO, CSS).  The BIN Mul ran ~15 % slower with one
  * plain hipMalloc on most plans than with the same buffer built from 2-MB
- * physical handles (DESIGN §4a "Placement, round 3"). */
-#define SPMV_PLACEMENT_AUTO 0   /* BIN products >= 32 MB, DIA values >= 256 MB: VMM;
-                                   everything else: PLAIN                         */
+ * physical handles (DESIGN §4a "Placement, round 3").
+ *
+ * Known limitation: placement is not fully under the library's control.  In
+ * a long-lived process that builds several large plans, about one plan in
+ * three lands in memory where the BIN Mul runs 15-23 % slower (and DIA at
+ * config 4 varies 1.48-1.54 ms), VMM or not; the first plan of a process has
+ * been fast on three boxes of four.  A caller who needs the best time should
+ * build its hot plan first (or rebuild a slow one); no API exposes the
+ * placement the hardware picked (profiles/round3/probe/
+ * mulorder_plans_arena_vmm_n8.jsonl). */
+#define SPMV_PLACEMENT_AUTO 0   /* BIN products >= 32 MB, DIA values >= 256 MB and
+                                   the streamed arrays (col / val / slots) of the
+                                   other formats >= 256 MB: VMM; the rest PLAIN  */
 #define SPMV_PLACEMENT_PLAIN 1  /* one hipMalloc                                     */
 #define SPMV_PLACEMENT_SEARCH 2 /* experiment (probe build only; the product library
                                    returns SPMV_ERROR_NOT_SUPPORTED): up to 8

@@ -120,9 +120,15 @@ def lib():
         raise SpmvError(f"{LIB_PATH} missing: run `make` (or __graft_entry__.build()) first; "
                         "there is no CPU fallback")
     L = C.CDLL(LIB_PATH)
-    # the ctypes structs below mirror version 2 of include/spmv_hip.h
-    if L.spmv_api_version() != API_VERSION:
-        raise SpmvError(f"{LIB_PATH} implements C-ABI version {L.spmv_api_version()}, this mirror {API_VERSION}")
+    # the ctypes structs below mirror version API_VERSION of include/spmv_hip.h
+    ver_fn = getattr(L, "spmv_api_version", None)
+    if ver_fn is None:
+        raise SpmvError(f"{LIB_PATH} exports no spmv_api_version (built before C-ABI version {API_VERSION}): "
+                        "rebuild it with `make`")
+    ver_fn.argtypes = []
+    ver_fn.restype = C.c_int32
+    if ver_fn() != API_VERSION:
+        raise SpmvError(f"{LIB_PATH} implements C-ABI version {ver_fn()}, this mirror {API_VERSION}")
     vp, i32, i64, f64 = C.c_void_p, C.c_int32, C.c_int64, C.c_double
     L.spmv_options_default.argtypes = [C.POINTER(Options)]
     L.spmv_plan_create_coo.argtypes = [i32, i32, i32, vp, vp, vp, C.POINTER(Options), C.POINTER(vp)]

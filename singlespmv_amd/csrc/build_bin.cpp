@@ -128,16 +128,18 @@ static int bin_params(spmv_plan_s *p, const spmv_options_t &o, int64_t m, int64_
         const int w = std::atoi(e);
         B.sum_waves = w == 2 || w == 4 ? w : 8;
     }
-    // product order: Mul order unless the caller asks for the Sum's (resolved
-    // against the layout in bin_mo_resolve)
+    // probe build: one product buffer re-used per row group (read here, before
+    // bin_mo_resolve, which needs it)
+    if (const char *e = probe_env("SPMV_BIN_REUSE")) B.reuse = std::atoi(e) != 0;
+    // product order: the caller's bin_product_order; AUTO resolves it in
+    // bin_mo_resolve (Mul order for segments of < kBinMulOrderMaxSeg expected
+    // entries, when the layout allows it)
     SPMV_CHECK_ARG(o.bin_product_order >= SPMV_BIN_ORDER_AUTO && o.bin_product_order <= SPMV_BIN_ORDER_MUL,
                    "bin_product_order must be 0, 1 or 2");
     B.order_req = o.bin_product_order;
     if (const char *e = probe_env("SPMV_BIN_ORDER")) B.order_req = std::atoi(e);
     B.max_rows = bin_max_rows(B.sum_waves);
     B.sum_u = B.sum_waves == 8 ? 8 : 32;  // must match launch_sum's <W2, U> pairs
-    B.slot_linear = false;
-    if (const char *e = probe_env("SPMV_BIN_SLOT_LINEAR")) B.slot_linear = std::atoi(e) != 0;
     p->algo_bytes = 12 * nnz + 8 * n + 8 * m;
     p->n_kernels = 2;
     p->kernel_name = "bin_mul_kernel+bin_sum_kernel";
@@ -247,12 +249,8 @@ constexpr double kBinMulOrderMaxSeg = 112.0;
 static void bin_mo_resolve(BinDev &B, const spmv_options_t &o, int64_t LL, int64_t nnz) {
     const bool want = B.order_req == SPMV_BIN_ORDER_MUL ||
                       (B.order_req == SPMV_BIN_ORDER_AUTO && B.seg_est < kBinMulOrderMaxSeg);
-    B.mo = want && LL == 0 && o.bin_groups <= 1 && !B.reuse && !B.slot_linear &&
-           B.sum_u == 32 && nnz + kBinProdSlack < ((int64_t)1 << 31);
+    B.mo = want && LL == 0 && o.bin_groups <= 1 && !B.reuse && B.sum_u == 32 && nnz + kBinProdSlack < ((int64_t)1 << 31);
     if (B.mo && !o.bin_pad && !probe_env("SPMV_BIN_PADLOG")) B.pad_log = 3;
-    B.mo_probe = 0;
-    if (const char *e = probe_env("SPMV_BIN_MO_PROBE")) B.mo_probe = B.mo ? std::atoi(e) : 0;
-    if (B.mo_probe & 8) B.sum_u = 24;  // probe: 24-entry Sum batches (slot runs padded to 1536)
 }
 
 // ---- row bins: <= max_rows rows, cut at cumulative nnz targets; a multiple
@@ -333,7 +331,6 @@ static void bin_offsets(spmv_plan_s *p, const spmv_options_t &o, BinLayout &L) {
     int G = o.bin_groups > 0 ? o.bin_groups : 1;
     if (G > NB) G = (int)NB;
     B.G = G;
-    if (const char *e = probe_env("SPMV_BIN_REUSE")) B.reuse = std::atoi(e) != 0;
     B.g_bin.assign((size_t)G + 1, NB);
     B.g_prod.assign((size_t)G + 1, E);
     B.g_bin[0] = 0;
@@ -392,7 +389,7 @@ static void bin_offsets(spmv_plan_s *p, const spmv_options_t &o, BinLayout &L) {
     }
     // slot runs: the same runs, each padded to whole Sum batches
     {
-        const int64_t step = B.slot_linear ? 1 : 64 * (int64_t)B.sum_u;
+        const int64_t step = 64 * (int64_t)B.sum_u;
         L.srun_off.assign(L.run_off.size(), 0);
         int64_t sc = 0;
         for (size_t r = 0; r + 1 < L.run_off.size(); ++r) {
@@ -431,7 +428,7 @@ static void bin_offsets(spmv_plan_s *p, const spmv_options_t &o, BinLayout &L) {
                 const int64_t b = L.mul_bins[(size_t)(g0 + j)];
                 L.off1[(size_t)(b * S + t)] = cur;
                 // Mul-ordered products: the Mul's segments are not padded
-                cur += B.mo && !(B.mo_probe & 1) ? L.cnt[(size_t)(b * S + t)] : L.rpad(L.cnt[(size_t)(b * S + t)]);
+                cur += B.mo ? L.cnt[(size_t)(b * S + t)] : L.rpad(L.cnt[(size_t)(b * S + t)]);
             }
             if (L.LL > 0) {  // G == 1: void up to a 64-entry boundary, then the long blocks
                 cur = (cur + 63) & ~(int64_t)63;
@@ -477,7 +474,7 @@ static void bin_mo_table(const BinDev &B, const BinLayout &L, std::vector<int32_
             const int64_t c = L.cnt[(size_t)(b * S + t)];
             for (int64_t k = 0; k < c; k += 8) {
                 const int64_t rel = o2 + k - r0, i = rel / step, w = rel - i * step;
-                const int64_t at = (B.mo_probe & 2) ? bin_mo_tab_at_grouped(w >> 3, (int)U) : bin_mo_tab_at(w >> 3, (int)U);
+                const int64_t at = bin_mo_tab_at(w >> 3, (int)U);
                 tab[(size_t)((s0 + i * step) / 8 + at)] = (int32_t)(o1 + k);
             }
         }
@@ -510,7 +507,7 @@ static void bin_fill_arrays(const BinDev &B, const HostCsr &A, const BinLayout &
             // slot index of product position q of strip t's segment (its run: block t / SB)
             auto sidx = [&](int64_t t, int64_t q) {
                 const size_t run = (size_t)((t / L.SB) * NB + b);
-                return (size_t)bin_slot_index(q, L.run_off[run], L.srun_off[run], B.slot_linear ? 0 : B.sum_u);
+                return (size_t)bin_slot_index(q, L.run_off[run], L.srun_off[run], B.sum_u);
             };
             const int32_t *row0 = L.row0.data();
             segbase[0] = 0;
@@ -552,7 +549,7 @@ static void bin_fill_arrays(const BinDev &B, const HostCsr &A, const BinLayout &
             for (int64_t s = 0; s < S; ++s) {
                 const int64_t n0 = L.cnt[(size_t)(b * S + s)], n8 = L.rpad(n0);
                 for (int64_t k = n0; k < n8; ++k) {
-                    if (!B.mo || (B.mo_probe & 1)) {
+                    if (!B.mo) {
                         val1[(size_t)(o1[s] + k)] = 0.0;
                         cs1[(size_t)(o1[s] + k)] = 0;
                     }
@@ -589,7 +586,7 @@ static void bin_fill_arrays(const BinDev &B, const HostCsr &A, const BinLayout &
                         ++pos;
                     }
                     const size_t run = (size_t)(NBK * NB + b);
-                    slot2[(size_t)bin_slot_index(pos, L.run_off[run], L.srun_off[run], B.slot_linear ? 0 : B.sum_u)] =
+                    slot2[(size_t)bin_slot_index(pos, L.run_off[run], L.srun_off[run], B.sum_u)] =
                         (uint16_t)(r - L.row0[(size_t)b]);
                 }
                 const bool end = p2 + 1 == nt || long_starts(L, b0, p2 + 1);

@@ -17,6 +17,19 @@ static thread_local std::string g_err;
 void set_error(const std::string &msg) { g_err = msg; }
 const char *last_error() { return g_err.c_str(); }
 
+// Placement of the streamed arrays of the row-parallel formats (CSR, ELL,
+// HYB, JDS, SS, COO, CSS; BIN and DIA place their large buffer themselves):
+// AUTO maps every array of >= kStreamVmmMinBytes into 2-MB VMM handles
+// (config 4, same launches on both placements, interleaved in one process:
+// CSR 2.95 -> 2.81 ms, ELL 2.57 -> 2.40; profiles/round4/probe/
+// c4_csr_ell_launch_variants.jsonl), VMM does so from 32 MB, PLAIN never.
+static void stream_placement(spmv_plan_s *p, int fmt, const spmv_options_t &o) {
+    if (fmt == SPMV_FORMAT_BIN || fmt == SPMV_FORMAT_DIA) return;
+    if (o.placement == SPMV_PLACEMENT_AUTO) p->arena.vmm_min = kStreamVmmMinBytes;
+    else if (o.placement == SPMV_PLACEMENT_VMM) p->arena.vmm_min = kBinVmmMinBytes;
+    if (const char *e = probe_env("SPMV_ARENA_VMM_MB")) p->arena.vmm_min = (size_t)std::max(0, std::atoi(e)) << 20;
+}
+
 static int check_device(int device) {
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess || count == 0) {
@@ -87,6 +100,7 @@ static int create_from_csr(const HostCsr &A, const spmv_options_t *opt_in, spmv_
     p->n = A.n;
     p->nnz = A.nnz;
     int fmt = o.format == SPMV_FORMAT_AUTO ? choose_format(A, o) : o.format;
+    stream_placement(p, fmt, o);
     int st;
     switch (fmt) {
         case SPMV_FORMAT_CSR: st = build_csr(p, A, o); break;
@@ -219,6 +233,7 @@ int spmv_plan_create_csr_device(int64_t m, int64_t n, int64_t nnz, const int64_t
         p->m = m;
         p->n = n;
         p->nnz = nnz;
+        stream_placement(p, o.format, o);
         const double mean = m ? (double)nnz / (double)m : 0.0;
         int st;
         switch (o.format) {
@@ -649,6 +664,8 @@ int spmv_plan_info(spmv_plan_t p, spmv_plan_info_t *info) {
     } else if (p->format == SPMV_FORMAT_DIA) {
         info->placement = p->dia.placement;
         pm = &p->dia.placement_ms;
+    } else {
+        info->placement = p->arena.maps.empty() ? SPMV_PLACEMENT_PLAIN : SPMV_PLACEMENT_VMM;
     }
     if (pm && !pm->empty()) {
         info->placement_candidates = (int32_t)pm->size();

@@ -45,6 +45,39 @@ __device__ __forceinline__ double group_sum(double v) {
     return v;
 }
 
+// 64-bit DPP move (two 32-bit v_mov_dpp).  Lanes the control does not feed
+// (or rows outside ROWMASK) read 0.
+template <int CTRL, int ROWMASK = 0xF>
+__device__ __forceinline__ double dpp_f64(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, ROWMASK, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, ROWMASK, 0xF, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+// group_sum<G> with the offsets below 16 taken by DPP instead of ds_bpermute,
+// bit-identical to group_sum<G> (same pairs, same order; IEEE addition is
+// commutative, so v + v[i ^ o] is the same sum in both lanes of a pair):
+// offset 8 is the row rotation by 8 (lane i reads (i + 8) mod 16 = i ^ 8);
+// offset 4 the row rotation by 4, which reads a lane holding v[i ^ 4] once
+// the offset-8 step has made every row 8-periodic (G >= 16; for G = 8 it
+// stays a ds_bpermute); offsets 2 and 1 are the quad permutations
+// [2,3,0,1] and [1,0,3,2], exactly i ^ 2 and i ^ 1.
+template <int G>
+__device__ __forceinline__ double group_sum_dpp(double v) {
+#pragma unroll
+    for (int o = G / 2; o >= 16; o >>= 1) v = __dadd_rn(v, __shfl_xor(v, o, 64));
+    if constexpr (G >= 16) {
+        v = __dadd_rn(v, dpp_f64<0x128>(v));  // row_ror:8
+        v = __dadd_rn(v, dpp_f64<0x124>(v));  // row_ror:4
+    } else if constexpr (G == 8) {
+        v = __dadd_rn(v, __shfl_xor(v, 4, 64));
+    }
+    if constexpr (G >= 4) v = __dadd_rn(v, dpp_f64<0x4E>(v));  // quad_perm [2,3,0,1]
+    if constexpr (G >= 2) v = __dadd_rn(v, dpp_f64<0xB1>(v));  // quad_perm [1,0,3,2]
+    return v;
+}
+
 // Inclusive prefix sum of an int across the 64-lane wave (Hillis-Steele).
 __device__ __forceinline__ int wave_inclusive_sum(int v, int lane) {
 #pragma unroll

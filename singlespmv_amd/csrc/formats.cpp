@@ -230,6 +230,13 @@ static void csr_bin_rows(const int64_t *row_ptr, int64_t m, std::vector<int32_t>
 // (then that L serves every row, no row list), keeps per-bin row lists.
 int csr_plan_lanes(spmv_plan_s *p, const int64_t *row_ptr, int64_t m, const spmv_options_t &o) {
     CsrDev &c = p->csr;
+    // 32-bit offsets of the slab kernel: the widest 64-row slab (+ one chunk
+    // of 64 lanes' overreach) in bytes of val < 2^31, and x below 4 GB
+    int64_t slab_max = 0;
+#pragma omp parallel for schedule(static) reduction(max : slab_max)
+    for (int64_t r = 0; r < m; r += 64)
+        slab_max = std::max<int64_t>(slab_max, row_ptr[std::min<int64_t>(r + 64, m)] - row_ptr[r]);
+    c.off32 = slab_max + 512 < ((int64_t)1 << 28) && p->n < ((int64_t)1 << 29);
     if (o.csr_lanes > 0) {
         c.lanes = o.csr_lanes;
         if (c.lanes < 1 || c.lanes > 64 || (c.lanes & (c.lanes - 1))) {
@@ -427,7 +434,7 @@ int build_jds(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
     p->stored_slots = ell_slots + p->hyb.nnz;
     p->algo_bytes = 12 * A.nnz + 8 * A.n + 8 * A.m + 4 * A.m + 12 * p->hyb.n_rows;
     p->n_kernels = p->hyb.n_rows ? 2 : 1;
-    p->kernel_name = "ell_slice_kernel<perm>";
+    p->kernel_name = p->hyb.n_rows ? "ell_slice_kernel<perm>+csr_adaptive_kernel" : "ell_slice_kernel<perm>";
     return SPMV_SUCCESS;
 }
 
@@ -491,7 +498,8 @@ int build_hyb(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
     p->stored_slots = ell_slots + h.nnz;
     p->algo_bytes = 12 * A.nnz + 8 * A.n + 8 * A.m + 12 * h.n_rows;
     p->n_kernels = h.n_rows ? 2 : 1;
-    p->kernel_name = "ell_slice_kernel";
+    // every kernel of one execute ("a+b": the PMC traffic of an execute sums them)
+    p->kernel_name = h.n_rows ? "ell_slice_kernel+csr_adaptive_kernel" : "ell_slice_kernel";
     return SPMV_SUCCESS;
 }
 
@@ -562,7 +570,7 @@ int build_ss(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
     p->empty_rows = s.n_empty;
     p->algo_bytes = 12 * A.nnz + 8 * A.n + 8 * A.m;
     p->n_kernels = 2;
-    p->kernel_name = "ss_tile_kernel<" + std::to_string(s.sigma) + ">";
+    p->kernel_name = "ss_tile_kernel<" + std::to_string(s.sigma) + ">+ss_fixup_kernel";
     return SPMV_SUCCESS;
 }
 

@@ -84,6 +84,7 @@ constexpr size_t kVmmChunk = (size_t)2 << 20;          // physical handle size
 constexpr size_t kVmmAlign = (size_t)1 << 30;          // VA alignment of the mapping
 constexpr size_t kBinVmmMinBytes = (size_t)32 << 20;   // AUTO: VMM from this product-buffer size
 constexpr size_t kDiaVmmMinBytes = (size_t)256 << 20;  // AUTO: VMM from this DIA value size
+constexpr size_t kStreamVmmMinBytes = (size_t)256 << 20;  // AUTO: VMM from this array size (CSR, ELL, ...)
 
 // ---- device memory owned by a plan --------------------------------------
 // Plain hipMalloc allocations, plus buffers mapped through the HIP virtual
@@ -128,6 +129,8 @@ struct CsrDev {
     int32_t *col = nullptr;   // [nnz + kPad]
     double *val = nullptr;    // [nnz + kPad]
     int lanes = 4;            // lanes per row (1..64); 0 = adaptive (bins)
+    bool off32 = false;       // every 64-row slab spans < 2^28 entries and n < 2^29:
+                              // 32-bit byte offsets in csr_slab2 (k_csr.hip)
     int32_t *bin_rows = nullptr;        // rows of every bin, ascending within a bin
     int64_t bin_off[kCsrBins + 1] = {};  // host: bin b = bin_rows[bin_off[b], bin_off[b+1])
 };
@@ -282,7 +285,6 @@ inline int bin_max_rows(int w2) { return kBinLdsDoubles / w2 - 1; }
 // lane reads its U slots as U/8 16-byte loads, each load instruction of the
 // wave covering 1 KB contiguously.
 __host__ __device__ inline int64_t bin_slot_index(int64_t e, int64_t r0, int64_t s0, int U) {
-    if (U == 0) return s0 + (e - r0);  // linear (ablation)
     const int64_t rel = e - r0, step = 64 * (int64_t)U;
     const int64_t i = rel / step, w = rel - i * step;
     const int64_t u = w >> 6, lane = w & 63;
@@ -299,9 +301,6 @@ __host__ __device__ inline int64_t bin_slot_index(int64_t e, int64_t r0, int64_t
 // so a lane loads its U/8 words at once and ds_bpermute hands chunk c to the
 // 8 lanes reading it.
 __host__ __device__ inline int64_t bin_mo_tab_at(int64_t c, int U) { return (c & 63) * (U / 8) + (c >> 6); }
-// probe variant (mo_probe & 2): lane group g = l/8 reads its U bases (chunks
-// 8u + g) as U/4 16-byte loads, no ds_bpermute
-__host__ __device__ inline int64_t bin_mo_tab_at_grouped(int64_t c, int U) { return (c & 7) * U + (c >> 3); }
 // The Sum reads whole batches of 64*U products without clamping at a run's
 // end (the padded slot batches send those lanes to the dummy slot), so the
 // product buffer carries one batch of slack past its last run.
@@ -331,15 +330,12 @@ struct BinDev {
     int order_req = 0;             // spmv_options_t.bin_product_order (SPMV_BIN_ORDER_*)
     double seg_est = 0;            // expected entries per (bin, strip) segment (bin_params)
     bool mo = false;               // products in Mul order (SPMV_BIN_ORDER_MUL, bin_mo_tab_at)
-    int mo_probe = 0;              // probe build (SPMV_BIN_MO_PROBE): 1 Mul order padded like the Sum's
-                                   // (64-B aligned chunks), 2 per-lane chunk tables (no ds_bpermute)
     int32_t *mtab = nullptr;       // mo: [ES / 8] Mul position of every 8-entry Sum chunk
     uint16_t *slot2 = nullptr;
     int64_t n_blocks = 1;         // strip blocks of the product layout
     int64_t *run_off = nullptr;   // [n_blocks*n_bins + 1]: run (blk, b) of bin b's products
     int64_t *srun_off = nullptr;  // [n_blocks*n_bins + 1]: its slots (runs padded to 64*sum_u)
     int sum_u = 32;               // Sum entries per lane per batch (the slot layout's U)
-    bool slot_linear = false;     // ablation: slots in product order (sum_u layout unused)
     int64_t strip_block = 0;      // strips per block (SB)
     int32_t *bin_row0 = nullptr;  // [n_bins + 1]
     double *prod = nullptr;       // product buffer (largest group)

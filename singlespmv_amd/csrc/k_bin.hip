@@ -60,14 +60,17 @@ struct MulBatch {
     int32_t d[U];
 };
 
-// LONG: blocks at or past `ls` (the strip's long blocks, 64-aligned) load
-// their lcode word instead of the segment destination.
+// MODE bits of the Mul (all give the same y): 1 nontemporal product stores
+// (Sum-ordered products), 4 products in Mul order (BinDev::mo: prod[e], no
+// destinations), 256 x strips by LDS-DMA.  PL: segments padded to 2^PL
+// entries.  LONG: blocks at or past `ls` (the strip's long blocks,
+// 64-aligned) load their lcode word instead of the segment destination.
 template <int U, int PL, int MODE, bool LONG>
 __device__ __forceinline__ void mul_load(MulBatch<U> &B, int64_t base, int64_t e0, int64_t e1, int lane,
                                          const double *__restrict__ val1, const uint16_t *__restrict__ cs1,
                                          const int32_t *__restrict__ dst1, int64_t ls, int64_t lsh,
                                          const int32_t *__restrict__ lcode) {
-    if constexpr ((MODE & 64) == 0 && !LONG) {
+    if constexpr (!LONG) {
         // lanes past the piece load the next entries unclamped (the arrays
         // carry kBinMulSlack; their stores are masked): one base address per
         // array, the u offsets are immediates (64 entries = 64 >> PL groups).
@@ -75,49 +78,31 @@ __device__ __forceinline__ void mul_load(MulBatch<U> &B, int64_t base, int64_t e
         const double *vb = val1 + base + lane;
         const uint16_t *cb = cs1 + base + lane;
         const int32_t *db = dst1 + ((base + lane) >> PL);
-        uint32_t cw[4] = {0, 0, 0, 0};
-        if constexpr ((MODE & 32768) != 0) {
-            // ablation (probe, wrong y): the batch's 1 KB of columns as ONE
-            // 16-byte load per lane (what an 8-entry lane-grouped cs1 would load)
-            static_assert(U == 8, "8 columns per 16-byte load");
-            const bin_u32x4 t = __builtin_nontemporal_load(reinterpret_cast<const bin_u32x4 *>(cs1 + base) + lane);
-            cw[0] = t[0], cw[1] = t[1], cw[2] = t[2], cw[3] = t[3];
-        }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             B.v[u] = ld_stream(vb + u * 64);
-            if constexpr ((MODE & 32768) != 0) B.c[u] = (cw[(u >> 1) & 3] >> (16 * (u & 1))) & 16383;
-            else B.c[u] = (MODE & 8) ? (uint32_t)(((base + u * 64 + lane) * 2654435761u) & 16383)
-                                : (uint32_t)__builtin_nontemporal_load(cb + u * 64);
-            // a lane past the piece (e >= e1, masked at the store) reads word 0:
-            // its e may lie beyond the strip's long blocks
-            const int64_t e = base + u * 64 + lane;
-            if (LONG && base + u * 64 >= ls) B.d[u] = ld_stream(lcode + (e < e1 ? e + lsh : 0));
-            else if constexpr ((MODE & 4) == 0) B.d[u] = ld_stream(db + u * (64 >> PL));
+            B.c[u] = (uint32_t)__builtin_nontemporal_load(cb + u * 64);
+            if constexpr ((MODE & 4) == 0) B.d[u] = ld_stream(db + u * (64 >> PL));
         }
         (void)e0;
+        (void)e1;
+        (void)ls;
+        (void)lsh;
+        (void)lcode;
         (void)db;
-    } else {  // LONG, or MODE 64 (A/B): every load clamped at the piece's end
+    } else {  // every load clamped at the piece's end
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int64_t e = base + u * 64 + lane;
             const int64_t ee = e < e1 ? e : e0;
             B.v[u] = ld_stream(val1 + ee);
-            B.c[u] = (MODE & 8) ? (uint32_t)((ee * 2654435761u) & 16383) : (uint32_t)__builtin_nontemporal_load(cs1 + ee);
-            if (LONG && base + u * 64 >= ls) B.d[u] = ld_stream(lcode + (e < e1 ? e + lsh : 0));
+            B.c[u] = (uint32_t)__builtin_nontemporal_load(cs1 + ee);
+            // a lane past the piece (e >= e1, masked at the store) reads word 0:
+            // its e may lie beyond the strip's long blocks
+            if (base + u * 64 >= ls) B.d[u] = ld_stream(lcode + (e < e1 ? e + lsh : 0));
             else if constexpr ((MODE & 4) == 0) B.d[u] = ld_stream(dst1 + (ee >> PL));
         }
     }
-}
-
-// 64-bit DPP move (two 32-bit v_mov_dpp): lanes the control does not feed
-// (or rows outside ROWMASK) read 0
-template <int CTRL, int ROWMASK>
-__device__ __forceinline__ double dpp_f64(double v) {
-    const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, ROWMASK, 0xF, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, ROWMASK, 0xF, false);
-    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 
 // One 64-entry long block: inclusive segmented scan of the products over the
@@ -126,7 +111,6 @@ __device__ __forceinline__ double dpp_f64(double v) {
 // 1/2/4/8 inside each 16-lane row, then row_bcast15 (rows 1, 3) and
 // row_bcast31 (rows 2, 3) -- so a partial is deterministic; a lane adds a
 // source only from its own piece (source lane >= the piece's first lane).
-template <int MODE>
 __device__ __forceinline__ void mul_long_block(double pr, int32_t code, bool ok, int lane,
                                                double *__restrict__ prod) {
     const bool start = code < 0 || !ok;
@@ -152,43 +136,29 @@ __device__ __forceinline__ void mul_long_block(double pr, int32_t code, bool ok,
     // neighbouring pieces of its (bin, strip), written by the next lanes or
     // the next block -- kept in L2 they merge into whole lines.  Nontemporal
     // partial stores cost the Mul that follows a Sum 0.111 -> 0.137 ms at
-    // config 3 (profiles/round2/probe/c3_long_store.jsonl).  MODE 16 / 32
-    // (probe ablations): nontemporal partial stores / none (wrong sums).
-    if ((MODE & 32) == 0 && ok && pos != 0x7FFFFFFF) {
-        if (MODE & 16) __builtin_nontemporal_store(v, prod + pos);
-        else prod[pos] = v;
-    }
+    // config 3 (profiles/round2/probe/c3_long_store.jsonl).
+    if (ok && pos != 0x7FFFFFFF) prod[pos] = v;
 }
 
 template <int U, int MODE, int PL, bool LONG>
 __device__ __forceinline__ void mul_store(const MulBatch<U> &B, int64_t base, int64_t e1, int lane,
-                                          const double *xs, double *__restrict__ prod, int64_t ls,
-                                          bool nt_tail = false) {
+                                          const double *xs, double *__restrict__ prod, int64_t ls) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const int64_t e = base + u * 64 + lane;
         if (LONG && base + u * 64 >= ls) {
-            mul_long_block<MODE>(__dmul_rn(B.v[u], xs[B.c[u]]), B.d[u], e < e1, lane, prod);
+            mul_long_block(__dmul_rn(B.v[u], xs[B.c[u]]), B.d[u], e < e1, lane, prod);
         } else if (e < e1) {
             const double pr = __dmul_rn(B.v[u], xs[B.c[u]]);
             // MODE 4: products in Mul order (BinDev::mo: contiguous, no
             // destinations) instead of the Sum order's segments
             double *dp = (MODE & 4) ? prod + e : prod + ((int64_t)B.d[u] << PL) + (e & ((1 << PL) - 1));
-            if (MODE & 2) {
-                if (pr == 1.2345e300) *dp = pr;
-            } else if ((MODE & 1) || ((MODE & 65536) && nt_tail)) {
-                __builtin_nontemporal_store(pr, dp);
-            } else {
-                *dp = pr;
-            }
+            if (MODE & 1) __builtin_nontemporal_store(pr, dp);
+            else *dp = pr;
         }
     }
 }
 
-// MODE: 1 nontemporal product stores, 4 products in Mul order (BinDev::mo;
-// on a Sum-ordered plan an ablation with wrong results), 256 x strips by
-// LDS-DMA; probe ablations: 2 no product stores (value kept alive), 8 no cs1
-// loads, 512 no x staging.  PL: segments padded to 2^PL entries.
 template <int U, int MODE, int PL, bool LONG>
 __global__ __launch_bounds__(kBinMulThreads) void bin_mul_kernel(
     const int64_t *__restrict__ piece_off, int64_t q_base, const int32_t *__restrict__ piece_strip,
@@ -206,13 +176,7 @@ __global__ __launch_bounds__(kBinMulThreads) void bin_mul_kernel(
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const int64_t q0 = piece_off[q_base + blockIdx.x], q1 = piece_off[q_base + blockIdx.x + 1];
-    for (int64_t qq = q0; qq < q1; ++qq) {
-        // MODE 131072 (probe A/B): each workgroup starts at a different one
-        // of its pieces (breaks the lockstep of the workgroups' streams)
-        const int64_t q = (MODE & 131072) ? q0 + (qq - q0 + blockIdx.x) % (q1 - q0) : qq;
-        // MODE 65536 (probe A/B): ordinary product stores for the first 70 %
-        // of the workgroup's pieces, nontemporal for the rest
-        const bool nt_tail = (MODE & 65536) && (qq - q0) * 10 >= (q1 - q0) * 7;
+    for (int64_t q = q0; q < q1; ++q) {
         // consecutive pieces of a workgroup are consecutive strips: stage x
         const int32_t st = piece_strip[q];
         const int64_t c0 = (int64_t)st * strip;
@@ -225,20 +189,22 @@ __global__ __launch_bounds__(kBinMulThreads) void bin_mul_kernel(
         // instead of 20); else, and always with long rows (their run path's
         // live registers would spill), one load per round trip
         constexpr int XL = 8;
-        if constexpr ((MODE & 512) != 0) {
-            // ablation (probe, wrong results): no x strip loads -- the cost of
-            // staging x, in the Mul's time
-        } else if constexpr ((MODE & 256) != 0) {
+        if constexpr ((MODE & 256) != 0) {
             // LDS-DMA (global_load_lds_dwordx4): each wave instruction copies
             // 1 KB of x straight into the strip, no VGPRs, all in flight at
-            // once (the barrier below waits for them); the launch checks that
-            // x + c0 is 16-byte aligned.  The tail past whole KB: plain loads.
+            // once; the launch checks that x + c0 is 16-byte aligned.  The
+            // tail past whole KB: plain loads.
             const int full = cw & ~127;
             for (int k = w; k * 128 < full; k += NW)
                 __builtin_amdgcn_global_load_lds(
                     (const __attribute__((address_space(1))) void *)(x + c0 + k * 128 + lane * 2),
                     (__attribute__((address_space(3))) void *)(xs + k * 128), 16, 0, 0);
             for (int i = full + threadIdx.x; i < cw; i += kBinMulThreads) xs[i] = x[c0 + i];
+            // other waves read these LDS bytes after the barrier: every DMA
+            // load of this wave must have landed first (vmcnt(0); expcnt and
+            // lgkmcnt left at their maxima), whatever the compiler's barrier
+            // lowering does (the CK block_sync_lds_direct_load idiom)
+            __builtin_amdgcn_s_waitcnt(0x0F70);
         } else if (LONG || !xburst) {
             for (int i = threadIdx.x; i < cw; i += kBinMulThreads) xs[i] = x[c0 + i];
         } else for (int i0 = threadIdx.x; i0 < cw; i0 += XL * kBinMulThreads) {
@@ -263,113 +229,67 @@ __global__ __launch_bounds__(kBinMulThreads) void bin_mul_kernel(
         for (int64_t it = 0; it < nit; it += 2) {
             const int64_t ba = bat(it), bb = bat(it + 1);
             if (it + 1 < nit) mul_load<U, PL, MODE, LONG>(B, bb, e0, e1, lane, val1, cs1, dst1, ls, lsh, lcode);
-            mul_store<U, MODE, PL, LONG>(A, ba, e1, lane, xs, prod, ls, nt_tail);
+            mul_store<U, MODE, PL, LONG>(A, ba, e1, lane, xs, prod, ls);
             if (it + 1 < nit) {
                 if (it + 2 < nit)
                     mul_load<U, PL, MODE, LONG>(A, bat(it + 2), e0, e1, lane, val1, cs1, dst1, ls, lsh, lcode);
-                mul_store<U, MODE, PL, LONG>(B, bb, e1, lane, xs, prod, ls, nt_tail);
+                mul_store<U, MODE, PL, LONG>(B, bb, e1, lane, xs, prod, ls);
             }
         }
     }
 }
 
-template <int U, int MODE>
+// two 16-bit row slots per word, unpacked at the add
+template <int U>
 struct SumBatch {
     double v[U];
-    // two 16-bit row slots per word, unpacked at the add (MODE 8: one per word)
-    uint32_t w[(MODE & 8) ? U : U / 2];
-    __device__ __forceinline__ uint32_t slot(int u) const {
-        if constexpr ((MODE & 8) != 0) return w[u];
-        else return (w[u >> 1] >> (16 * (u & 1))) & 0xFFFFu;
-    }
+    uint32_t w[U / 2];
+    __device__ __forceinline__ uint32_t slot(int u) const { return (w[u >> 1] >> (16 * (u & 1))) & 0xFFFFu; }
 };
 
 // sbase: the batch's slot block (bin_slot_index): this lane's slots u..u+7
-// are one 16-byte word, the wave's word q one contiguous KB
-template <int U, int MODE>
-__device__ __forceinline__ void sum_load(SumBatch<U, MODE> &B, int64_t base, int64_t p0, int64_t p1, int lane,
-                                         int64_t pbase, int64_t sbase, const uint16_t *__restrict__ slot2,
-                                         const double *__restrict__ prod) {
+// are one 16-byte word, the wave's word q one contiguous KB.  The whole batch
+// is loaded unclamped: lanes past the run's end read the next run's products
+// (or the buffer's slack, kBinProdSlack) and their slots -- the padding of
+// the batch's slot block -- are the dummy slot, so nothing but +x reaches a
+// real row.  One base address, the u offsets are immediates: no per-entry
+// clamp or 64-bit address math.  Products nontemporal (config 2 Sum 0.308 ->
+// 0.298 ms, neutral at config 3 and the N = 8 shape,
+// profiles/round1/probe/bin_sum_nt_loads.jsonl).
+template <int U>
+__device__ __forceinline__ void sum_load(SumBatch<U> &B, int64_t base, int lane, int64_t pbase, int64_t sbase,
+                                         const uint16_t *__restrict__ slot2, const double *__restrict__ prod) {
     static_assert(U % 8 == 0, "slots are read 8 per 16-byte load");
     // slots first: the adds consume slot word q before product u >= 8q, and
     // loads complete in issue order
-    if constexpr ((MODE & 8) != 0) {  // ablation: slots in product order, one 2-byte load per entry
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int64_t e = base + u * 64 + lane;
-            B.w[u] = (uint32_t)__builtin_nontemporal_load(slot2 + sbase + (e < p1 ? e : p0) - base);
-        }
-    }
     const bin_u32x4 *sp = reinterpret_cast<const bin_u32x4 *>(slot2 + sbase + (int64_t)lane * 8);
 #pragma unroll
-    for (int q = 0; q < ((MODE & 12) ? 0 : U / 8); ++q) {
+    for (int q = 0; q < U / 8; ++q) {
         const bin_u32x4 w = __builtin_nontemporal_load(sp + q * 64);
 #pragma unroll
         for (int h = 0; h < 4; ++h) B.w[4 * q + h] = w[h];
     }
-    if constexpr ((MODE & 16) != 0) {
-        // ablation (wrong sums): the same bytes as 16-byte loads, lane l
-        // reading products 2l, 2l+1 of each 128-entry block
+    const double *pp = prod + (base - pbase) + lane;
 #pragma unroll
-        for (int u = 0; u < U; u += 2) {
-            const int64_t e = base + (u / 2) * 128 + 2 * lane;
-            const int64_t ee = e + 1 < p1 ? e : p0;
-            const f64x2 v = ld_stream2(prod + (ee - pbase));
-            B.v[u] = v.x;
-            B.v[u + 1] = v.y;
-        }
-    } else if constexpr ((MODE & 40) != 0) {  // slot-linear ablation / 32: the clamped loads (A/B)
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int64_t e = base + u * 64 + lane;
-            const int64_t ee = e < p1 ? e : p0;
-            B.v[u] = (MODE & 1) ? ld_stream(prod + (ee - pbase)) : prod[ee - pbase];
-        }
-    } else {
-        // the whole batch, unclamped: lanes past the run's end read the next
-        // run's products (or the buffer's slack, kBinProdSlack) and their
-        // slots -- the padding of the batch's slot block -- are the dummy
-        // slot, so nothing but +x reaches a real row.  One base address, the
-        // u offsets are immediates: no per-entry clamp or 64-bit address math.
-        const double *pp = prod + (base - pbase) + lane;
-#pragma unroll
-        for (int u = 0; u < U; ++u) B.v[u] = (MODE & 1) ? ld_stream(pp + u * 64) : pp[u * 64];
-    }
-    if ((MODE & 12) == 4) {
-#pragma unroll
-        for (int u = 0; u < U / 2; ++u) B.w[u] = (uint32_t)(((base + u * 64 + lane) * 2654435761u) % 4096u);
-    }
+    for (int u = 0; u < U; ++u) B.v[u] = ld_stream(pp + u * 64);
 }
 
-template <int U, int MODE, int DUMMY>
-__device__ __forceinline__ void sum_add(const SumBatch<U, MODE> &B, int64_t base, int64_t p1, int lane, double *ys,
-                                        double &sink) {
+template <int U>
+__device__ __forceinline__ void sum_add(const SumBatch<U> &B, double *ys) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-        // lanes past the run read the padding of the slot block: the dummy slot
-        if (MODE & 2) {
-            sink += B.v[u] * (double)B.slot(u);
-        } else if constexpr ((MODE & 40) != 0) {  // slot-linear ablation / clamped A/B: mask here
-            const bool ok = base + u * 64 + lane < p1;
-            atomicAdd(&ys[ok ? B.slot(u) : DUMMY], ok ? B.v[u] : 0.0);
-        } else {
-            atomicAdd(&ys[B.slot(u)], B.v[u]);  // past the run: the dummy slot
-        }
-    }
+    for (int u = 0; u < U; ++u) atomicAdd(&ys[B.slot(u)], B.v[u]);  // past the run: the dummy slot
 }
 
-// MODE (internal ablations): 1 nontemporal product loads (the default), 2 no LDS atomics,
-// 4 no slot loads, 32 product loads clamped at the run's end (the round-2 loads, A/B),
-// 128 no LDS zeroing / y write-back, 256 one bin at a time (A/B: the loads of a
-// bin's first batch wait for the previous bin's y write-back), 512 nontemporal
-// y stores (the default, with 1; y is not re-read by the kernel).  W2 waves per
-// workgroup, each owning a slice of kBinLdsDoubles / W2 doubles.  A bin's
-// products are NBK runs (one per strip block, run_off[blk*nbins + b]); the
-// batches walk them in order (a batch never crosses a run), ping-ponged so one
-// batch is always in flight -- across the wave's bins too: the next bin's
-// first batches are already loading while the finished bin's y is written
-// from LDS (its write-back and the loads overlap instead of alternating).
-template <int W2, int U, int MODE>
+// The Sum of Sum-ordered products.  W2 waves per workgroup, each owning a
+// slice of kBinLdsDoubles / W2 doubles.  A bin's products are NBK runs (one
+// per strip block, run_off[blk*nbins + b]); the batches walk them in order
+// (a batch never crosses a run), ping-ponged so one batch is always in
+// flight -- across the wave's bins too: the next bin's first batches are
+// already loading while the finished bin's y is written from LDS (its
+// write-back and the loads overlap instead of alternating).  y leaves with
+// nontemporal stores (not re-read by the kernel: config 2 Sum 0.302 -> 0.292
+// ms, N = 8 shape 0.318 -> 0.308, profiles/round2/probe/sum_nt_y_*.jsonl).
+template <int W2, int U>
 __global__ __launch_bounds__(64 * W2) void bin_sum_kernel(
     int64_t b0, int64_t b1, int64_t nbins, int64_t nblk, const int64_t *__restrict__ run_off,
     const int64_t *__restrict__ srun_off, const int32_t *__restrict__ bin_row0, int64_t pbase,
@@ -385,128 +305,75 @@ __global__ __launch_bounds__(64 * W2) void bin_sum_kernel(
     const int lane = threadIdx.x & 63;
     double *ys = ylds + w * SLICE;
     const int64_t bfirst = b0 + (int64_t)blockIdx.x * W2 + w, bstride = (int64_t)gridDim.x * W2;
-    if constexpr ((MODE & (2 | 128 | 256)) != 0) {
-        for (int64_t b = bfirst; b < b1; b += bstride) {
-            const int64_t r0 = bin_row0[b];
-            const int rows = (int)(bin_row0[b + 1] - r0);
-            if ((MODE & 128) == 0)  // 128 (ablation): no LDS zeroing / y write-back
-                for (int i = lane; i < rows; i += 64) ys[i] = 0.0;
-            double sink = 0.0;
-            // run cursor: batch = [pos, min(pos + STEP, end)) of run k
-            // run k of bin b: products from rs, slots from ss (batch-aligned)
-            int64_t k = 0, pos = run_off[b], end = run_off[b + 1], rs = pos, ss = srun_off[b];
-            auto next = [&](int64_t &lo, int64_t &hi, int64_t &sb) -> bool {
-                while (pos >= end) {
-                    if (++k >= nblk) return false;
-                    pos = rs = run_off[k * nbins + b];
-                    end = run_off[k * nbins + b + 1];
-                    ss = srun_off[k * nbins + b];
-                }
-                lo = pos;
-                hi = pos + STEP < end ? pos + STEP : end;
-                sb = ss + (lo - rs);
-                pos = hi;
-                return true;
-            };
-            SumBatch<U, MODE> A, B;
-            int64_t alo, ahi, asb, blo, bhi, bsb;
-            bool has_a = next(alo, ahi, asb);
-            if (has_a) sum_load<U, MODE>(A, alo, alo, ahi, lane, pbase, asb, slot2, prod);
-            while (has_a) {
-                const bool has_b = next(blo, bhi, bsb);
-                if (has_b) sum_load<U, MODE>(B, blo, blo, bhi, lane, pbase, bsb, slot2, prod);
-                sum_add<U, MODE, SLICE - 1>(A, alo, ahi, lane, ys, sink);
-                if (!has_b) break;
-                has_a = next(alo, ahi, asb);
-                if (has_a) sum_load<U, MODE>(A, alo, alo, ahi, lane, pbase, asb, slot2, prod);
-                sum_add<U, MODE, SLICE - 1>(B, blo, bhi, lane, ys, sink);
+    if (bfirst >= b1) return;
+    // one cursor over all of the wave's bins: bin cb, its run k, the
+    // batch [pos, min(pos + STEP, end)); products from rs, slots from ss
+    int64_t cb = bfirst, k = 0, pos = run_off[cb], end = run_off[cb + 1], rs = pos, ss = srun_off[cb];
+    auto next = [&](int64_t &lo, int64_t &sb, int64_t &bb) -> bool {
+        while (pos >= end) {
+            if (++k >= nblk) {  // bin cb exhausted: the wave's next bin
+                cb += bstride;
+                if (cb >= b1) return false;
+                k = 0;
+                pos = rs = run_off[cb];
+                end = run_off[cb + 1];
+                ss = srun_off[cb];
+                continue;
             }
-            if ((MODE & 2) && sink == 1.2345e300) ys[0] = sink;
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            if ((MODE & 128) == 0)
-                for (int i = lane; i < rows; i += 64) y[r0 + i] = ys[i];
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            pos = rs = run_off[k * nbins + cb];
+            end = run_off[k * nbins + cb + 1];
+            ss = srun_off[k * nbins + cb];
         }
-    } else {
-        if (bfirst >= b1) return;
-        // one cursor over all of the wave's bins: bin cb, its run k, the
-        // batch [pos, min(pos + STEP, end)); products from rs, slots from ss
-        int64_t cb = bfirst, k = 0, pos = run_off[cb], end = run_off[cb + 1], rs = pos, ss = srun_off[cb];
-        auto next = [&](int64_t &lo, int64_t &hi, int64_t &sb, int64_t &bb) -> bool {
-            while (pos >= end) {
-                if (++k >= nblk) {  // bin cb exhausted: the wave's next bin
-                    cb += bstride;
-                    if (cb >= b1) return false;
-                    k = 0;
-                    pos = rs = run_off[cb];
-                    end = run_off[cb + 1];
-                    ss = srun_off[cb];
-                    continue;
-                }
-                pos = rs = run_off[k * nbins + cb];
-                end = run_off[k * nbins + cb + 1];
-                ss = srun_off[k * nbins + cb];
-            }
-            lo = pos;
-            hi = pos + STEP < end ? pos + STEP : end;
-            sb = ss + (lo - rs);
-            bb = cb;
-            pos = hi;
-            return true;
-        };
-        // acc: the bin in the LDS slice; done: the wave's first bin whose y
-        // is not written yet (bins without products get zeros)
-        int64_t acc = -1, done = bfirst;
-        auto write_zero = [&](int64_t bz) {
-            const int64_t r0 = bin_row0[bz];
-            const int rows = (int)(bin_row0[bz + 1] - r0);
-            for (int i = lane; i < rows; i += 64) {
-                if constexpr ((MODE & 512) != 0) __builtin_nontemporal_store(0.0, y + r0 + i);
-                else y[r0 + i] = 0.0;
-            }
-        };
-        auto finish = [&]() {  // the slice's bin: LDS adds done -> y
-            const int64_t r0 = bin_row0[acc];
-            const int rows = (int)(bin_row0[acc + 1] - r0);
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            for (int i = lane; i < rows; i += 64) {
-                if constexpr ((MODE & 512) != 0) __builtin_nontemporal_store(ys[i], y + r0 + i);
-                else y[r0 + i] = ys[i];
-            }
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            done = acc + bstride;
-        };
-        auto begin = [&](int64_t nb) {  // the next batch belongs to bin nb
-            if (nb == acc) return;
-            if (acc >= 0) finish();
-            for (; done < nb; done += bstride) write_zero(done);
-            const int rows = (int)(bin_row0[nb + 1] - bin_row0[nb]);
-            for (int i = lane; i < rows; i += 64) ys[i] = 0.0;
-            acc = nb;
-            done = nb + bstride;
-        };
-        double sink = 0.0;
-        SumBatch<U, MODE> A, B;
-        int64_t alo, ahi, asb, ab, blo, bhi, bsb, bbn;
-        bool has_a = next(alo, ahi, asb, ab);
-        if (has_a) sum_load<U, MODE>(A, alo, alo, ahi, lane, pbase, asb, slot2, prod);
-        while (has_a) {
-            const bool has_b = next(blo, bhi, bsb, bbn);
-            if (has_b) sum_load<U, MODE>(B, blo, blo, bhi, lane, pbase, bsb, slot2, prod);
-            begin(ab);
-            sum_add<U, MODE, SLICE - 1>(A, alo, ahi, lane, ys, sink);
-            if (!has_b) break;
-            has_a = next(alo, ahi, asb, ab);
-            if (has_a) sum_load<U, MODE>(A, alo, alo, ahi, lane, pbase, asb, slot2, prod);
-            begin(bbn);
-            sum_add<U, MODE, SLICE - 1>(B, blo, bhi, lane, ys, sink);
-        }
+        lo = pos;
+        sb = ss + (lo - rs);
+        bb = cb;
+        pos = pos + STEP < end ? pos + STEP : end;
+        return true;
+    };
+    // acc: the bin in the LDS slice; done: the wave's first bin whose y
+    // is not written yet (bins without products get zeros)
+    int64_t acc = -1, done = bfirst;
+    auto write_zero = [&](int64_t bz) {
+        const int64_t r0 = bin_row0[bz];
+        const int rows = (int)(bin_row0[bz + 1] - r0);
+        for (int i = lane; i < rows; i += 64) __builtin_nontemporal_store(0.0, y + r0 + i);
+    };
+    auto finish = [&]() {  // the slice's bin: LDS adds done -> y
+        const int64_t r0 = bin_row0[acc];
+        const int rows = (int)(bin_row0[acc + 1] - r0);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        for (int i = lane; i < rows; i += 64) __builtin_nontemporal_store(ys[i], y + r0 + i);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        done = acc + bstride;
+    };
+    auto begin = [&](int64_t nb) {  // the next batch belongs to bin nb
+        if (nb == acc) return;
         if (acc >= 0) finish();
-        for (; done < b1; done += bstride) write_zero(done);
+        for (; done < nb; done += bstride) write_zero(done);
+        const int rows = (int)(bin_row0[nb + 1] - bin_row0[nb]);
+        for (int i = lane; i < rows; i += 64) ys[i] = 0.0;
+        acc = nb;
+        done = nb + bstride;
+    };
+    SumBatch<U> A, B;
+    int64_t alo, asb, ab, blo, bsb, bbn;
+    bool has_a = next(alo, asb, ab);
+    if (has_a) sum_load<U>(A, alo, lane, pbase, asb, slot2, prod);
+    while (has_a) {
+        const bool has_b = next(blo, bsb, bbn);
+        if (has_b) sum_load<U>(B, blo, lane, pbase, bsb, slot2, prod);
+        begin(ab);
+        sum_add<U>(A, ys);
+        if (!has_b) break;
+        has_a = next(alo, asb, ab);
+        if (has_a) sum_load<U>(A, alo, lane, pbase, asb, slot2, prod);
+        begin(bbn);
+        sum_add<U>(B, ys);
     }
+    if (acc >= 0) finish();
+    for (; done < b1; done += bstride) write_zero(done);
 }
 
-// Mul-ordered plans (BinDev::mo) take every variant with MODE 4
 // ---- Mul-ordered products (BinDev::mo, internal.hpp bin_mo_tab_at) -------
 // The Sum's walk is bin_sum_kernel's (one cursor over a wave's bins, the next
 // batch loading while the current one is added, y written per bin), but a
@@ -517,38 +384,26 @@ __global__ __launch_bounds__(64 * W2) void bin_sum_kernel(
 // 64 B.  The table is loaded one batch ahead of the products it addresses,
 // so waiting for it never drains the batch of products in flight (loads
 // complete in issue order).
-// MODE 8192 (probe, mo_probe 2): per-lane tables (bin_mo_tab_at_grouped),
-// U words per lane, no ds_bpermute; MODE 2048 (probe ablation, wrong y): the
-// table and ds_bpermute as usual, but the products read contiguously
-template <int U, int MODE>
+template <int U>
 struct SumTab {
-    int32_t t[(MODE & 8192) ? U : U / 8];
+    int32_t t[U / 8];
 };
 
-template <int U, int MODE>
-__device__ __forceinline__ void sum_mo_tab(SumTab<U, MODE> &T, int64_t sb, int lane, const int32_t *__restrict__ mtab) {
-    static_assert(U == 32 || U == 24, "U/8 table words per lane");
-    if constexpr (U == 24) {  // probe (SPMV_BIN_MO_PROBE & 8): 3 words per lane
-        const int32_t *tp = mtab + (sb >> 3) + lane * 3;
+template <int U>
+__device__ __forceinline__ void sum_mo_tab(SumTab<U> &T, int64_t sb, int lane, const int32_t *__restrict__ mtab) {
+    static_assert(U == 32, "U/8 = 4 table words per lane: one 16-byte load");
+    const bin_u32x4 w = __builtin_nontemporal_load(reinterpret_cast<const bin_u32x4 *>(mtab + (sb >> 3)) + lane);
 #pragma unroll
-        for (int h = 0; h < 3; ++h) T.t[h] = __builtin_nontemporal_load(tp + h);
-    } else if constexpr ((MODE & 8192) != 0) {
-        const bin_u32x4 *tp = reinterpret_cast<const bin_u32x4 *>(mtab + (sb >> 3) + (lane >> 3) * U);
-#pragma unroll
-        for (int q = 0; q < U / 4; ++q) {
-            const bin_u32x4 w = __builtin_nontemporal_load(tp + q);
-#pragma unroll
-            for (int h = 0; h < 4; ++h) T.t[4 * q + h] = (int32_t)w[h];
-        }
-    } else {
-        const bin_u32x4 w = __builtin_nontemporal_load(reinterpret_cast<const bin_u32x4 *>(mtab + (sb >> 3)) + lane);
-#pragma unroll
-        for (int h = 0; h < 4; ++h) T.t[h] = (int32_t)w[h];
-    }
+    for (int h = 0; h < 4; ++h) T.t[h] = (int32_t)w[h];
 }
 
-template <int U, int MODE>
-__device__ __forceinline__ void sum_mo_load(SumBatch<U, MODE> &B, const SumTab<U, MODE> &T, int64_t sb, int lane,
+// ordinary (cached) product loads: a chunk's 64 B start at any 8-byte
+// offset, so most chunks share a 128-B line with the next one -- kept in L2
+// it is read from HBM once.  Nontemporal loads (the Sum order's choice) cost
+// the rank shape's Sum 0.310 -> 0.342 ms on the same plan
+// (profiles/round3/probe/mulorder_store_load_policy_*.jsonl)
+template <int U>
+__device__ __forceinline__ void sum_mo_load(SumBatch<U> &B, const SumTab<U> &T, int64_t sb, int lane,
                                             const uint16_t *__restrict__ slot2, const double *__restrict__ prod) {
     const bin_u32x4 *sp = reinterpret_cast<const bin_u32x4 *>(slot2 + sb + (int64_t)lane * 8);
 #pragma unroll
@@ -558,73 +413,51 @@ __device__ __forceinline__ void sum_mo_load(SumBatch<U, MODE> &B, const SumTab<U
         for (int h = 0; h < 4; ++h) B.w[4 * q + h] = w[h];
     }
     const double *pl = prod + (lane & 7);
-    if constexpr ((MODE & 8192) != 0) {
+    // all U bases first, then the U loads: a load right behind its own
+    // ds_bpermute waits out the LDS latency, U times per batch
+    int c[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) B.v[u] = (MODE & 1) ? ld_stream(pl + T.t[u]) : pl[T.t[u]];
-    } else {
-        // all U bases first, then the U loads: a load right behind its own
-        // ds_bpermute waits out the LDS latency, U times per batch
-        int c[U];
+    for (int u = 0; u < U; ++u) c[u] = __builtin_amdgcn_ds_bpermute((((u & 7) << 3) + (lane >> 3)) << 2, T.t[u >> 3]);
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int u = 0; u < U; ++u) c[u] = __builtin_amdgcn_ds_bpermute((((u & 7) << 3) + (lane >> 3)) << 2, T.t[u >> 3]);
-        if constexpr ((MODE & 16384) == 0) __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            if constexpr ((MODE & 2048) != 0) B.v[u] = ld_stream(prod + (sb >> 1) + u * 64 + lane + (c[u] >> 31));
-            else if constexpr ((MODE & 1) == 0) B.v[u] = pl[c[u]];  // the default (launch_sum_mo)
-            else B.v[u] = ld_stream(pl + c[u]);
-        }
-    }
+    for (int u = 0; u < U; ++u) B.v[u] = pl[c[u]];
 }
 
-// ---- the Sum with its pipeline kept inside one bin --------------------------
-// (the Mul-ordered Sum, and the Sum order's A/B against bin_sum_kernel's flat
-// walk).  LLVM's s_waitcnt insertion is conservative around vector stores
-// issued in a loop of unknown trip count (the flat walk writes a finished
+// ---- the Mul-ordered Sum: its pipeline kept inside one bin ---------------
+// LLVM's s_waitcnt insertion is conservative around vector stores issued in
+// a loop of unknown trip count (bin_sum_kernel's flat walk writes a finished
 // bin's y and the zeros of empty bins inside its batch loop) and around
-// conditionally issued loads: the ISA of the flat walks waits for vmcnt(0)
-// (or a few) before a batch's adds or table reads, draining the batch in
-// flight.  Here each bin's batch loop issues its loads unconditionally (the
-// batches past the bin's end re-load its last batch and are dropped) and
-// stores nothing, so its waits count only its own pipeline; the bin's y is
-// written after the loop, while the next bin's first batches already load
-// (the loop's batches past its bin's end are the next bin's).  A bin's
-// batches walk its runs in order (run 0: its segments; with long rows run 1:
-// its pieces; at most two runs).
-template <int W2, int U, int MODE, bool MO>
+// conditionally issued loads: the ISA of such a walk waits for vmcnt(0) (or a
+// few) before a batch's adds or table reads, draining the batch in flight.
+// Here each bin's batch loop issues its loads unconditionally (the batches
+// past the bin's end re-load its last batch and are dropped) and stores
+// nothing, so its waits count only its own pipeline; the bin's y is written
+// after the loop, while the next bin's first batches already load (the
+// loop's batches past its bin's end are the next bin's).  Mul-ordered plans
+// have no long rows (build_bin.cpp bin_mo_resolve): one run per bin.
+template <int W2, int U>
 __global__ __launch_bounds__(64 * W2) void bin_sum_bin_kernel(
-    int64_t b0, int64_t b1, int64_t nbins, int64_t nblk, const int64_t *__restrict__ run_off,
-    const int64_t *__restrict__ srun_off, const int32_t *__restrict__ bin_row0, int64_t pbase,
-    const uint16_t *__restrict__ slot2, const int32_t *__restrict__ mtab, const double *__restrict__ prod,
-    double *__restrict__ y) {
+    int64_t b0, int64_t b1, const int64_t *__restrict__ run_off, const int64_t *__restrict__ srun_off,
+    const int32_t *__restrict__ bin_row0, const uint16_t *__restrict__ slot2, const int32_t *__restrict__ mtab,
+    const double *__restrict__ prod, double *__restrict__ y) {
     constexpr int SLICE = kBinLdsDoubles / W2;
     constexpr int64_t STEP = 64 * U;
     __shared__ double ylds[kBinLdsDoubles];
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     double *ys = ylds + w * SLICE;
-    double sink = 0.0;
-    // a bin's rows and runs (run 0: its segments; with long rows run 1: its
-    // pieces), batch j's slot block and product base
+    // a bin's rows, its batch count and batch j's slot block
     struct BinRun {
-        int64_t r0 = 0, nb = 0, n0 = 0, rs0 = 0, ss0 = 0, rs1 = 0, ss1 = 0;
+        int64_t r0 = 0, nb = 0, ss0 = 0;
         int rows = 0;
-        __device__ int64_t s(int64_t j) const { return j < n0 ? ss0 + j * STEP : ss1 + (j - n0) * STEP; }
-        __device__ int64_t p(int64_t j) const { return j < n0 ? rs0 + j * STEP : rs1 + (j - n0) * STEP; }
+        __device__ int64_t s(int64_t j) const { return ss0 + j * STEP; }
     };
     auto bin_at = [&](int64_t b) {
         BinRun R;
         R.r0 = bin_row0[b];
         R.rows = (int)(bin_row0[b + 1] - R.r0);
-        R.rs0 = run_off[b];
         R.ss0 = srun_off[b];
-        R.n0 = (run_off[b + 1] - R.rs0 + STEP - 1) / STEP;
-        R.nb = R.n0;
-        if (!MO && nblk > 1) {
-            R.rs1 = run_off[nbins + b];
-            R.ss1 = srun_off[nbins + b];
-            R.nb += (run_off[nbins + b + 1] - R.rs1 + STEP - 1) / STEP;
-        }
+        R.nb = (run_off[b + 1] - run_off[b] + STEP - 1) / STEP;
         return R;
     };
     const int64_t bstride = (int64_t)gridDim.x * W2;
@@ -632,8 +465,8 @@ __global__ __launch_bounds__(64 * W2) void bin_sum_bin_kernel(
     if (b >= b1) return;
     BinRun R = bin_at(b);
     for (int i = lane; i < R.rows; i += 64) ys[i] = 0.0;
-    SumBatch<U, MODE> PA, PB;
-    SumTab<U, MODE> TA, TB;
+    SumBatch<U> PA, PB;
+    SumTab<U> TA, TB;
     bool pre = false;  // R's batch 0 (PA) and batch 1's table (TB) are in flight
     for (;;) {
         const int64_t bn = b + bstride;
@@ -646,46 +479,32 @@ __global__ __launch_bounds__(64 * W2) void bin_sum_bin_kernel(
             if (j < R.nb) return R.s(j);
             return pfn ? N.s(j - R.nb < N.nb ? j - R.nb : N.nb - 1) : R.s(R.nb - 1);
         };
-        auto pbat = [&](int64_t j) -> int64_t {
-            if (j < R.nb) return R.p(j);
-            return pfn ? N.p(j - R.nb < N.nb ? j - R.nb : N.nb - 1) : R.p(R.nb - 1);
-        };
-        auto load = [&](SumBatch<U, MODE> &P, const SumTab<U, MODE> &T, int64_t j) {
-            if constexpr (MO) sum_mo_load<U, MODE>(P, T, sbat(j), lane, slot2, prod);
-            else sum_load<U, MODE>(P, pbat(j), 0, 0, lane, pbase, sbat(j), slot2, prod);
-        };
         bool swapped = false;
         if (R.nb > 0) {
             if (!pre) {
-                if constexpr (MO) {
-                    sum_mo_tab<U, MODE>(TA, sbat(0), lane, mtab);
-                    sum_mo_tab<U, MODE>(TB, sbat(1), lane, mtab);
-                }
-                load(PA, TA, 0);
+                sum_mo_tab<U>(TA, sbat(0), lane, mtab);
+                sum_mo_tab<U>(TB, sbat(1), lane, mtab);
+                sum_mo_load<U>(PA, TA, sbat(0), lane, slot2, prod);
             }
             for (int64_t j = 0;; j += 2) {
                 // batch j (PA) is added while j+1's products (table TB) and
                 // j+2's table (into TA: PA's loads are issued) are in flight
-                if constexpr (MO) sum_mo_tab<U, MODE>(TA, sbat(j + 2), lane, mtab);
-                load(PB, TB, j + 1);
-                sum_add<U, MODE, SLICE - 1>(PA, 0, 0, lane, ys, sink);
+                sum_mo_tab<U>(TA, sbat(j + 2), lane, mtab);
+                sum_mo_load<U>(PB, TB, sbat(j + 1), lane, slot2, prod);
+                sum_add<U>(PA, ys);
                 if (j + 1 >= R.nb) {
                     swapped = true;  // the next bin's batch 0 is in PB, its batch 1's table in TA
                     break;
                 }
-                if constexpr (MO) sum_mo_tab<U, MODE>(TB, sbat(j + 3), lane, mtab);
-                load(PA, TA, j + 2);
-                sum_add<U, MODE, SLICE - 1>(PB, 0, 0, lane, ys, sink);
+                sum_mo_tab<U>(TB, sbat(j + 3), lane, mtab);
+                sum_mo_load<U>(PA, TA, sbat(j + 2), lane, slot2, prod);
+                sum_add<U>(PB, ys);
                 if (j + 2 >= R.nb) break;
             }
         }
         pre = R.nb > 0 && pfn;
-        if ((MODE & 2) && sink == 1.2345e300) ys[0] = sink;
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        for (int i = lane; i < R.rows; i += 64) {
-            if constexpr ((MODE & 512) != 0) __builtin_nontemporal_store(ys[i], y + R.r0 + i);
-            else y[R.r0 + i] = ys[i];
-        }
+        for (int i = lane; i < R.rows; i += 64) __builtin_nontemporal_store(ys[i], y + R.r0 + i);
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         if (!more) break;
         for (int i = lane; i < N.rows; i += 64) ys[i] = 0.0;
@@ -698,50 +517,15 @@ __global__ __launch_bounds__(64 * W2) void bin_sum_bin_kernel(
     }
 }
 
-template <int W2, int MODE, int U = 32>
-static void launch_sum_mo_t(const spmv_plan_s *p, double *y) {
-    const BinDev &B = p->bin;
-    hipLaunchKernelGGL((bin_sum_bin_kernel<W2, U, MODE, true>), dim3((unsigned)B.nwg2), dim3(64 * W2), 0,
-                       p->stream, (int64_t)0, B.n_bins, B.n_bins, (int64_t)1, B.run_off, B.srun_off, B.bin_row0,
-                       (int64_t)0, B.slot2, B.mtab, B.prod, y);
-}
-
 template <int W2>
 static void launch_sum_mo(const spmv_plan_s *p, double *y) {
-#ifdef SPMV_PROBES
-    if (p->bin.mo_probe & 2) {
-        launch_sum_mo_t<W2, 512 | 8192>(p, y);
-        return;
-    }
-    if (p->bin.sum_u == 24) {  // probe: 24-entry batches (two batches within the 63 loads in flight)
-        launch_sum_mo_t<W2, 512, 24>(p, y);
-        return;
-    }
-    if (launch_dbg(p->bin.dbg) & (1 << 25)) {  // ablation: contiguous product reads (wrong y)
-        launch_sum_mo_t<W2, 512 | 2048>(p, y);
-        return;
-    }
-    if (launch_dbg(p->bin.dbg) & (1 << 30)) {  // A/B: nontemporal product loads
-        launch_sum_mo_t<W2, 1 | 512>(p, y);
-        return;
-    }
-    if (launch_dbg(p->bin.dbg) & (1 << 27)) {  // A/B: bases and loads interleaved by the scheduler
-        launch_sum_mo_t<W2, 512 | 16384>(p, y);
-        return;
-    }
-#endif
-    // ordinary (cached) product loads: a chunk's 64 B start at any 8-byte
-    // offset, so most chunks share a 128-B line with the next one -- kept in
-    // L2 it is read from HBM once.  Nontemporal loads (the Sum order's
-    // choice) cost the rank shape's Sum 0.310 -> 0.342 ms on the same plan
-    // (profiles/round3/probe/mulorder_store_load_policy_*.jsonl)
-    launch_sum_mo_t<W2, 512>(p, y);
+    const BinDev &B = p->bin;
+    hipLaunchKernelGGL((bin_sum_bin_kernel<W2, 32>), dim3((unsigned)B.nwg2), dim3(64 * W2), 0, p->stream,
+                       (int64_t)0, B.n_bins, B.run_off, B.srun_off, B.bin_row0, B.slot2, B.mtab, B.prod, y);
 }
 
 template <int MODE, int PL, int U = 8>
-static void launch_mul_t(const spmv_plan_s *p, int g, const double *x);
-template <int MODE, int PL, int U = 8>
-static void launch_mul_tt(const spmv_plan_s *p, int g, const double *x) {
+static void launch_mul_t(const spmv_plan_s *p, int g, const double *x) {
     const BinDev &B = p->bin;
     if (B.long_len > 0)
         hipLaunchKernelGGL((bin_mul_kernel<U, MODE, PL, true>), dim3((unsigned)B.nwg1), dim3(kBinMulThreads), 0,
@@ -754,71 +538,29 @@ static void launch_mul_tt(const spmv_plan_s *p, int g, const double *x) {
                            B.val1, B.cs1, B.dst1, x, p->n, (int32_t)B.strip, B.prod, nullptr, nullptr, nullptr,
                            B.xburst);
 }
-template <int MODE, int PL, int U>
-static void launch_mul_t(const spmv_plan_s *p, int g, const double *x) {
-    if (p->bin.mo) launch_mul_tt<MODE | 4, PL, U>(p, g, x);
-    else launch_mul_tt<MODE, PL, U>(p, g, x);
-}
 
 template <int PL>
 static void launch_mul_p(const spmv_plan_s *p, int g, const double *x) {
-    // default: nontemporal stores (measured 0.81 -> 0.71 ms at config 2,
-    // profiles/round1/probe/bin_probe_c2.jsonl), x strips staged by LDS-DMA
-    // wherever x + c0 is 16-byte aligned (MODE 256: config 2 Mul 0.536 ->
+    // Sum-ordered products: nontemporal stores (measured 0.81 -> 0.71 ms at
+    // config 2, profiles/round1/probe/bin_probe_c2.jsonl).  Mul-ordered
+    // products (BinDev::mo): ordinary stores -- the contiguous write streams
+    // of all workgroups ran the rank shape's Mul at 0.593-0.660 instead of
+    // 0.642-0.733 ms on two boxes, the Sum after them (cached loads)
+    // 0.307-0.310 -> 0.346-0.363: execute 0.944 -> 0.933 and 1.039 -> 1.017
+    // ms (profiles/round3/probe/mulorder_store_load_policy_*).  x strips by
+    // LDS-DMA wherever x + c0 is 16-byte aligned (config 2 Mul 0.536 ->
     // 0.520 ms, N = 8 rank shape 0.738 -> 0.717, config 3 -1 %, same plans,
-    // profiles/round3/probe/mul_glds_*.jsonl), else through registers.  The
-    // ablation MODEs exist only in the probe build (SPMV_BIN_DEBUG bits 0-1,
-    // -DSPMV_PROBES).
-    // Mul-ordered products (BinDev::mo) are stored with ordinary stores: the
-    // contiguous write streams of all workgroups ran the rank shape's Mul at
-    // 0.593-0.660 instead of 0.642-0.733 ms on two boxes, the Sum after
-    // them (cached loads) 0.307-0.310 -> 0.346-0.363: execute 0.944 -> 0.933
-    // and 1.039 -> 1.017 ms (profiles/round3/probe/mulorder_store_load_policy_*).
-    const bool dma = (reinterpret_cast<uintptr_t>(x) & 15) == 0 && p->bin.strip % 2 == 0;
-    const bool mo = p->bin.mo;
-#ifndef SPMV_PROBES
-    if (dma) {
-        if (mo) launch_mul_t<256, PL>(p, g, x);
-        else launch_mul_t<257, PL>(p, g, x);
+    // profiles/round3/probe/mul_glds_*.jsonl), else through registers.
+    bool dma = (reinterpret_cast<uintptr_t>(x) & 15) == 0 && p->bin.strip % 2 == 0;
+    // probe build, SPMV_LAUNCH_DEBUG bit 24: registers instead of LDS-DMA
+    if (launch_dbg(p->bin.dbg) & (1 << 24)) dma = false;
+    if (p->bin.mo) {
+        if (dma) launch_mul_t<256 | 4, PL>(p, g, x);
+        else launch_mul_t<4, PL>(p, g, x);
     } else {
-        if (mo) launch_mul_t<0, PL>(p, g, x);
+        if (dma) launch_mul_t<256 | 1, PL>(p, g, x);
         else launch_mul_t<1, PL>(p, g, x);
     }
-#else
-    const int dbg = launch_dbg(p->bin.dbg);
-    switch (dbg & 3) {
-        case 1: launch_mul_t<0, PL>(p, g, x); break;
-        case 2: launch_mul_t<2, PL>(p, g, x); break;
-        case 3:  // ablations: sequential NT writes (+256: no cs1 loads either)
-            if (dbg & 256) launch_mul_t<13, PL>(p, g, x);
-            else launch_mul_t<5, PL>(p, g, x);
-            break;
-        default:
-            // long-block partial stores: 2048 nontemporal, 4096 none (ablations);
-            // 16384: loads clamped at the piece's end (A/B); 131072 / 262144:
-            // x strips staged serially / in bursts (A/B, build_bin.cpp xburst);
-            // 1 << 24: x strips through registers instead of LDS-DMA (A/B)
-            if (dbg & (1 << 21)) launch_mul_t<513, PL>(p, g, x);  // ablation: no x staging
-            else if ((dbg & (1 << 28)) && dma) launch_mul_t<257 | 32768, PL>(p, g, x);  // ablation: 16-B column loads
-            else if ((dbg & (1 << 29)) && dma) {  // A/B: the other product-store policy
-                if (mo) launch_mul_t<257, PL>(p, g, x);
-                else launch_mul_t<256, PL>(p, g, x);
-            }
-            else if ((dbg & (1 << 20)) && dma) launch_mul_t<257 | 131072, PL>(p, g, x);  // A/B: rotated pieces
-            else if ((dbg & (1 << 22)) && dma) launch_mul_t<256 | 65536, PL>(p, g, x);  // A/B: nontemporal tail
-            else if (dbg & (1 << 23)) launch_mul_t<1, PL, 4>(p, g, x);  // A/B: 4-entry batches (half in flight)
-            else if (dbg & 16384) launch_mul_t<65, PL>(p, g, x);
-            else if (dbg & 2048) launch_mul_t<17, PL>(p, g, x);
-            else if (dbg & 4096) launch_mul_t<33, PL>(p, g, x);
-            else if (dma && !(dbg & (1 << 24))) {
-                if (mo) launch_mul_t<256, PL>(p, g, x);
-                else launch_mul_t<257, PL>(p, g, x);
-            } else {
-                if (mo) launch_mul_t<0, PL>(p, g, x);
-                else launch_mul_t<1, PL>(p, g, x);
-            }
-    }
-#endif
 }
 
 static void launch_mul(const spmv_plan_s *p, int g, const double *x) {
@@ -828,72 +570,13 @@ static void launch_mul(const spmv_plan_s *p, int g, const double *x) {
 }
 
 // Sum over the bins of group g (g < 0: every bin, product buffer = all products)
-template <int W2, int U, int MODE>
-static void launch_sum_t(const spmv_plan_s *p, int g, double *y) {
+template <int W2, int U>
+static void launch_sum_w(const spmv_plan_s *p, int g, double *y) {
     const BinDev &B = p->bin;
     const int64_t b0 = g < 0 ? 0 : B.g_bin[g], b1 = g < 0 ? B.n_bins : B.g_bin[g + 1];
     const int64_t pbase = g < 0 ? 0 : B.g_prod[g];
-#ifdef SPMV_PROBES
-    // A/B (SPMV_LAUNCH_DEBUG bit 26): the pipeline kept inside each bin
-    if (MODE == (1 | 512) && B.n_blocks <= 2 && (launch_dbg(B.dbg) & (1 << 26))) {
-        hipLaunchKernelGGL((bin_sum_bin_kernel<W2, U, MODE, false>), dim3((unsigned)B.nwg2), dim3(64 * W2), 0,
-                           p->stream, b0, b1, B.n_bins, B.n_blocks, B.run_off, B.srun_off, B.bin_row0, pbase,
-                           B.slot2, (const int32_t *)nullptr, B.prod, y);
-        return;
-    }
-#endif
-    hipLaunchKernelGGL((bin_sum_kernel<W2, U, MODE>), dim3((unsigned)B.nwg2), dim3(64 * W2), 0, p->stream, b0, b1,
+    hipLaunchKernelGGL((bin_sum_kernel<W2, U>), dim3((unsigned)B.nwg2), dim3(64 * W2), 0, p->stream, b0, b1,
                        B.n_bins, B.n_blocks, B.run_off, B.srun_off, B.bin_row0, pbase, B.slot2, B.prod, y);
-}
-
-template <int W2, int U>
-static void launch_sum_w(const spmv_plan_s *p, int g, double *y) {
-#ifndef SPMV_PROBES
-    // nontemporal product loads (config 2 Sum 0.308 -> 0.298 ms, neutral at
-    // config 3 and the N = 8 shape, profiles/round1/probe/bin_sum_nt_loads.jsonl)
-    // and nontemporal y stores (config 2 Sum 0.302 -> 0.292 ms, N = 8 shape
-    // 0.318 -> 0.308, config 3 -0.5 %, profiles/round2/probe/sum_nt_y_*.jsonl)
-    launch_sum_t<W2, U, 1 | 512>(p, g, y);
-#else
-    // probe build: SPMV_BIN_DEBUG bits 2-3 -> Sum MODE
-    const int dbg = launch_dbg(p->bin.dbg);
-    if (dbg & 512) {  // ablation: no slot loads
-        launch_sum_t<W2, U, 4>(p, g, y);
-        return;
-    }
-    if (dbg & 1024) {  // ablation: 16-byte product loads (wrong sums)
-        launch_sum_t<W2, U, 17>(p, g, y);
-        return;
-    }
-    if (dbg & 8192) {  // A/B: product loads clamped at the run's end, masked adds
-        launch_sum_t<W2, U, 33>(p, g, y);
-        return;
-    }
-    if (dbg & 32768) {  // ablation: no LDS zeroing / y write-back (wrong y)
-        launch_sum_t<W2, U, 129>(p, g, y);
-        return;
-    }
-    if (dbg & 524288) {  // A/B: ordinary y stores (the default's are nontemporal)
-        launch_sum_t<W2, U, 1>(p, g, y);
-        return;
-    }
-    if (dbg & 65536) {  // A/B: one bin at a time
-        launch_sum_t<W2, U, 257>(p, g, y);
-        return;
-    }
-    // default: nontemporal product loads (config 2 Sum 0.308 -> 0.298 ms,
-    // neutral at config 3 and the N = 8 shape, profiles/round1/probe/bin_sum_nt_loads.jsonl);
-    // bits 2-3 = 1: ordinary loads (ablation)
-    if (p->bin.slot_linear) {  // ablation: slots in product order (SPMV_BIN_SLOT_LINEAR)
-        launch_sum_t<W2, U, 9>(p, g, y);
-        return;
-    }
-    switch ((dbg >> 2) & 3) {
-        case 1: launch_sum_t<W2, U, 0>(p, g, y); break;
-        case 2: launch_sum_t<W2, U, 2>(p, g, y); break;
-        default: launch_sum_t<W2, U, 1 | 512>(p, g, y);
-    }
-#endif
 }
 
 int bin_time_mul(const spmv_plan_s *p, const double *x, float *ms) {

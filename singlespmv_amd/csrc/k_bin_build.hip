@@ -214,7 +214,7 @@ int bin_fill_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, c
     void *q;
     // val1 / cs1 / dst1 with the Mul's unclamped-batch slack (kBinMulSlack), zeroed
     // (Mul order: the entries fill [0, nnz) unpadded, the rest is slack)
-    const int64_t Ez = B.mo && !(B.mo_probe & 1) ? p->nnz : E;
+    const int64_t Ez = B.mo ? p->nnz : E;
     SPMV_RETURN_IF(p->arena.alloc(&q, sizeof(double) * (size_t)(E + kBinMulSlack)));
     B.val1 = (double *)q;
     SPMV_HIP_TRY(hipMemsetAsync(B.val1 + Ez, 0, sizeof(double) * (size_t)(E - Ez + kBinMulSlack), st));
@@ -253,9 +253,9 @@ int bin_fill_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, c
     SPMV_HIP_TRY(hipMemsetAsync(d_kh, 0, 8 * (size_t)E, st));  // now the k-run cursors
     hipLaunchKernelGGL(bin_place_kernel, dim3(grid), dim3(256), 0, st, d_rp, d_col, d_val, p->nnz, d_bstart, NB,
                        d_row0, (int32_t)C, S, d_off1, d_off2, d_ks, d_kh, d_pbb, B.pad_log, d_run, d_srun,
-                       B.strip_block, B.slot_linear ? 0 : B.sum_u, B.val1, B.cs1, B.slot2,
+                       B.strip_block, B.sum_u, B.val1, B.cs1, B.slot2,
                        B.dst1);
-    if (!B.mo || (B.mo_probe & 1))  // (Mul order: the Mul's segments are not padded)
+    if (!B.mo)  // (Mul order: the Mul's segments are not padded)
         hipLaunchKernelGGL(bin_pad_kernel, dim3(grid_of(NB * S)), dim3(256), 0, st, d_cnt, NB * S, d_off1, B.pad_log,
                            B.val1, B.cs1);
     return finish(st, "fill");

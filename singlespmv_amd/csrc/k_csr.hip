@@ -52,6 +52,208 @@ __global__ __launch_bounds__(256) void csr_vec4_kernel(int64_t m, const int32_t 
     if (lane == 0) y[row] = acc;
 }
 
+// csr_slab<L, U>: one wave per slab of 64 consecutive rows, the 64 / L rows
+// of a step summed by L-lane groups exactly as csr_vec4<L> sums them (same
+// chunks, same order, same butterfly: bit-identical y), U steps' col / val
+// loads issued before their gathers.  Lane t keeps row r0 + t's sum (one
+// ds_bpermute per step), so y leaves as ONE coalesced 512-B store per wave
+// instead of 64 / L scattered 8-B stores per 4-row wave; a long-lived wave
+// also replaces 16 short ones (config 4: 16 lanes, 4 rows per wave).
+template <int L, typename RP, int U>
+__global__ __launch_bounds__(256) void csr_slab_kernel(int64_t m, const RP *__restrict__ rp,
+                                                       const int32_t *__restrict__ col,
+                                                       const double *__restrict__ val,
+                                                       const double *__restrict__ x, double *__restrict__ y) {
+    constexpr int R = 64 / L;  // rows per step
+    const int lane = threadIdx.x & 63;
+    const int64_t r0 = ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 64;
+    if (r0 >= m) return;  // wave-uniform
+    const int g = lane / L, gl = lane & (L - 1);
+    const int64_t rl = r0 + lane;
+    const int64_t rpl = (int64_t)rp[rl < m ? rl : m];        // lane t: start of row r0 + t
+    const int64_t rpe = (int64_t)rp[r0 + 64 < m ? r0 + 64 : m];  // end of the slab
+    double mine = 0.0;
+    for (int st = 0; st < L; st += U) {
+        int64_t s[U], e[U], j0[U];
+        i32x4 c[U];
+        f64x2 a[U], b[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int li = (st + u) * R + g;
+            s[u] = __shfl(rpl, li, 64);
+            const int64_t nx = __shfl(rpl, (li + 1) & 63, 64);
+            e[u] = li == 63 ? rpe : nx;
+            j0[u] = (s[u] & ~(int64_t)3) + 4 * gl;
+            if (j0[u] < e[u]) {
+                c[u] = ld_stream4(col + j0[u]);
+                a[u] = ld_stream2(val + j0[u]);
+                b[u] = ld_stream2(val + j0[u] + 2);
+            } else {
+                c[u] = i32x4{0, 0, 0, 0};
+                a[u] = f64x2{0.0, 0.0};
+                b[u] = a[u];
+            }
+        }
+        double gx[U][4];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t j = j0[u];
+            gx[u][0] = (j + 0 >= s[u] && j + 0 < e[u]) ? ld_x(x, c[u].x) : 0.0;
+            gx[u][1] = (j + 1 >= s[u] && j + 1 < e[u]) ? ld_x(x, c[u].y) : 0.0;
+            gx[u][2] = (j + 2 >= s[u] && j + 2 < e[u]) ? ld_x(x, c[u].z) : 0.0;
+            gx[u][3] = (j + 3 >= s[u] && j + 3 < e[u]) ? ld_x(x, c[u].w) : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t j = j0[u];
+            double acc = 0.0;
+            if (j + 0 >= s[u] && j + 0 < e[u]) acc = madd(a[u].x, gx[u][0], acc);
+            if (j + 1 >= s[u] && j + 1 < e[u]) acc = madd(a[u].y, gx[u][1], acc);
+            if (j + 2 >= s[u] && j + 2 < e[u]) acc = madd(b[u].x, gx[u][2], acc);
+            if (j + 3 >= s[u] && j + 3 < e[u]) acc = madd(b[u].y, gx[u][3], acc);
+            // rows longer than one chunk of the group: the rest in order
+            for (int64_t jj = j + 4 * L; jj < e[u]; jj += 4 * L) {
+                const i32x4 cc = ld_stream4(col + jj);
+                const f64x2 v01 = ld_stream2(val + jj);
+                const f64x2 v23 = ld_stream2(val + jj + 2);
+                const double x0 = jj + 0 < e[u] ? ld_x(x, cc.x) : 0.0;
+                const double x1 = jj + 1 < e[u] ? ld_x(x, cc.y) : 0.0;
+                const double x2 = jj + 2 < e[u] ? ld_x(x, cc.z) : 0.0;
+                const double x3 = jj + 3 < e[u] ? ld_x(x, cc.w) : 0.0;
+                if (jj + 0 < e[u]) acc = madd(v01.x, x0, acc);
+                if (jj + 1 < e[u]) acc = madd(v01.y, x1, acc);
+                if (jj + 2 < e[u]) acc = madd(v23.x, x2, acc);
+                if (jj + 3 < e[u]) acc = madd(v23.y, x3, acc);
+            }
+            acc = group_sum<L>(acc);
+            // row (st + u) * R + g' sits in group g'; lane t takes row t
+            const double v = __shfl(acc, (lane % R) * L, 64);
+            if (lane / R == st + u) mine = v;
+        }
+    }
+    if (rl < m) __builtin_nontemporal_store(mine, y + rl);
+}
+
+// csr_slab2<L, U>: csr_slab with no divergent control flow on the common
+// path.  Lanes past their row's end load the row's first chunk again (same
+// lines, no new traffic) and every loaded column is a real column (plan
+// creation validated them; the kPad tail is zero), so the col / val loads
+// and the x gathers are unconditional.  When every row of a batch of U steps
+// is one aligned chunk of its group (4L entries from a 16-byte boundary:
+// configs 2 and 4) the adds run unmasked; otherwise an entry outside [s, e)
+// is dropped by a select on its add (one 32-bit compare per entry) -- either
+// way the arithmetic of csr_vec4.  Group sums by DPP (group_sum_dpp:
+// bit-identical to group_sum), the row sums through a 512-B LDS slab per
+// wave, then one coalesced store.  Row pointers are exchanged by ds_bpermute
+// as 32-bit values relative to the slab's first entry.  O32 (CsrDev::off32:
+// every slab's byte span and x's fit 31 / 32 bits): the col / val loads and
+// the x gathers address a wave-uniform base plus a 32-bit byte offset (the
+// global_load saddr form: no 64-bit address arithmetic per lane).
+template <bool O32>
+__device__ __forceinline__ const void *at_bytes(const void *base, int idx, int size) {
+    if constexpr (O32) return (const char *)base + (uint32_t)idx * (uint32_t)size;
+    else return (const char *)base + (int64_t)idx * size;
+}
+
+template <int L, typename RP, int U, bool O32>
+__global__ __launch_bounds__(256) void csr_slab2_kernel(int64_t m, const RP *__restrict__ rp,
+                                                        const int32_t *__restrict__ col,
+                                                        const double *__restrict__ val,
+                                                        const double *__restrict__ x, double *__restrict__ y) {
+    constexpr int R = 64 / L;  // rows per step
+    __shared__ double ysl[4][64];
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR)
+    const int lane = threadIdx.x & 63;
+    const int64_t r0 = ((int64_t)blockIdx.x * 4 + wv) * 64;
+    if (r0 >= m) return;  // wave-uniform
+    const int g = lane / L, gl = lane & (L - 1);
+    const int64_t rl = r0 + lane;
+    auto ldx = [&](int c) -> double { return *(const double *)at_bytes<O32>(x, c, 8); };
+    // the slab's entries [base, end) (a slab of 64 rows holds < 2^31 entries:
+    // its offsets are 32-bit)
+    const int64_t base = (int64_t)rp[r0] & ~(int64_t)3;
+    const int rpl = (int)((int64_t)rp[rl < m ? rl : m] - base);            // lane t: row r0 + t's start
+    const int rpe = (int)((int64_t)rp[r0 + 64 < m ? r0 + 64 : m] - base);  // the slab's end
+    const int32_t *cb = col + base;
+    const double *vb = val + base;
+    for (int st = 0; st < L; st += U) {
+        int j0[U], rel[U], len[U];
+        bool full = true;
+        i32x4 c[U];
+        f64x2 a[U], b[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int li = (st + u) * R + g;
+            const int s = __shfl(rpl, li, 64);
+            const int nx = __shfl(rpl, (li + 1) & 63, 64);
+            const int e = li == 63 ? rpe : nx;
+            const int a0 = s & ~3;
+            j0[u] = a0 + 4 * gl;
+            rel[u] = j0[u] - s;
+            len[u] = e - s;
+            full = full && (s & 3) == 0 && len[u] == 4 * L;
+            const int jl = j0[u] < e ? j0[u] : a0;
+            c[u] = ld_stream4((const int32_t *)at_bytes<O32>(cb, jl, 4));
+            a[u] = ld_stream2((const double *)at_bytes<O32>(vb, jl, 8));
+            b[u] = ld_stream2((const double *)at_bytes<O32>(vb, jl + 2, 8));
+        }
+        double gx[U][4];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            gx[u][0] = ldx(c[u].x);
+            gx[u][1] = ldx(c[u].y);
+            gx[u][2] = ldx(c[u].z);
+            gx[u][3] = ldx(c[u].w);
+        }
+        if (__ballot(!full) == 0) {  // no lane with a partial row: unmasked adds
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                double acc = 0.0;
+                acc = madd(a[u].x, gx[u][0], acc);
+                acc = madd(a[u].y, gx[u][1], acc);
+                acc = madd(b[u].x, gx[u][2], acc);
+                acc = madd(b[u].y, gx[u][3], acc);
+                acc = group_sum_dpp<L>(acc);
+                if (gl == 0) ysl[wv][(st + u) * R + g] = acc;
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                double acc = 0.0, t;
+                t = madd(a[u].x, gx[u][0], acc);
+                acc = (unsigned)(rel[u] + 0) < (unsigned)len[u] ? t : acc;
+                t = madd(a[u].y, gx[u][1], acc);
+                acc = (unsigned)(rel[u] + 1) < (unsigned)len[u] ? t : acc;
+                t = madd(b[u].x, gx[u][2], acc);
+                acc = (unsigned)(rel[u] + 2) < (unsigned)len[u] ? t : acc;
+                t = madd(b[u].y, gx[u][3], acc);
+                acc = (unsigned)(rel[u] + 3) < (unsigned)len[u] ? t : acc;
+                // rows longer than one chunk of the group: the rest in order
+                const int e = j0[u] - rel[u] + len[u];  // the row's end
+                for (int jj = j0[u] + 4 * L; jj < e; jj += 4 * L) {
+                    const i32x4 cc = ld_stream4((const int32_t *)at_bytes<O32>(cb, jj, 4));
+                    const f64x2 v01 = ld_stream2((const double *)at_bytes<O32>(vb, jj, 8));
+                    const f64x2 v23 = ld_stream2((const double *)at_bytes<O32>(vb, jj + 2, 8));
+                    const double x0 = ldx(cc.x), x1 = ldx(cc.y), x2 = ldx(cc.z), x3 = ldx(cc.w);
+                    acc = madd(v01.x, x0, acc);
+                    t = madd(v01.y, x1, acc);
+                    acc = jj + 1 < e ? t : acc;
+                    t = madd(v23.x, x2, acc);
+                    acc = jj + 2 < e ? t : acc;
+                    t = madd(v23.y, x3, acc);
+                    acc = jj + 3 < e ? t : acc;
+                }
+                acc = group_sum_dpp<L>(acc);
+                if (gl == 0) ysl[wv][(st + u) * R + g] = acc;
+            }
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (rl < m) __builtin_nontemporal_store(ysl[wv][lane], y + rl);
+}
+
 // One 256-thread workgroup per row (the longest-row bin of adaptive CSR):
 // four waves stride the row in 1 KiB chunks, each reduces with the fixed
 // butterfly, and the four wave sums are added in wave order (deterministic).
@@ -205,17 +407,56 @@ static int launch_adaptive(const spmv_plan_s *p, const int64_t *bin_off, const i
     return SPMV_SUCCESS;
 }
 
+// launch-time shape of the row-parallel CSR kernels (probe build: read at
+// every launch, so variants are A/B'd on one plan's memory)
+struct CsrLaunch {
+    int slab = 0;    // 1: csr_slab_kernel
+    int u = 1;       // slab: steps whose loads are issued together
+    size_t lds = 0;  // dynamic LDS per workgroup (caps workgroups per CU)
+};
+static CsrLaunch csr_launch_shape() {
+    CsrLaunch s;
+    if (const char *e = probe_env("SPMV_LAUNCH_CSR")) s.slab = std::atoi(e);
+    if (const char *e = probe_env("SPMV_LAUNCH_CSR_U")) s.u = std::atoi(e);
+    if (const char *e = probe_env("SPMV_LAUNCH_CSR_LDS_KB")) s.lds = (size_t)std::atoi(e) * 1024;
+    return s;
+}
+
+template <int L, typename RP, int U>
+static void launch_slab_u(const spmv_plan_s *p, int kind, size_t lds, const double *x, double *y) {
+    constexpr int UU = U < L ? U : L;
+    const int64_t waves = (p->m + 63) / 64;
+    if (kind == 2 && p->csr.off32)
+        hipLaunchKernelGGL((csr_slab2_kernel<L, RP, UU, true>), dim3((unsigned)((waves + 3) / 4)), dim3(256), lds,
+                           p->stream, p->m, (const RP *)p->csr.row_ptr, p->csr.col, p->csr.val, x, y);
+    else if (kind >= 2)
+        hipLaunchKernelGGL((csr_slab2_kernel<L, RP, UU, false>), dim3((unsigned)((waves + 3) / 4)), dim3(256), lds,
+                           p->stream, p->m, (const RP *)p->csr.row_ptr, p->csr.col, p->csr.val, x, y);
+    else
+        hipLaunchKernelGGL((csr_slab_kernel<L, RP, UU>), dim3((unsigned)((waves + 3) / 4)), dim3(256), lds,
+                           p->stream, p->m, (const RP *)p->csr.row_ptr, p->csr.col, p->csr.val, x, y);
+}
+
 template <int L, typename RP>
 static int launch_csr_t(const spmv_plan_s *p, int64_t nrows, const int32_t *rows, const double *x, double *y) {
     const int64_t threads = nrows * L;
     const int64_t blocks = (threads + 255) / 256;
     if (blocks == 0) return SPMV_SUCCESS;
-    if (rows)
+    const CsrLaunch sh = rows ? CsrLaunch{} : csr_launch_shape();
+    if (sh.slab) {
+        switch (sh.u) {
+            case 2: launch_slab_u<L, RP, 2>(p, sh.slab, sh.lds, x, y); break;
+            case 4: launch_slab_u<L, RP, 4>(p, sh.slab, sh.lds, x, y); break;
+            case 8: launch_slab_u<L, RP, 8>(p, sh.slab, sh.lds, x, y); break;
+            default: launch_slab_u<L, RP, 1>(p, sh.slab, sh.lds, x, y);
+        }
+    } else if (rows) {
         hipLaunchKernelGGL((csr_vec4_kernel<L, RP, true>), dim3((unsigned)blocks), dim3(256), 0, p->stream, nrows,
                            rows, (const RP *)p->csr.row_ptr, p->csr.col, p->csr.val, x, y);
-    else
-        hipLaunchKernelGGL((csr_vec4_kernel<L, RP, false>), dim3((unsigned)blocks), dim3(256), 0, p->stream, nrows,
-                           rows, (const RP *)p->csr.row_ptr, p->csr.col, p->csr.val, x, y);
+    } else {
+        hipLaunchKernelGGL((csr_vec4_kernel<L, RP, false>), dim3((unsigned)blocks), dim3(256), sh.lds, p->stream,
+                           nrows, rows, (const RP *)p->csr.row_ptr, p->csr.col, p->csr.val, x, y);
+    }
     SPMV_HIP_TRY(hipGetLastError());
     return SPMV_SUCCESS;
 }

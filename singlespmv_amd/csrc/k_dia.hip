@@ -132,7 +132,12 @@ int launch_dia(const spmv_plan_s *p, const double *x, double *y) {
     // 1.476-1.527 ms at 1 per CU, 1.500-1.594 at 2, 1.537-1.641 at 8
     // (profiles/round3/probe/dia_occupancy_paired_c4.jsonl,
     // dia_unroll_occupancy_c4.jsonl)
-    int kb = d.lds_kb >= 0 ? d.lds_kb : kDiaLdsKb;
+    // The cap is measured on config 4 only (10 GB of values); below the size
+    // at which DIA values take VMM handles (kDiaVmmMinBytes, 256 MB) the
+    // launch keeps the x window's own occupancy (more latency hiding for
+    // small matrices)
+    const bool big = (size_t)d.n_diags * (size_t)d.mp * sizeof(double) >= kDiaVmmMinBytes;
+    int kb = d.lds_kb >= 0 ? d.lds_kb : (big ? kDiaLdsKb : 0);
     if (const char *e = probe_env("SPMV_LAUNCH_DIA_LDS_KB")) kb = std::atoi(e);
     const int dbg = launch_dbg(d.dbg);
     const size_t lds = std::max(sizeof(double) * (size_t)win, (size_t)kb * 1024);

@@ -79,24 +79,29 @@ __global__ __launch_bounds__(256) void ell_slice_kernel(int64_t m, int64_t n_sli
 }
 
 template <int U>
-static void launch_ell_u(const spmv_plan_s *p, const double *x, double *y) {
+static void launch_ell_u(const spmv_plan_s *p, const double *x, double *y, size_t lds) {
     const EllDev &e = p->ell;
     const int64_t blocks = (e.n_slices + 3) / 4;
     if (e.perm)
-        hipLaunchKernelGGL((ell_slice_kernel<U, false, true>), dim3((unsigned)blocks), dim3(256), 0, p->stream,
+        hipLaunchKernelGGL((ell_slice_kernel<U, false, true>), dim3((unsigned)blocks), dim3(256), lds, p->stream,
                            p->m, e.n_slices, e.perm, e.slice_off, e.col, e.val, x, y);
     else
-        hipLaunchKernelGGL((ell_slice_kernel<U, false, false>), dim3((unsigned)blocks), dim3(256), 0,
+        hipLaunchKernelGGL((ell_slice_kernel<U, false, false>), dim3((unsigned)blocks), dim3(256), lds,
                            p->stream, p->m, e.n_slices, e.perm, e.slice_off, e.col, e.val, x, y);
 }
 
 int launch_ell(const spmv_plan_s *p, const double *x, double *y) {
     const EllDev &e = p->ell;
     if (e.n_slices == 0) return SPMV_SUCCESS;
-    switch (e.unroll) {  // quads (4 slots each) per lane per iteration
-        case 1: launch_ell_u<1>(p, x, y); break;
-        case 4: launch_ell_u<4>(p, x, y); break;
-        default: launch_ell_u<2>(p, x, y);
+    // probe build: launch-time unroll / LDS request (workgroups per CU)
+    int unroll = e.unroll;
+    size_t lds = 0;
+    if (const char *v = probe_env("SPMV_LAUNCH_ELL_UNROLL")) unroll = std::atoi(v);
+    if (const char *v = probe_env("SPMV_LAUNCH_ELL_LDS_KB")) lds = (size_t)std::atoi(v) * 1024;
+    switch (unroll) {  // quads (4 slots each) per lane per iteration
+        case 1: launch_ell_u<1>(p, x, y, lds); break;
+        case 4: launch_ell_u<4>(p, x, y, lds); break;
+        default: launch_ell_u<2>(p, x, y, lds);
     }
     SPMV_HIP_TRY(hipGetLastError());
     return SPMV_SUCCESS;

@@ -25,10 +25,14 @@ import singlespmv_amd as sp
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "singlespmv_amd", "csrc")
-PROBE_VARS = ["SPMV_BIN_DEBUG", "SPMV_BIN_PADLOG", "SPMV_BIN_SUMWAVES", "SPMV_BIN_SLOT_LINEAR", "SPMV_BIN_REUSE",
+PROBE_VARS = ["SPMV_BIN_DEBUG", "SPMV_BIN_PADLOG", "SPMV_BIN_SUMWAVES", "SPMV_BIN_REUSE",
               "SPMV_BIN_SB", "SPMV_BIN_CUS", "SPMV_BIN_PLACEMENT", "SPMV_BIN_HOST_BUILD", "SPMV_CSS_DEBUG",
               "SPMV_CSS_LAYOUT", "SPMV_CSS_PIECE_DIV", "SPMV_CSS_WGS", "SPMV_DIA_DEBUG", "SPMV_DIA_PLACEMENT",
-              "SPMV_ELL_UNROLL", "SPMV_CSR_FORCE_RP64", "SPMV_PLACEMENT_MODE", "SPMV_VMM_CHUNK_MB", "SPMV_BIN_ORDER"]
+              "SPMV_ELL_UNROLL", "SPMV_CSR_FORCE_RP64", "SPMV_PLACEMENT_MODE", "SPMV_VMM_CHUNK_MB", "SPMV_BIN_ORDER",
+              "SPMV_LAUNCH_DEBUG", "SPMV_VMM_ALIGN_MB", "SPMV_VMM_STRIDE", "SPMV_VMM_SHUFFLE", "SPMV_DIA_GROUP",
+              "SPMV_DIA_LDS_KB", "SPMV_LAUNCH_DIA_LDS_KB", "SPMV_ARENA_VMM_MB", "SPMV_LAUNCH_CSR",
+              "SPMV_LAUNCH_CSR_U", "SPMV_LAUNCH_CSR_LDS_KB", "SPMV_LAUNCH_ELL_UNROLL", "SPMV_LAUNCH_ELL_LDS_KB",
+              "SPMV_BIN_MUL_PERM", "SPMV_BIN_PLACEMENT_GAP_MB"]
 
 
 def _strings(path):
@@ -66,13 +70,35 @@ def _kernel_bodies(asm, name_part):
 
 
 @pytest.mark.parametrize("src,kernel", [("k_probe.hip", "lds_order_kernel"), ("k_bin.hip", "bin_sum_kernel"),
-                                        ("k_css.hip", "css_sweep_kernel")])
+                                        ("k_bin.hip", "bin_sum_bin_kernel"), ("k_css.hip", "css_sweep_kernel")])
 def test_lds_adds_are_single_ds_add_f64(src, kernel):
     bodies = _kernel_bodies(_device_asm(os.path.join("singlespmv_amd", "csrc", src)), kernel)
     assert bodies, f"no {kernel} in {src}"
     for b in bodies:
         assert "ds_add_f64" in b or "ds_add_rtn_f64" in b, f"{kernel}: LDS f64 add is not ds_add_f64"
         assert "ds_cmpst" not in b and "ds_cmpswap" not in b, f"{kernel}: CAS loop"
+
+
+def test_lds_dma_strips_drained_before_the_barrier():
+    """The Mul's x strips staged by LDS-DMA (global_load_lds) are read by the
+    other waves after the workgroup barrier: every such body waits for
+    vmcnt(0) between its last DMA load and the next s_barrier (the source
+    asks for it explicitly; this keeps a compiler change from dropping it)."""
+    bodies = [b for b in _kernel_bodies(_device_asm(os.path.join("singlespmv_amd", "csrc", "k_bin.hip")),
+                                        "bin_mul_kernel") if "global_load_lds" in b]
+    assert bodies, "no LDS-DMA bin_mul_kernel instance"
+    for b in bodies:
+        last = b.rfind("global_load_lds")
+        bar = b.find("s_barrier", last)
+        assert bar > 0 and re.search(r"s_waitcnt vmcnt\(0\)", b[last:bar]), "DMA strip not drained before the barrier"
+
+
+def test_product_bin_kernels_carry_no_ablation():
+    """k_bin.hip holds the product kernels only: the probe ablations (wrong-y
+    modes) of rounds 1-3 are gone from its source (their results stay under
+    profiles/)."""
+    src = open(os.path.join(CSRC, "k_bin.hip")).read()
+    assert "ablation" not in src.lower() and "wrong y" not in src
 
 
 def test_vector_checks():

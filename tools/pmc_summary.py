@@ -73,7 +73,10 @@ def main(src, tag, config_key_prefix):
                 tot, found = 0.0, 0
                 for part in parts:
                     # the instantiation the timed loop ran: most launches
-                    cands = [s for k, s in summary.items() if part in k.split("(")[0]]
+                    # (template arguments stripped: "ell_slice_kernel<perm>" is
+                    # the instance "ell_slice_kernel<2, false, true>"; profile one
+                    # format per run so a part names one instantiation)
+                    cands = [s for k, s in summary.items() if part.split("<")[0] in k.split("(")[0]]
                     if cands:
                         tot += max(cands, key=lambda s: s["launches"])[field]
                         found += 1
