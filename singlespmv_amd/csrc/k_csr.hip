@@ -2,6 +2,11 @@
 // (src/opt_crs.cpp:57-69, `y[i] = sum_j val[j] * x[idx[j]]`) re-designed for
 // wave64.
 //
+// The product kernels: csr_slab2 (near-uniform rows, below) and
+// csr_adaptive (rows binned by length).  csr_vec4 is the round-3 kernel whose
+// order of arithmetic both keep; the probe build still launches it for A/Bs
+// (SPMV_LAUNCH_CSR=0).
+//
 // csr_vec4<L, RP>: a group of L lanes (L | 64) owns one row.  The group walks
 // the row from its 16-byte-aligned start a = ptr[i] & ~3 in chunks of 4*L
 // entries; each lane issues ONE 16-byte load of 4 column indices and TWO
@@ -52,90 +57,14 @@ __global__ __launch_bounds__(256) void csr_vec4_kernel(int64_t m, const int32_t 
     if (lane == 0) y[row] = acc;
 }
 
-// csr_slab<L, U>: one wave per slab of 64 consecutive rows, the 64 / L rows
-// of a step summed by L-lane groups exactly as csr_vec4<L> sums them (same
-// chunks, same order, same butterfly: bit-identical y), U steps' col / val
-// loads issued before their gathers.  Lane t keeps row r0 + t's sum (one
-// ds_bpermute per step), so y leaves as ONE coalesced 512-B store per wave
-// instead of 64 / L scattered 8-B stores per 4-row wave; a long-lived wave
-// also replaces 16 short ones (config 4: 16 lanes, 4 rows per wave).
-template <int L, typename RP, int U>
-__global__ __launch_bounds__(256) void csr_slab_kernel(int64_t m, const RP *__restrict__ rp,
-                                                       const int32_t *__restrict__ col,
-                                                       const double *__restrict__ val,
-                                                       const double *__restrict__ x, double *__restrict__ y) {
-    constexpr int R = 64 / L;  // rows per step
-    const int lane = threadIdx.x & 63;
-    const int64_t r0 = ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 64;
-    if (r0 >= m) return;  // wave-uniform
-    const int g = lane / L, gl = lane & (L - 1);
-    const int64_t rl = r0 + lane;
-    const int64_t rpl = (int64_t)rp[rl < m ? rl : m];        // lane t: start of row r0 + t
-    const int64_t rpe = (int64_t)rp[r0 + 64 < m ? r0 + 64 : m];  // end of the slab
-    double mine = 0.0;
-    for (int st = 0; st < L; st += U) {
-        int64_t s[U], e[U], j0[U];
-        i32x4 c[U];
-        f64x2 a[U], b[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int li = (st + u) * R + g;
-            s[u] = __shfl(rpl, li, 64);
-            const int64_t nx = __shfl(rpl, (li + 1) & 63, 64);
-            e[u] = li == 63 ? rpe : nx;
-            j0[u] = (s[u] & ~(int64_t)3) + 4 * gl;
-            if (j0[u] < e[u]) {
-                c[u] = ld_stream4(col + j0[u]);
-                a[u] = ld_stream2(val + j0[u]);
-                b[u] = ld_stream2(val + j0[u] + 2);
-            } else {
-                c[u] = i32x4{0, 0, 0, 0};
-                a[u] = f64x2{0.0, 0.0};
-                b[u] = a[u];
-            }
-        }
-        double gx[U][4];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int64_t j = j0[u];
-            gx[u][0] = (j + 0 >= s[u] && j + 0 < e[u]) ? ld_x(x, c[u].x) : 0.0;
-            gx[u][1] = (j + 1 >= s[u] && j + 1 < e[u]) ? ld_x(x, c[u].y) : 0.0;
-            gx[u][2] = (j + 2 >= s[u] && j + 2 < e[u]) ? ld_x(x, c[u].z) : 0.0;
-            gx[u][3] = (j + 3 >= s[u] && j + 3 < e[u]) ? ld_x(x, c[u].w) : 0.0;
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int64_t j = j0[u];
-            double acc = 0.0;
-            if (j + 0 >= s[u] && j + 0 < e[u]) acc = madd(a[u].x, gx[u][0], acc);
-            if (j + 1 >= s[u] && j + 1 < e[u]) acc = madd(a[u].y, gx[u][1], acc);
-            if (j + 2 >= s[u] && j + 2 < e[u]) acc = madd(b[u].x, gx[u][2], acc);
-            if (j + 3 >= s[u] && j + 3 < e[u]) acc = madd(b[u].y, gx[u][3], acc);
-            // rows longer than one chunk of the group: the rest in order
-            for (int64_t jj = j + 4 * L; jj < e[u]; jj += 4 * L) {
-                const i32x4 cc = ld_stream4(col + jj);
-                const f64x2 v01 = ld_stream2(val + jj);
-                const f64x2 v23 = ld_stream2(val + jj + 2);
-                const double x0 = jj + 0 < e[u] ? ld_x(x, cc.x) : 0.0;
-                const double x1 = jj + 1 < e[u] ? ld_x(x, cc.y) : 0.0;
-                const double x2 = jj + 2 < e[u] ? ld_x(x, cc.z) : 0.0;
-                const double x3 = jj + 3 < e[u] ? ld_x(x, cc.w) : 0.0;
-                if (jj + 0 < e[u]) acc = madd(v01.x, x0, acc);
-                if (jj + 1 < e[u]) acc = madd(v01.y, x1, acc);
-                if (jj + 2 < e[u]) acc = madd(v23.x, x2, acc);
-                if (jj + 3 < e[u]) acc = madd(v23.y, x3, acc);
-            }
-            acc = group_sum<L>(acc);
-            // row (st + u) * R + g' sits in group g'; lane t takes row t
-            const double v = __shfl(acc, (lane % R) * L, 64);
-            if (lane / R == st + u) mine = v;
-        }
-    }
-    if (rl < m) __builtin_nontemporal_store(mine, y + rl);
-}
-
-// csr_slab2<L, U>: csr_slab with no divergent control flow on the common
-// path.  Lanes past their row's end load the row's first chunk again (same
+// csr_slab2<L, U, O32> (the product CSR kernel for near-uniform rows): one
+// wave per slab of 64 consecutive rows, the 64 / L rows of a step summed by
+// L-lane groups exactly as csr_vec4<L> sums them (same chunks, same order,
+// same butterfly: bit-identical y), U steps' col / val loads issued before
+// their gathers.  A long-lived wave replaces 64 / (256 / L) short ones and y
+// leaves in one coalesced store per wave (config 4, same plans: csr_vec4<16>
+// 2.82 -> 2.48 ms, profiles/round4/probe/).  No divergent control flow on the
+// common path.  Lanes past their row's end load the row's first chunk again (same
 // lines, no new traffic) and every loaded column is a real column (plan
 // creation validated them; the kPad tail is zero), so the col / val loads
 // and the x gathers are unconditional.  When every row of a batch of U steps
@@ -252,34 +181,6 @@ __global__ __launch_bounds__(256) void csr_slab2_kernel(int64_t m, const RP *__r
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     if (rl < m) __builtin_nontemporal_store(ysl[wv][lane], y + rl);
-}
-
-// One 256-thread workgroup per row (the longest-row bin of adaptive CSR):
-// four waves stride the row in 1 KiB chunks, each reduces with the fixed
-// butterfly, and the four wave sums are added in wave order (deterministic).
-template <typename RP>
-__global__ __launch_bounds__(256) void csr_block_kernel(const int32_t *__restrict__ rows, const RP *__restrict__ rp,
-                                                        const int32_t *__restrict__ col,
-                                                        const double *__restrict__ val,
-                                                        const double *__restrict__ x, double *__restrict__ y) {
-    __shared__ double part[4];
-    const int64_t row = rows[blockIdx.x];
-    const int64_t s = rp[row];
-    const int64_t e = rp[row + 1];
-    double acc = 0.0;
-    for (int64_t j = (s & ~(int64_t)3) + 4 * threadIdx.x; j < e; j += 4 * 256) {
-        const i32x4 c = ld_stream4(col + j);
-        const f64x2 v01 = ld_stream2(val + j);
-        const f64x2 v23 = ld_stream2(val + j + 2);
-        if (j + 0 >= s && j + 0 < e) acc = madd(v01.x, ld_x(x, c.x), acc);
-        if (j + 1 >= s && j + 1 < e) acc = madd(v01.y, ld_x(x, c.y), acc);
-        if (j + 2 >= s && j + 2 < e) acc = madd(v23.x, ld_x(x, c.z), acc);
-        if (j + 3 >= s && j + 3 < e) acc = madd(v23.y, ld_x(x, c.w), acc);
-    }
-    acc = group_sum<64>(acc);
-    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
-    __syncthreads();
-    if (threadIdx.x == 0) y[row] = __dadd_rn(__dadd_rn(part[0], part[1]), __dadd_rn(part[2], part[3]));
 }
 
 // Adaptive CSR in ONE launch: workgroup ranges map to the length bins
@@ -407,12 +308,16 @@ static int launch_adaptive(const spmv_plan_s *p, const int64_t *bin_off, const i
     return SPMV_SUCCESS;
 }
 
-// launch-time shape of the row-parallel CSR kernels (probe build: read at
-// every launch, so variants are A/B'd on one plan's memory)
+// launch-time shape of the row-parallel CSR kernels: csr_slab2 with U =
+// min(4, L) steps per batch (config 4, 16 lanes: U = 1 / 2 / 4 / 8 ran
+// 2.64 / 2.55 / 2.49 / 2.54 ms; config 2 within 1 %; profiles/round4/probe/).
+// The probe build reads SPMV_LAUNCH_CSR (0: csr_vec4, the round-3 kernel),
+// SPMV_LAUNCH_CSR_U and SPMV_LAUNCH_CSR_LDS_KB at every launch, so variants
+// are A/B'd on one plan's memory.
 struct CsrLaunch {
-    int slab = 0;    // 1: csr_slab_kernel
-    int u = 1;       // slab: steps whose loads are issued together
-    size_t lds = 0;  // dynamic LDS per workgroup (caps workgroups per CU)
+    int slab = 2;    // 2: csr_slab2_kernel, 0: csr_vec4_kernel (probe A/B)
+    int u = 4;       // slab: steps whose loads are issued together
+    size_t lds = 0;  // dynamic LDS per workgroup (caps workgroups per CU; probe)
 };
 static CsrLaunch csr_launch_shape() {
     CsrLaunch s;
@@ -423,62 +328,48 @@ static CsrLaunch csr_launch_shape() {
 }
 
 template <int L, typename RP, int U>
-static void launch_slab_u(const spmv_plan_s *p, int kind, size_t lds, const double *x, double *y) {
+static void launch_slab_u(const spmv_plan_s *p, size_t lds, const double *x, double *y) {
     constexpr int UU = U < L ? U : L;
     const int64_t waves = (p->m + 63) / 64;
-    if (kind == 2 && p->csr.off32)
+    if (p->csr.off32)
         hipLaunchKernelGGL((csr_slab2_kernel<L, RP, UU, true>), dim3((unsigned)((waves + 3) / 4)), dim3(256), lds,
                            p->stream, p->m, (const RP *)p->csr.row_ptr, p->csr.col, p->csr.val, x, y);
-    else if (kind >= 2)
-        hipLaunchKernelGGL((csr_slab2_kernel<L, RP, UU, false>), dim3((unsigned)((waves + 3) / 4)), dim3(256), lds,
-                           p->stream, p->m, (const RP *)p->csr.row_ptr, p->csr.col, p->csr.val, x, y);
     else
-        hipLaunchKernelGGL((csr_slab_kernel<L, RP, UU>), dim3((unsigned)((waves + 3) / 4)), dim3(256), lds,
+        hipLaunchKernelGGL((csr_slab2_kernel<L, RP, UU, false>), dim3((unsigned)((waves + 3) / 4)), dim3(256), lds,
                            p->stream, p->m, (const RP *)p->csr.row_ptr, p->csr.col, p->csr.val, x, y);
 }
 
 template <int L, typename RP>
-static int launch_csr_t(const spmv_plan_s *p, int64_t nrows, const int32_t *rows, const double *x, double *y) {
+static int launch_csr_t(const spmv_plan_s *p, int64_t nrows, const double *x, double *y) {
     const int64_t threads = nrows * L;
     const int64_t blocks = (threads + 255) / 256;
     if (blocks == 0) return SPMV_SUCCESS;
-    const CsrLaunch sh = rows ? CsrLaunch{} : csr_launch_shape();
+    const CsrLaunch sh = csr_launch_shape();
     if (sh.slab) {
         switch (sh.u) {
-            case 2: launch_slab_u<L, RP, 2>(p, sh.slab, sh.lds, x, y); break;
-            case 4: launch_slab_u<L, RP, 4>(p, sh.slab, sh.lds, x, y); break;
-            case 8: launch_slab_u<L, RP, 8>(p, sh.slab, sh.lds, x, y); break;
-            default: launch_slab_u<L, RP, 1>(p, sh.slab, sh.lds, x, y);
+            case 1: launch_slab_u<L, RP, 1>(p, sh.lds, x, y); break;
+            case 2: launch_slab_u<L, RP, 2>(p, sh.lds, x, y); break;
+            case 8: launch_slab_u<L, RP, 8>(p, sh.lds, x, y); break;
+            default: launch_slab_u<L, RP, 4>(p, sh.lds, x, y);
         }
-    } else if (rows) {
-        hipLaunchKernelGGL((csr_vec4_kernel<L, RP, true>), dim3((unsigned)blocks), dim3(256), 0, p->stream, nrows,
-                           rows, (const RP *)p->csr.row_ptr, p->csr.col, p->csr.val, x, y);
     } else {
         hipLaunchKernelGGL((csr_vec4_kernel<L, RP, false>), dim3((unsigned)blocks), dim3(256), sh.lds, p->stream,
-                           nrows, rows, (const RP *)p->csr.row_ptr, p->csr.col, p->csr.val, x, y);
+                           nrows, nullptr, (const RP *)p->csr.row_ptr, p->csr.col, p->csr.val, x, y);
     }
     SPMV_HIP_TRY(hipGetLastError());
     return SPMV_SUCCESS;
 }
 
 template <typename RP>
-static int launch_csr_lanes(const spmv_plan_s *p, int lanes, int64_t nrows, const int32_t *rows, const double *x,
-                            double *y) {
+static int launch_csr_lanes(const spmv_plan_s *p, int lanes, int64_t nrows, const double *x, double *y) {
     switch (lanes) {
-        case 1: return launch_csr_t<1, RP>(p, nrows, rows, x, y);
-        case 2: return launch_csr_t<2, RP>(p, nrows, rows, x, y);
-        case 4: return launch_csr_t<4, RP>(p, nrows, rows, x, y);
-        case 8: return launch_csr_t<8, RP>(p, nrows, rows, x, y);
-        case 16: return launch_csr_t<16, RP>(p, nrows, rows, x, y);
-        case 32: return launch_csr_t<32, RP>(p, nrows, rows, x, y);
-        case 64: return launch_csr_t<64, RP>(p, nrows, rows, x, y);
-        case 256:
-            if (nrows > 0) {
-                hipLaunchKernelGGL((csr_block_kernel<RP>), dim3((unsigned)nrows), dim3(256), 0, p->stream, rows,
-                                   (const RP *)p->csr.row_ptr, p->csr.col, p->csr.val, x, y);
-                SPMV_HIP_TRY(hipGetLastError());
-            }
-            return SPMV_SUCCESS;
+        case 1: return launch_csr_t<1, RP>(p, nrows, x, y);
+        case 2: return launch_csr_t<2, RP>(p, nrows, x, y);
+        case 4: return launch_csr_t<4, RP>(p, nrows, x, y);
+        case 8: return launch_csr_t<8, RP>(p, nrows, x, y);
+        case 16: return launch_csr_t<16, RP>(p, nrows, x, y);
+        case 32: return launch_csr_t<32, RP>(p, nrows, x, y);
+        case 64: return launch_csr_t<64, RP>(p, nrows, x, y);
         default: set_error("csr lanes must be a power of two in [1,64]"); return SPMV_ERROR_INVALID_VALUE;
     }
 }
@@ -486,7 +377,7 @@ static int launch_csr_lanes(const spmv_plan_s *p, int lanes, int64_t nrows, cons
 template <typename RP>
 static int launch_csr_rp(const spmv_plan_s *p, const double *x, double *y) {
     const CsrDev &c = p->csr;
-    if (!c.bin_rows) return launch_csr_lanes<RP>(p, c.lanes, p->m, nullptr, x, y);
+    if (!c.bin_rows) return launch_csr_lanes<RP>(p, c.lanes, p->m, x, y);
     // adaptive: every bin in one launch (workgroup ranges per bin)
     return launch_adaptive<RP, false>(p, c.bin_off, c.bin_rows, (const RP *)c.row_ptr, c.col, c.val, x, y, nullptr);
 }

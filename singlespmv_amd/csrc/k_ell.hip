@@ -13,12 +13,22 @@
 // slots carry val = 0 and repeat a real column of the row.  With PERM the
 // slices hold rows sorted by length (JDS, src/opt_jds.cpp:29-71, 91-103) and
 // y is written through the permutation.
+//
+// O32 (x below 4 GB, a slice below 2 GB): the wave's slice base is
+// wave-uniform (SGPR) and every load addresses it, or x, plus a 32-bit byte
+// offset (the global_load saddr form), instead of 64-bit per-lane addresses.
 #include "device.hpp"
 #include "internal.hpp"
 
 namespace spmv {
 
-template <int UNROLL, bool ADD, bool PERM>
+template <bool O32>
+__device__ __forceinline__ const char *ell_at(const void *base, int64_t byte_off) {
+    if constexpr (O32) return (const char *)base + (uint32_t)byte_off;
+    else return (const char *)base + byte_off;
+}
+
+template <int UNROLL, bool ADD, bool PERM, bool O32 = false>
 __global__ __launch_bounds__(256) void ell_slice_kernel(int64_t m, int64_t n_slices,
                                                         const int32_t *__restrict__ perm,
                                                         const int64_t *__restrict__ slice_off,
@@ -26,13 +36,21 @@ __global__ __launch_bounds__(256) void ell_slice_kernel(int64_t m, int64_t n_sli
                                                         const double *__restrict__ val,
                                                         const double *__restrict__ x,
                                                         double *__restrict__ y) {
-    const int64_t slice = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+    const int64_t slice = (int64_t)blockIdx.x * (blockDim.x / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (slice >= n_slices) return;
     const int64_t base = slice_off[slice];
     const int64_t quads = (slice_off[slice + 1] - base) >> 8;  // (width/4)
-    const int32_t *cp = col + base + lane * 4;
-    const double *vp = val + base + lane * 2;
+    const int32_t *cs = col + base;  // wave-uniform slice bases
+    const double *vs = val + base;
+    auto ldc = [&](int64_t q) { return ld_stream4((const int32_t *)ell_at<O32>(cs, (q * 256 + lane * 4) * 4)); };
+    auto ldv = [&](int64_t q, int h) {
+        return ld_stream2((const double *)ell_at<O32>(vs, (q * 256 + h * 128 + lane * 2) * 8));
+    };
+    auto ldx = [&](int c) -> double {
+        if constexpr (O32) return *(const double *)((const char *)x + (uint32_t)c * 8u);
+        else return ld_x(x, c);
+    };
     double acc = 0.0;
     int64_t q = 0;
     for (; q + UNROLL <= quads; q += UNROLL) {
@@ -40,17 +58,17 @@ __global__ __launch_bounds__(256) void ell_slice_kernel(int64_t m, int64_t n_sli
         f64x2 a[UNROLL], b[UNROLL];
 #pragma unroll
         for (int u = 0; u < UNROLL; ++u) {
-            c[u] = ld_stream4(cp + (q + u) * 256);
-            a[u] = ld_stream2(vp + (q + u) * 256);
-            b[u] = ld_stream2(vp + (q + u) * 256 + 128);
+            c[u] = ldc(q + u);
+            a[u] = ldv(q + u, 0);
+            b[u] = ldv(q + u, 1);
         }
         double g[UNROLL][4];
 #pragma unroll
         for (int u = 0; u < UNROLL; ++u) {
-            g[u][0] = ld_x(x, c[u].x);
-            g[u][1] = ld_x(x, c[u].y);
-            g[u][2] = ld_x(x, c[u].z);
-            g[u][3] = ld_x(x, c[u].w);
+            g[u][0] = ldx(c[u].x);
+            g[u][1] = ldx(c[u].y);
+            g[u][2] = ldx(c[u].z);
+            g[u][3] = ldx(c[u].w);
         }
 #pragma unroll
         for (int u = 0; u < UNROLL; ++u) {
@@ -61,10 +79,10 @@ __global__ __launch_bounds__(256) void ell_slice_kernel(int64_t m, int64_t n_sli
         }
     }
     for (; q < quads; ++q) {
-        const i32x4 c = ld_stream4(cp + q * 256);
-        const f64x2 a = ld_stream2(vp + q * 256);
-        const f64x2 b = ld_stream2(vp + q * 256 + 128);
-        const double g0 = ld_x(x, c.x), g1 = ld_x(x, c.y), g2 = ld_x(x, c.z), g3 = ld_x(x, c.w);
+        const i32x4 c = ldc(q);
+        const f64x2 a = ldv(q, 0);
+        const f64x2 b = ldv(q, 1);
+        const double g0 = ldx(c.x), g1 = ldx(c.y), g2 = ldx(c.z), g3 = ldx(c.w);
         acc = madd(a.x, g0, acc);
         acc = madd(a.y, g1, acc);
         acc = madd(b.x, g2, acc);
@@ -74,20 +92,30 @@ __global__ __launch_bounds__(256) void ell_slice_kernel(int64_t m, int64_t n_sli
     if (srow < m) {
         const int64_t row = PERM ? (int64_t)perm[srow] : srow;  // JDS: back to matrix order
         if (ADD) y[row] = __dadd_rn(y[row], acc);
-        else y[row] = acc;
+        else if (PERM) y[row] = acc;
+        else __builtin_nontemporal_store(acc, y + row);  // not re-read: streamed out
     }
+}
+
+template <int U, bool O32>
+static void launch_ell_uo(const spmv_plan_s *p, const double *x, double *y, size_t lds) {
+    const EllDev &e = p->ell;
+    const int64_t blocks = (e.n_slices + 3) / 4;
+    if (e.perm)
+        hipLaunchKernelGGL((ell_slice_kernel<U, false, true, O32>), dim3((unsigned)blocks), dim3(256), lds,
+                           p->stream, p->m, e.n_slices, e.perm, e.slice_off, e.col, e.val, x, y);
+    else
+        hipLaunchKernelGGL((ell_slice_kernel<U, false, false, O32>), dim3((unsigned)blocks), dim3(256), lds,
+                           p->stream, p->m, e.n_slices, e.perm, e.slice_off, e.col, e.val, x, y);
 }
 
 template <int U>
 static void launch_ell_u(const spmv_plan_s *p, const double *x, double *y, size_t lds) {
-    const EllDev &e = p->ell;
-    const int64_t blocks = (e.n_slices + 3) / 4;
-    if (e.perm)
-        hipLaunchKernelGGL((ell_slice_kernel<U, false, true>), dim3((unsigned)blocks), dim3(256), lds, p->stream,
-                           p->m, e.n_slices, e.perm, e.slice_off, e.col, e.val, x, y);
-    else
-        hipLaunchKernelGGL((ell_slice_kernel<U, false, false>), dim3((unsigned)blocks), dim3(256), lds,
-                           p->stream, p->m, e.n_slices, e.perm, e.slice_off, e.col, e.val, x, y);
+    // 32-bit offsets: x below 4 GB and a slice's values below 2 GB
+    bool o32 = p->n < ((int64_t)1 << 29) && (int64_t)p->ell.max_width * 64 * 8 < ((int64_t)1 << 31);
+    if (const char *v = probe_env("SPMV_LAUNCH_ELL_O32")) o32 = o32 && std::atoi(v) != 0;
+    if (o32) launch_ell_uo<U, true>(p, x, y, lds);
+    else launch_ell_uo<U, false>(p, x, y, lds);
 }
 
 int launch_ell(const spmv_plan_s *p, const double *x, double *y) {
