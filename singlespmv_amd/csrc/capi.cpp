@@ -22,7 +22,7 @@ const char *last_error() { return g_err.c_str(); }
 // AUTO maps every array of >= kStreamVmmMinBytes into 2-MB VMM handles
 // (config 4, same launches on both placements, interleaved in one process:
 // CSR 2.95 -> 2.81 ms, ELL 2.57 -> 2.40; profiles/round4/probe/
-// c4_csr_ell_launch_variants.jsonl), VMM does so from 32 MB, PLAIN never.
+// c4_csr_vec4_slab_caps_vmm_plain.jsonl, c4_ell_caps_unroll_vmm_plain.jsonl), VMM does so from 32 MB, PLAIN never.
 static void stream_placement(spmv_plan_s *p, int fmt, const spmv_options_t &o) {
     if (fmt == SPMV_FORMAT_BIN || fmt == SPMV_FORMAT_DIA) return;
     if (o.placement == SPMV_PLACEMENT_AUTO) p->arena.vmm_min = kStreamVmmMinBytes;

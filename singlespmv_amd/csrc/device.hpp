@@ -8,6 +8,7 @@
 namespace spmv {
 
 typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
+typedef int32_t i32x2 __attribute__((ext_vector_type(2)));
 typedef double f64x2 __attribute__((ext_vector_type(2)));
 
 // Streamed matrix data (col/val) is read exactly once per SpMV: load it with

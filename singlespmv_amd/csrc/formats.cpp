@@ -289,6 +289,31 @@ int csr_plan_lanes(spmv_plan_s *p, const int64_t *row_ptr, int64_t m, const spmv
     return upload(p, &c.bin_rows, rows.data(), m);
 }
 
+// x windows of csr_slabx's kCsrWinRows-row workgroups (k_csr.hip):
+// the column span of each workgroup's entries; kept when every span fits
+// kCsrMaxWin columns (banded matrices), else none.
+static int csr_x_windows(spmv_plan_s *p, const HostCsr &A) {
+    CsrDev &c = p->csr;
+    const int64_t nwg = (A.m + kCsrWinRows - 1) / kCsrWinRows;
+    std::vector<int32_t> w0((size_t)std::max<int64_t>(nwg, 1), 0);
+    int64_t span = 1;
+#pragma omp parallel for schedule(static) reduction(max : span)
+    for (int64_t b = 0; b < nwg; ++b) {
+        const int64_t e0 = A.row_ptr[b * kCsrWinRows], e1 = A.row_ptr[std::min<int64_t>(A.m, (b + 1) * kCsrWinRows)];
+        int32_t lo = std::numeric_limits<int32_t>::max(), hi = -1;
+        for (int64_t j = e0; j < e1; ++j) {
+            lo = std::min(lo, A.col[j]);
+            hi = std::max(hi, A.col[j]);
+        }
+        if (hi < 0) lo = hi = 0;
+        w0[(size_t)b] = lo;
+        span = std::max<int64_t>(span, (int64_t)hi - lo + 1);
+    }
+    if (span > kCsrMaxWin || nwg == 0) return SPMV_SUCCESS;
+    c.win = (int32_t)span;
+    return upload(p, &c.win0, w0.data(), nwg);
+}
+
 int build_csr(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
     CsrDev &c = p->csr;
     // 64-bit row pointers from 2^31 entries on; SPMV_CSR_FORCE_RP64 (internal)
@@ -305,6 +330,7 @@ int build_csr(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
     SPMV_RETURN_IF(upload(p, &c.col, A.col, A.nnz, kPad));
     SPMV_RETURN_IF(upload(p, &c.val, A.val, A.nnz, kPad));
     SPMV_RETURN_IF(csr_plan_lanes(p, A.row_ptr, A.m, o));
+    if (c.lanes > 0) SPMV_RETURN_IF(csr_x_windows(p, A));
     csr_finish_info(p);
     return SPMV_SUCCESS;
 }
@@ -363,6 +389,27 @@ int build_ell(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &, int cap,
         }
     }
     SPMV_RETURN_IF(upload(p, &e.slice_off, off.data(), e.n_slices + 1));
+    if (!order) {  // x windows of 4-slice workgroups (ell_slicex, k_ell.hip); the slots' columns
+        const int64_t nwg = (e.n_slices + 3) / 4;  // are real columns of their rows (padding repeats one)
+        std::vector<int32_t> w0((size_t)std::max<int64_t>(nwg, 1), 0);
+        int64_t span = 1;
+#pragma omp parallel for schedule(static) reduction(max : span)
+        for (int64_t b = 0; b < nwg; ++b) {
+            const int64_t j0 = off[(size_t)(4 * b)], j1 = off[(size_t)std::min<int64_t>(e.n_slices, 4 * b + 4)];
+            int32_t lo = std::numeric_limits<int32_t>::max(), hi = -1;
+            for (int64_t j = j0; j < j1; ++j) {
+                lo = std::min(lo, col[(size_t)j]);
+                hi = std::max(hi, col[(size_t)j]);
+            }
+            if (hi < 0) lo = hi = 0;
+            w0[(size_t)b] = lo;
+            span = std::max<int64_t>(span, (int64_t)hi - lo + 1);
+        }
+        if (span <= kCsrMaxWin && nwg > 0) {
+            e.win = (int32_t)span;
+            SPMV_RETURN_IF(upload(p, &e.win0, w0.data(), nwg));
+        }
+    }
     SPMV_RETURN_IF(upload(p, &e.col, col.data(), total));
     SPMV_RETURN_IF(upload(p, &e.val, val.data(), total));
     e.max_width = maxw;

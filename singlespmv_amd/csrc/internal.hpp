@@ -123,6 +123,8 @@ constexpr int kPad = 8;
 // bin b summed by kCsrBinLanes[b] lanes per row (256 = one workgroup per row).
 constexpr int kCsrBins = 8;
 constexpr int kCsrBinLanes[kCsrBins] = {1, 2, 4, 8, 16, 32, 64, 256};
+constexpr int kCsrMaxWin = 4096;   // columns of a csr_slabx / ell_slicex x window (32 KB of LDS)
+constexpr int kCsrWinRows = 512;  // rows of a csr_slabx workgroup (4 waves x 2 slabs of 64)
 struct CsrDev {
     void *row_ptr = nullptr;  // int32 or int64 [m+1]
     bool rp64 = false;
@@ -131,6 +133,8 @@ struct CsrDev {
     int lanes = 4;            // lanes per row (1..64); 0 = adaptive (bins)
     bool off32 = false;       // every 64-row slab spans < 2^28 entries and n < 2^29:
                               // 32-bit byte offsets in csr_slab2 (k_csr.hip)
+    int32_t *win0 = nullptr;  // [ceil(m / kCsrWinRows)]: first column of each workgroup's
+    int32_t win = 0;          //   x window of `win` columns (null: no window fits kCsrMaxWin)
     int32_t *bin_rows = nullptr;        // rows of every bin, ascending within a bin
     int64_t bin_off[kCsrBins + 1] = {};  // host: bin b = bin_rows[bin_off[b], bin_off[b+1])
 };
@@ -149,6 +153,8 @@ struct EllDev {
     int32_t *col = nullptr;
     double *val = nullptr;
     int max_width = 0;
+    int32_t *win0 = nullptr;       // [ceil(n_slices / 4)]: x window of each 4-slice workgroup
+    int32_t win = 0;               //   (columns; null: no window fits kCsrMaxWin)
     int unroll = 2;  // quads per lane per iteration (SPMV_ELL_UNROLL, internal;
                      // 2 beat 4 by 28 % at config 4, 5 % at config 2)
 };

@@ -63,7 +63,7 @@ __global__ __launch_bounds__(256) void csr_vec4_kernel(int64_t m, const int32_t 
 // same butterfly: bit-identical y), U steps' col / val loads issued before
 // their gathers.  A long-lived wave replaces 64 / (256 / L) short ones and y
 // leaves in one coalesced store per wave (config 4, same plans: csr_vec4<16>
-// 2.82 -> 2.48 ms, profiles/round4/probe/).  No divergent control flow on the
+// 2.82 -> 2.48 ms, profiles/round4/probe/c4_csr_slab2_first.jsonl).  No divergent control flow on the
 // common path.  Lanes past their row's end load the row's first chunk again (same
 // lines, no new traffic) and every loaded column is a real column (plan
 // creation validated them; the kPad tail is zero), so the col / val loads
@@ -181,6 +181,189 @@ __global__ __launch_bounds__(256) void csr_slab2_kernel(int64_t m, const RP *__r
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     if (rl < m) __builtin_nontemporal_store(ysl[wv][lane], y + rl);
+}
+
+// csr_slabx<L, U, S, O32>: csr_slab2 for matrices whose rows stay near the
+// diagonal (banded, config 4).  A workgroup owns 256 S consecutive rows (each
+// wave S consecutive 64-row slabs) and reads x over one column window
+// [win0[wg], win0[wg] + win) (host-computed, CsrDev::win0 for 256 S-row
+// groups); it is staged into LDS once, so the x reads are LDS reads
+// (lgkmcnt) and no longer share the in-order vmcnt queue with the col / val
+// stream -- which lets the stream run one batch ahead: batch i + 1's loads
+// (the next slab's first one included) are in flight while batch i's x reads
+// and adds run (A / B ping-pong, as BIN's kernels), and the first batch is
+// issued before the window is staged.  Same chunks, same order, same
+// butterfly as csr_slab2: bit-identical y.  Lanes whose loaded entry lies
+// outside the window (masked entries of a neighbouring row) read a clamped,
+// in-window slot.
+template <int L, int U>
+struct CsrBatch {
+    i32x4 c[U];
+    f64x2 a[U], b[U];
+    int s[U], len[U];  // the row's start (relative to the wave's base) and length
+    bool full;
+};
+
+// PAIRS: lane gl of a group takes the chunk's entries 2 gl, 2 gl + 1 and
+// 2L + 2 gl, 2L + 2 gl + 1 (two 8-byte column and two 16-byte value loads)
+// instead of 4 gl .. 4 gl + 3: every value load instruction then reads whole
+// 128-byte lines (16 L contiguous bytes per group; the 4-entry mapping's two
+// value loads each read half of every line of a 32 L-byte span, twice the
+// L1 -> L2 line requests).  The lane's four entries are added in that order
+// (a different rounding from csr_slab2 for L > 1; L = 1 is the sequential
+// sum either way).
+template <int L, typename RP, int U, int S, bool O32, bool PAIRS = false>
+__global__ __launch_bounds__(256) void csr_slabx_kernel(int64_t m, const RP *__restrict__ rp,
+                                                        const int32_t *__restrict__ col,
+                                                        const double *__restrict__ val,
+                                                        const double *__restrict__ x, double *__restrict__ y,
+                                                        const int32_t *__restrict__ win0, int32_t win, int64_t n) {
+    constexpr int R = 64 / L;   // rows per step
+    constexpr int NB = L / U;   // batches per slab
+    extern __shared__ double xs[];  // [win]
+    __shared__ double ysl[4][64];
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int g = lane / L, gl = lane & (L - 1);
+    // the wave's slabs: rows r0 + 64 k, k < S (r0 >= m: no rows, but the wave
+    // still helps stage the window and meets the barrier)
+    const int64_t r0 = ((int64_t)blockIdx.x * 4 + wv) * 64 * S;
+    const int64_t rbase = r0 < m ? r0 : m;
+    const int64_t base = (int64_t)rp[rbase] & ~(int64_t)3;
+    int rpl[S], rpe[S];
+#pragma unroll
+    for (int k = 0; k < S; ++k) {
+        const int64_t rk = r0 + 64 * k + lane, ek = r0 + 64 * (k + 1);
+        rpl[k] = (int)((int64_t)rp[rk < m ? rk : m] - base);
+        rpe[k] = (int)((int64_t)rp[ek < m ? ek : m] - base);
+    }
+    const int32_t *cb = col + base;
+    const double *vb = val + base;
+    auto load = [&](CsrBatch<L, U> &B, int i) {  // batch i: slab i / NB, steps (i % NB) U ..
+        const int k = i / NB, st = (i % NB) * U;
+        B.full = true;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int li = (st + u) * R + g;
+            const int s = __shfl(rpl[k], li, 64);
+            const int nx = __shfl(rpl[k], (li + 1) & 63, 64);
+            const int e = li == 63 ? rpe[k] : nx;
+            const int a0 = s & ~3;
+            B.s[u] = s;
+            B.len[u] = e - s;
+            B.full = B.full && (s & 3) == 0 && B.len[u] == 4 * L;
+            if constexpr (PAIRS) {
+                const int ja = a0 + 2 * gl, jb = a0 + 2 * L + 2 * gl;
+                const int la = ja < e ? ja : a0, lb = jb < e ? jb : a0;
+                const i32x2 ca = __builtin_nontemporal_load((const i32x2 *)at_bytes<O32>(cb, la, 4));
+                const i32x2 cc = __builtin_nontemporal_load((const i32x2 *)at_bytes<O32>(cb, lb, 4));
+                B.c[u] = i32x4{ca.x, ca.y, cc.x, cc.y};
+                B.a[u] = ld_stream2((const double *)at_bytes<O32>(vb, la, 8));
+                B.b[u] = ld_stream2((const double *)at_bytes<O32>(vb, lb, 8));
+            } else {
+                const int j0 = a0 + 4 * gl;
+                const int jl = j0 < e ? j0 : a0;
+                B.c[u] = ld_stream4((const int32_t *)at_bytes<O32>(cb, jl, 4));
+                B.a[u] = ld_stream2((const double *)at_bytes<O32>(vb, jl, 8));
+                B.b[u] = ld_stream2((const double *)at_bytes<O32>(vb, jl + 2, 8));
+            }
+        }
+    };
+    const int64_t c0 = win0[blockIdx.x];
+    const uint32_t wmax = (uint32_t)win - 1;
+    auto xw = [&](int c) -> double {
+        const uint32_t i = (uint32_t)((int64_t)c - c0);
+        return xs[i < wmax ? i : wmax];
+    };
+    auto compute = [&](const CsrBatch<L, U> &B, int i) {
+        const int k = i / NB, st = (i % NB) * U;
+        double gx[U][4];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            gx[u][0] = xw(B.c[u].x);
+            gx[u][1] = xw(B.c[u].y);
+            gx[u][2] = xw(B.c[u].z);
+            gx[u][3] = xw(B.c[u].w);
+        }
+        const bool all_full = __ballot(!B.full) == 0;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            double acc = 0.0, t;
+            if (all_full) {
+                acc = madd(B.a[u].x, gx[u][0], acc);
+                acc = madd(B.a[u].y, gx[u][1], acc);
+                acc = madd(B.b[u].x, gx[u][2], acc);
+                acc = madd(B.b[u].y, gx[u][3], acc);
+            } else {
+                // positions of the lane's 4 entries relative to the row start
+                const int a0 = B.s[u] & ~3;
+                const int ra = (PAIRS ? a0 + 2 * gl : a0 + 4 * gl) - B.s[u];
+                const int rb = ra + (PAIRS ? 2 * L : 2);
+                t = madd(B.a[u].x, gx[u][0], acc);
+                acc = (unsigned)(ra + 0) < (unsigned)B.len[u] ? t : acc;
+                t = madd(B.a[u].y, gx[u][1], acc);
+                acc = (unsigned)(ra + 1) < (unsigned)B.len[u] ? t : acc;
+                t = madd(B.b[u].x, gx[u][2], acc);
+                acc = (unsigned)(rb + 0) < (unsigned)B.len[u] ? t : acc;
+                t = madd(B.b[u].y, gx[u][3], acc);
+                acc = (unsigned)(rb + 1) < (unsigned)B.len[u] ? t : acc;
+                const int e = B.s[u] + B.len[u];  // the row's end
+                // rows longer than one chunk of the group: the rest in order
+                for (int jj = a0 + 4 * gl + 4 * L; jj < e; jj += 4 * L) {
+                    const i32x4 cc = ld_stream4((const int32_t *)at_bytes<O32>(cb, jj, 4));
+                    const f64x2 v01 = ld_stream2((const double *)at_bytes<O32>(vb, jj, 8));
+                    const f64x2 v23 = ld_stream2((const double *)at_bytes<O32>(vb, jj + 2, 8));
+                    const double x0 = xw(cc.x), x1 = xw(cc.y), x2 = xw(cc.z), x3 = xw(cc.w);
+                    acc = madd(v01.x, x0, acc);
+                    t = madd(v01.y, x1, acc);
+                    acc = jj + 1 < e ? t : acc;
+                    t = madd(v23.x, x2, acc);
+                    acc = jj + 2 < e ? t : acc;
+                    t = madd(v23.y, x3, acc);
+                    acc = jj + 3 < e ? t : acc;
+                }
+            }
+            acc = group_sum_dpp<L>(acc);
+            if (gl == 0) ysl[wv][(st + u) * R + g] = acc;
+        }
+        if (i % NB == NB - 1) {  // the slab is done: its 64 sums leave in one coalesced store
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const int64_t rl = r0 + 64 * k + lane;
+            if (rl < m) __builtin_nontemporal_store(ysl[wv][lane], y + rl);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+    };
+    // the wave's batches: all S slabs while their rows exist
+    const int nb = r0 >= m ? 0 : (int)std::min<int64_t>(S, (m - r0 + 63) / 64) * NB;
+    CsrBatch<L, U> A, B;
+    // window staging: its loads go out first, then the first batch's, so
+    // both are in flight together
+    constexpr int XT = 4;  // window values per thread held in flight (win <= 256 XT: one pass)
+    double t[XT];
+#pragma unroll
+    for (int q = 0; q < XT; ++q) {
+        const int i = threadIdx.x + q * 256;
+        t[q] = i < win ? x[c0 + i < n ? c0 + i : n - 1] : 0.0;
+    }
+    if (nb > 0) load(A, 0);
+#pragma unroll
+    for (int q = 0; q < XT; ++q) {
+        const int i = threadIdx.x + q * 256;
+        if (i < win) xs[i] = t[q];
+    }
+    for (int i = threadIdx.x + XT * 256; i < win; i += 256) xs[i] = x[c0 + i < n ? c0 + i : n - 1];
+    __syncthreads();
+    for (int i = 0; i < nb; i += 2) {
+        if (i + 1 < nb) load(B, i + 1);
+        compute(A, i);
+        if (i + 1 >= nb) break;
+        if (i + 2 < nb) load(A, i + 2);
+        compute(B, i + 1);
+    }
 }
 
 // Adaptive CSR in ONE launch: workgroup ranges map to the length bins
@@ -310,7 +493,8 @@ static int launch_adaptive(const spmv_plan_s *p, const int64_t *bin_off, const i
 
 // launch-time shape of the row-parallel CSR kernels: csr_slab2 with U =
 // min(4, L) steps per batch (config 4, 16 lanes: U = 1 / 2 / 4 / 8 ran
-// 2.64 / 2.55 / 2.49 / 2.54 ms; config 2 within 1 %; profiles/round4/probe/).
+// 2.64 / 2.55 / 2.49 / 2.54 ms; config 2 within 1 %; profiles/round4/probe/
+// c4_csr_slab2_first.jsonl, c2_csr_slab2_slabx.jsonl).
 // The probe build reads SPMV_LAUNCH_CSR (0: csr_vec4, the round-3 kernel),
 // SPMV_LAUNCH_CSR_U and SPMV_LAUNCH_CSR_LDS_KB at every launch, so variants
 // are A/B'd on one plan's memory.
@@ -328,9 +512,27 @@ static CsrLaunch csr_launch_shape() {
 }
 
 template <int L, typename RP, int U>
-static void launch_slab_u(const spmv_plan_s *p, size_t lds, const double *x, double *y) {
+static void launch_slab_u(const spmv_plan_s *p, int kind, size_t lds, const double *x, double *y) {
     constexpr int UU = U < L ? U : L;
     const int64_t waves = (p->m + 63) / 64;
+    const CsrDev &c = p->csr;
+    if (kind >= 3 && c.win0) {  // x window in LDS, stream one batch ahead (4: entry pairs)
+        constexpr int S = kCsrWinRows / 256;
+        const size_t wl = std::max(lds, sizeof(double) * (size_t)c.win);
+        const unsigned grid = (unsigned)((p->m + kCsrWinRows - 1) / kCsrWinRows);
+        auto go = [&](auto kern) {
+            hipLaunchKernelGGL(kern, dim3(grid), dim3(256), wl, p->stream, p->m, (const RP *)c.row_ptr, c.col, c.val,
+                               x, y, c.win0, c.win, p->n);
+        };
+        if (kind == 4) {
+            if (c.off32) go(csr_slabx_kernel<L, RP, UU, S, true, true>);
+            else go(csr_slabx_kernel<L, RP, UU, S, false, true>);
+        } else {
+            if (c.off32) go(csr_slabx_kernel<L, RP, UU, S, true, false>);
+            else go(csr_slabx_kernel<L, RP, UU, S, false, false>);
+        }
+        return;
+    }
     if (p->csr.off32)
         hipLaunchKernelGGL((csr_slab2_kernel<L, RP, UU, true>), dim3((unsigned)((waves + 3) / 4)), dim3(256), lds,
                            p->stream, p->m, (const RP *)p->csr.row_ptr, p->csr.col, p->csr.val, x, y);
@@ -347,10 +549,10 @@ static int launch_csr_t(const spmv_plan_s *p, int64_t nrows, const double *x, do
     const CsrLaunch sh = csr_launch_shape();
     if (sh.slab) {
         switch (sh.u) {
-            case 1: launch_slab_u<L, RP, 1>(p, sh.lds, x, y); break;
-            case 2: launch_slab_u<L, RP, 2>(p, sh.lds, x, y); break;
-            case 8: launch_slab_u<L, RP, 8>(p, sh.lds, x, y); break;
-            default: launch_slab_u<L, RP, 4>(p, sh.lds, x, y);
+            case 1: launch_slab_u<L, RP, 1>(p, sh.slab, sh.lds, x, y); break;
+            case 2: launch_slab_u<L, RP, 2>(p, sh.slab, sh.lds, x, y); break;
+            case 8: launch_slab_u<L, RP, 8>(p, sh.slab, sh.lds, x, y); break;
+            default: launch_slab_u<L, RP, 4>(p, sh.slab, sh.lds, x, y);
         }
     } else {
         hipLaunchKernelGGL((csr_vec4_kernel<L, RP, false>), dim3((unsigned)blocks), dim3(256), sh.lds, p->stream,

@@ -49,6 +49,9 @@ def test_two_rank_bench_flow(config, fmts, launch):
     if config == "c2":  # equal slices: the iterative all_gather(y -> next x) step
         assert d["iterative"] is not None and d["iterative"]["ms_per_iter"] > 0
     assert [p["rank"] for p in d["per_rank"]] == [0, 1]
+    for p in d["per_rank"]:  # the multi-GPU rehearsal record: setup time and memory per rank
+        assert p["setup_s_to_first_trial"] > 0 and p["peak_rss_gb"] > 0 and p["headline_plan_device_gb"] > 0
+        assert p["device_used_gb_after_build"] >= p["headline_plan_device_gb"]
 
 
 @pytest.mark.parametrize("ranks", [2, 4])

@@ -13,6 +13,8 @@
 #   prof_c2|prof_c3|prof_c4|prof_simN
 #                     rocprofv3 kernel trace + FETCH_SIZE / WRITE_SIZE passes
 #                     (tools/profile_round.sh) of the headline plan of that shape
+#   prof:<cfg>:<fmt>  the same for ONE format of config <cfg> (c2|c3|c4)
+#   rehearsal8        bench.py --gpus 8 at the config-5 shape, 8 gloo ranks on one GPU
 #   gloo2_c3          the self-launched 2-rank bench (gloo, one GPU) with --verify
 #   py:<script args>  python3 -u <script args> (a tools/ probe), stdout to <step>.log
 #   exe:<binary args>  a stand-alone probe binary (bin/region_probe ...)
@@ -50,6 +52,17 @@ for step in "$@"; do
     prof_sim[0-9]*)
       timeout -k 10 1000 bash tools/profile_round.sh "${OUTNAME}_${step#prof_}" --sim-world "${step#prof_sim}" \
           --formats auto --only-config --steps 20 --warmup 5 --trials 3 > "$O/$tag.log" 2>&1 ;;
+    prof:*)
+      # prof:<config>:<format>: one format of one config per profile (PMC keys
+      # name the kernels of one execute, tools/pmc_summary.py)
+      spec=${step#prof:}; cfg=${spec%%:*}; fmt=${spec#*:}
+      timeout -k 10 1000 bash tools/profile_round.sh "${OUTNAME}_${cfg}_${fmt}" --config "$cfg" \
+          --formats "$fmt" --only-config --steps 20 --warmup 5 --trials 3 > "$O/$tag.log" 2>&1 ;;
+    rehearsal8)
+      # the 8-rank flow at the config-5 shape on ONE GPU (gloo: the ranks share
+      # the device; kernel times are meaningless, setup time / memory are not)
+      BENCH_DIST_BACKEND=gloo timeout -k 10 1100 python3 -u bench.py --gpus 8 --steps 3 --warmup 1 --trials 1 \
+          > "$O/$tag.json" 2> "$O/$tag.err" ;;
     gloo2_c3)
       BENCH_DIST_BACKEND=gloo timeout -k 10 400 python3 -u bench.py --gpus 2 --config c3 --rows 500000 \
           --formats auto --no-cpu --only-config --verify > "$O/$tag.json" 2> "$O/$tag.err" ;;
