@@ -193,7 +193,7 @@ void csr_finish_info(spmv_plan_s *p) {
     p->algo_bytes = 12 * p->nnz + (c.rp64 ? 8 : 4) * (p->m + 1) + 8 * p->n + 8 * p->m;
     p->n_kernels = 1;
     if (c.lanes > 0) {
-        p->kernel_name = "csr_slab2_kernel<" + std::to_string(c.lanes) + ">";
+        p->kernel_name = std::string(c.win0 ? "csr_slabx_kernel<" : "csr_slab2_kernel<") + std::to_string(c.lanes) + ">";
     } else {
         p->kernel_name = "csr_adaptive_kernel";
         p->algo_bytes += 4 * p->m;  // the bins' row lists

@@ -10,6 +10,7 @@
 //        by binary search, and the 64-lane x sigma tile transpose.
 // Unlike CSR5's in-place transpose (anonymouslib_cuda.h:203-204) the
 // caller's arrays are never modified.
+#include <algorithm>
 #include <cstdlib>
 #include <vector>
 
@@ -17,6 +18,8 @@
 #include "internal.hpp"
 
 namespace spmv {
+
+int csr_x_windows_device(spmv_plan_s *p, const int64_t *d_rp);
 
 namespace {
 
@@ -241,7 +244,65 @@ int build_csr_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, 
     std::vector<int64_t> hrp((size_t)p->m + 1);
     SPMV_HIP_TRY(hipMemcpy(hrp.data(), d_rp, 8 * (size_t)(p->m + 1), hipMemcpyDeviceToHost));
     SPMV_RETURN_IF(csr_plan_lanes(p, hrp.data(), p->m, o));
+    if (c.lanes > 0) SPMV_RETURN_IF(csr_x_windows_device(p, d_rp));
     csr_finish_info(p);
+    return SPMV_SUCCESS;
+}
+
+// csr_x_windows on the device (formats.cpp): the column span [lo, hi] of each
+// kCsrWinRows-row workgroup's entries, one workgroup per window
+__global__ __launch_bounds__(256) void csr_window_kernel(const int64_t *__restrict__ rp, int64_t m,
+                                                         const int32_t *__restrict__ col, int32_t *__restrict__ lo,
+                                                         int32_t *__restrict__ span) {
+    __shared__ int32_t smin[256], smax[256];
+    const int64_t b = blockIdx.x;
+    const int64_t e0 = rp[b * kCsrWinRows];
+    const int64_t r1 = (b + 1) * kCsrWinRows < m ? (b + 1) * kCsrWinRows : m;
+    const int64_t e1 = rp[r1];
+    int32_t mn = INT32_MAX, mx = -1;
+    for (int64_t j = e0 + threadIdx.x; j < e1; j += 256) {
+        const int32_t c = col[j];
+        mn = c < mn ? c : mn;
+        mx = c > mx ? c : mx;
+    }
+    smin[threadIdx.x] = mn;
+    smax[threadIdx.x] = mx;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (threadIdx.x < o) {
+            smin[threadIdx.x] = min(smin[threadIdx.x], smin[threadIdx.x + o]);
+            smax[threadIdx.x] = max(smax[threadIdx.x], smax[threadIdx.x + o]);
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        const bool empty = smax[0] < 0;
+        lo[b] = empty ? 0 : smin[0];
+        span[b] = empty ? 1 : smax[0] - smin[0] + 1;
+    }
+}
+
+int csr_x_windows_device(spmv_plan_s *p, const int64_t *d_rp) {
+    CsrDev &c = p->csr;
+    const int64_t nwg = (p->m + kCsrWinRows - 1) / kCsrWinRows;
+    if (nwg == 0) return SPMV_SUCCESS;
+    int32_t *lo = nullptr, *span = nullptr;
+    SPMV_RETURN_IF(p->arena.alloc((void **)&lo, sizeof(int32_t) * (size_t)nwg));
+    SPMV_HIP_TRY(hipMalloc(&span, sizeof(int32_t) * (size_t)nwg));
+    hipLaunchKernelGGL(csr_window_kernel, dim3((unsigned)nwg), dim3(256), 0, p->stream, d_rp, p->m, c.col, lo, span);
+    std::vector<int32_t> hs((size_t)nwg);
+    const hipError_t e1 = hipGetLastError();
+    const hipError_t e2 = e1 == hipSuccess ? hipMemcpy(hs.data(), span, sizeof(int32_t) * (size_t)nwg,
+                                                       hipMemcpyDeviceToHost) : e1;
+    (void)hipFree(span);
+    SPMV_HIP_TRY(e2);
+    const int32_t w = *std::max_element(hs.begin(), hs.end());
+    if (w > kCsrMaxWin) {
+        p->arena.free(lo);
+        return SPMV_SUCCESS;
+    }
+    c.win0 = lo;
+    c.win = w;
     return SPMV_SUCCESS;
 }
 
@@ -317,7 +378,7 @@ int build_ss_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, c
     p->empty_rows = s.n_empty;
     p->algo_bytes = 12 * nnz + 8 * p->n + 8 * m;
     p->n_kernels = 2;
-    p->kernel_name = "ss_tile_kernel<" + std::to_string(s.sigma) + ">";
+    p->kernel_name = "ss_tile_kernel<" + std::to_string(s.sigma) + ">+ss_fixup_kernel";
     return SPMV_SUCCESS;
 }
 

@@ -204,15 +204,7 @@ struct CsrBatch {
     bool full;
 };
 
-// PAIRS: lane gl of a group takes the chunk's entries 2 gl, 2 gl + 1 and
-// 2L + 2 gl, 2L + 2 gl + 1 (two 8-byte column and two 16-byte value loads)
-// instead of 4 gl .. 4 gl + 3: every value load instruction then reads whole
-// 128-byte lines (16 L contiguous bytes per group; the 4-entry mapping's two
-// value loads each read half of every line of a 32 L-byte span, twice the
-// L1 -> L2 line requests).  The lane's four entries are added in that order
-// (a different rounding from csr_slab2 for L > 1; L = 1 is the sequential
-// sum either way).
-template <int L, typename RP, int U, int S, bool O32, bool PAIRS = false>
+template <int L, typename RP, int U, int S, bool O32>
 __global__ __launch_bounds__(256) void csr_slabx_kernel(int64_t m, const RP *__restrict__ rp,
                                                         const int32_t *__restrict__ col,
                                                         const double *__restrict__ val,
@@ -252,21 +244,11 @@ __global__ __launch_bounds__(256) void csr_slabx_kernel(int64_t m, const RP *__r
             B.s[u] = s;
             B.len[u] = e - s;
             B.full = B.full && (s & 3) == 0 && B.len[u] == 4 * L;
-            if constexpr (PAIRS) {
-                const int ja = a0 + 2 * gl, jb = a0 + 2 * L + 2 * gl;
-                const int la = ja < e ? ja : a0, lb = jb < e ? jb : a0;
-                const i32x2 ca = __builtin_nontemporal_load((const i32x2 *)at_bytes<O32>(cb, la, 4));
-                const i32x2 cc = __builtin_nontemporal_load((const i32x2 *)at_bytes<O32>(cb, lb, 4));
-                B.c[u] = i32x4{ca.x, ca.y, cc.x, cc.y};
-                B.a[u] = ld_stream2((const double *)at_bytes<O32>(vb, la, 8));
-                B.b[u] = ld_stream2((const double *)at_bytes<O32>(vb, lb, 8));
-            } else {
-                const int j0 = a0 + 4 * gl;
-                const int jl = j0 < e ? j0 : a0;
-                B.c[u] = ld_stream4((const int32_t *)at_bytes<O32>(cb, jl, 4));
-                B.a[u] = ld_stream2((const double *)at_bytes<O32>(vb, jl, 8));
-                B.b[u] = ld_stream2((const double *)at_bytes<O32>(vb, jl + 2, 8));
-            }
+            const int j0 = a0 + 4 * gl;
+            const int jl = j0 < e ? j0 : a0;
+            B.c[u] = ld_stream4((const int32_t *)at_bytes<O32>(cb, jl, 4));
+            B.a[u] = ld_stream2((const double *)at_bytes<O32>(vb, jl, 8));
+            B.b[u] = ld_stream2((const double *)at_bytes<O32>(vb, jl + 2, 8));
         }
     };
     const int64_t c0 = win0[blockIdx.x];
@@ -297,8 +279,8 @@ __global__ __launch_bounds__(256) void csr_slabx_kernel(int64_t m, const RP *__r
             } else {
                 // positions of the lane's 4 entries relative to the row start
                 const int a0 = B.s[u] & ~3;
-                const int ra = (PAIRS ? a0 + 2 * gl : a0 + 4 * gl) - B.s[u];
-                const int rb = ra + (PAIRS ? 2 * L : 2);
+                const int ra = a0 + 4 * gl - B.s[u];
+                const int rb = ra + 2;
                 t = madd(B.a[u].x, gx[u][0], acc);
                 acc = (unsigned)(ra + 0) < (unsigned)B.len[u] ? t : acc;
                 t = madd(B.a[u].y, gx[u][1], acc);
@@ -491,15 +473,19 @@ static int launch_adaptive(const spmv_plan_s *p, const int64_t *bin_off, const i
     return SPMV_SUCCESS;
 }
 
-// launch-time shape of the row-parallel CSR kernels: csr_slab2 with U =
-// min(4, L) steps per batch (config 4, 16 lanes: U = 1 / 2 / 4 / 8 ran
-// 2.64 / 2.55 / 2.49 / 2.54 ms; config 2 within 1 %; profiles/round4/probe/
-// c4_csr_slab2_first.jsonl, c2_csr_slab2_slabx.jsonl).
-// The probe build reads SPMV_LAUNCH_CSR (0: csr_vec4, the round-3 kernel),
-// SPMV_LAUNCH_CSR_U and SPMV_LAUNCH_CSR_LDS_KB at every launch, so variants
-// are A/B'd on one plan's memory.
+// launch-time shape of the row-parallel CSR kernels: csr_slabx where the plan
+// has x windows (banded rows), else csr_slab2, with U = min(4, L) steps per
+// batch.  Config 4 (16 lanes), same plans: csr_vec4 2.80-2.87, csr_slab2 U =
+// 1 / 2 / 4 / 8 2.64 / 2.55 / 2.49 / 2.54 ms, csr_slabx U = 4 2.41-2.54 ms
+// against csr_slab2's 2.54-2.62 on the same plans; config 2 (gather-bound)
+// within 1 % (profiles/round4/probe/c4_csr_slab2_first.jsonl,
+// c4_csr_slabx_s1.jsonl, c4_csr_slabx_pairs.jsonl, c2_csr_slab2_slabx.jsonl).
+// The probe build reads SPMV_LAUNCH_CSR (0: csr_vec4, the round-3 kernel; 2:
+// csr_slab2), SPMV_LAUNCH_CSR_U and SPMV_LAUNCH_CSR_LDS_KB at every launch, so
+// variants are A/B'd on one plan's memory.
 struct CsrLaunch {
-    int slab = 2;    // 2: csr_slab2_kernel, 0: csr_vec4_kernel (probe A/B)
+    int slab = 3;    // 3: csr_slabx where the plan has x windows, else csr_slab2; 2: csr_slab2;
+                     // 0: csr_vec4 (probe A/B)
     int u = 4;       // slab: steps whose loads are issued together
     size_t lds = 0;  // dynamic LDS per workgroup (caps workgroups per CU; probe)
 };
@@ -516,7 +502,7 @@ static void launch_slab_u(const spmv_plan_s *p, int kind, size_t lds, const doub
     constexpr int UU = U < L ? U : L;
     const int64_t waves = (p->m + 63) / 64;
     const CsrDev &c = p->csr;
-    if (kind >= 3 && c.win0) {  // x window in LDS, stream one batch ahead (4: entry pairs)
+    if (kind >= 3 && c.win0) {  // x window in LDS, stream one batch ahead
         constexpr int S = kCsrWinRows / 256;
         const size_t wl = std::max(lds, sizeof(double) * (size_t)c.win);
         const unsigned grid = (unsigned)((p->m + kCsrWinRows - 1) / kCsrWinRows);
@@ -524,13 +510,8 @@ static void launch_slab_u(const spmv_plan_s *p, int kind, size_t lds, const doub
             hipLaunchKernelGGL(kern, dim3(grid), dim3(256), wl, p->stream, p->m, (const RP *)c.row_ptr, c.col, c.val,
                                x, y, c.win0, c.win, p->n);
         };
-        if (kind == 4) {
-            if (c.off32) go(csr_slabx_kernel<L, RP, UU, S, true, true>);
-            else go(csr_slabx_kernel<L, RP, UU, S, false, true>);
-        } else {
-            if (c.off32) go(csr_slabx_kernel<L, RP, UU, S, true, false>);
-            else go(csr_slabx_kernel<L, RP, UU, S, false, false>);
-        }
+        if (c.off32) go(csr_slabx_kernel<L, RP, UU, S, true>);
+        else go(csr_slabx_kernel<L, RP, UU, S, false>);
         return;
     }
     if (p->csr.off32)
