@@ -127,6 +127,12 @@ def _bin_ceiling_line(model, read_gbs, write_gbs, mixed_gbs, nnz, launch_ms) -> 
     return c
 
 
+def progress(msg: str) -> None:
+    """A progress line on stderr (every rank, tagged): long setups (the 8-rank
+    rehearsal, 1.28 G-entry configs) stay visibly alive."""
+    print(f"[bench r{os.environ.get('RANK', '0')} +{time.time() - T_START:.1f}s] {msg}", file=sys.stderr, flush=True)
+
+
 def cpu_model() -> str:
     try:
         for line in open("/proc/cpuinfo"):
@@ -295,6 +301,7 @@ def build_matrix(ctx, args, config: str, rows_override: int = 0):
     # total flops of the job: every rank's own nnz
     nnz_total = int(round(ctx.sdist.sum_over_ranks([float(nnz_local)], ctx.dev)[0]))
     t_gen = time.time() - t0
+    progress(f"{config}: rows [{row0}, {row1}) generated, {nnz_local} nnz, {t_gen:.1f} s")
     # x: generated once on rank 0, replicated by RCCL broadcast over xGMI
     x = torch.empty(n_glob, dtype=torch.float64, device=ctx.dev)
     if ctx.rank == 0:
@@ -349,6 +356,7 @@ def time_formats(ctx, args, M, fmts, trials_head: int, y_check=None, setup_mark=
             continue
         t_plan = time.time() - tp
         info = plan.info()
+        progress(f"{M['config']}: {fmt} plan ({info['kernel']}) built in {t_plan:.1f} s")
         stream = torch.cuda.Stream(device=ctx.dev)
         plan.set_stream(stream)
         torch.cuda.synchronize()
