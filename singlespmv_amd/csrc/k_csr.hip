@@ -204,7 +204,7 @@ struct CsrBatch {
     bool full;
 };
 
-template <int L, typename RP, int U, int S, bool O32>
+template <int L, typename RP, int U, int S, bool O32, bool NT = true>
 __global__ __launch_bounds__(256) void csr_slabx_kernel(int64_t m, const RP *__restrict__ rp,
                                                         const int32_t *__restrict__ col,
                                                         const double *__restrict__ val,
@@ -246,9 +246,15 @@ __global__ __launch_bounds__(256) void csr_slabx_kernel(int64_t m, const RP *__r
             B.full = B.full && (s & 3) == 0 && B.len[u] == 4 * L;
             const int j0 = a0 + 4 * gl;
             const int jl = j0 < e ? j0 : a0;
-            B.c[u] = ld_stream4((const int32_t *)at_bytes<O32>(cb, jl, 4));
-            B.a[u] = ld_stream2((const double *)at_bytes<O32>(vb, jl, 8));
-            B.b[u] = ld_stream2((const double *)at_bytes<O32>(vb, jl + 2, 8));
+            if constexpr (NT) {
+                B.c[u] = ld_stream4((const int32_t *)at_bytes<O32>(cb, jl, 4));
+                B.a[u] = ld_stream2((const double *)at_bytes<O32>(vb, jl, 8));
+                B.b[u] = ld_stream2((const double *)at_bytes<O32>(vb, jl + 2, 8));
+            } else {  // probe A/B: cached loads
+                B.c[u] = *(const i32x4 *)at_bytes<O32>(cb, jl, 4);
+                B.a[u] = *(const f64x2 *)at_bytes<O32>(vb, jl, 8);
+                B.b[u] = *(const f64x2 *)at_bytes<O32>(vb, jl + 2, 8);
+            }
         }
     };
     const int64_t c0 = win0[blockIdx.x];
@@ -510,6 +516,12 @@ static void launch_slab_u(const spmv_plan_s *p, int kind, size_t lds, const doub
             hipLaunchKernelGGL(kern, dim3(grid), dim3(256), wl, p->stream, p->m, (const RP *)c.row_ptr, c.col, c.val,
                                x, y, c.win0, c.win, p->n);
         };
+#ifdef SPMV_PROBES
+        if (kind == 5 && c.off32) {  // probe A/B: cached col / val loads
+            go(csr_slabx_kernel<L, RP, UU, S, true, false>);
+            return;
+        }
+#endif
         if (c.off32) go(csr_slabx_kernel<L, RP, UU, S, true>);
         else go(csr_slabx_kernel<L, RP, UU, S, false>);
         return;

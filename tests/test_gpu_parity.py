@@ -131,6 +131,42 @@ def test_csr_lanes(lanes):
         assert np.array_equal(y, yo)
 
 
+@pytest.mark.parametrize("lanes", [0, 1, 4, 16, 64])
+@pytest.mark.parametrize("empty", [False, True])
+def test_csr_window_kernel(lanes, empty):
+    """Banded rows: the CSR plan keeps an x window per 512-row workgroup and
+    runs csr_slabx (x from LDS, the stream one batch ahead) -- lanes 4 with
+    81-entry rows take its long-row loop; adding one explicit zero far off the
+    band to the last row leaves no window (csr_slab2), and every other row is
+    bit-identical between the two kernels (same chunks, same order)."""
+    if lanes == 0 and empty:
+        pytest.skip("AUTO bins rows of mixed lengths (the adaptive kernel)")
+    m = 20077
+    rp, col, val = sp.generate_csr(sp.gen_spec("banded", m, band_lo=-40, band_hi=40, seed=21))
+    if empty:
+        rp, col, val = _with_empty_rows(rp, col, val, 0.1, 3)
+    x = sp.generate_vector(m, seed=22)
+    kw = {"csr_lanes": lanes} if lanes else {}
+    plan = sp.Plan.from_csr(m, m, rp, col, val, "csr", **kw)
+    assert plan.info()["kernel"].startswith("csr_slabx_kernel"), plan.info()["kernel"]
+    y = run_plan(plan, x, m)
+    yo = oracle_y(rp, col, val, x)
+    check_close(y, yo, what=f"slabx lanes {lanes}")
+    if lanes == 1:
+        assert np.array_equal(y, yo)
+    # the same matrix with an explicit 0 at column 0 of the last row: no window
+    s = int(rp[-2])
+    col2 = np.concatenate([col[:s], [0], col[s:]]).astype(np.int32)
+    val2 = np.concatenate([val[:s], [0.0], val[s:]])
+    rp2 = rp.copy()
+    rp2[-1] += 1
+    plan2 = sp.Plan.from_csr(m, m, rp2, col2, val2, "csr", **kw)
+    assert plan2.info()["kernel"].startswith("csr_slab2_kernel"), plan2.info()["kernel"]
+    y2 = run_plan(plan2, x, m)
+    assert np.array_equal(y[:-1], y2[:-1])
+    check_close(y2, yo, what=f"slab2 lanes {lanes}")
+
+
 @pytest.mark.parametrize("sigma", [4, 8, 12, 16, 20, 24, 32])
 @pytest.mark.parametrize("kind", ["powerlaw", "uniform", "empty_rows"])
 def test_ss_sigma(sigma, kind):
