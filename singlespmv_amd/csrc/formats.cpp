@@ -289,29 +289,54 @@ int csr_plan_lanes(spmv_plan_s *p, const int64_t *row_ptr, int64_t m, const spmv
     return upload(p, &c.bin_rows, rows.data(), m);
 }
 
-// x windows of csr_slabx's kCsrWinRows-row workgroups (k_csr.hip):
-// the column span of each workgroup's entries; kept when every span fits
+// x windows of csr_slabx's workgroups (k_csr.hip): the column span of each
+// kCsrWinGroup-row granule's entries; a workgroup of S granules reads the
+// union of theirs.  Kept when the default workgroup's union fits
 // kCsrMaxWin columns (banded matrices), else none.
-static int csr_x_windows(spmv_plan_s *p, const HostCsr &A) {
+int csr_windows_finish(spmv_plan_s *p, const std::vector<int32_t> &lo, const std::vector<int32_t> &hi) {
     CsrDev &c = p->csr;
-    const int64_t nwg = (A.m + kCsrWinRows - 1) / kCsrWinRows;
-    std::vector<int32_t> w0((size_t)std::max<int64_t>(nwg, 1), 0);
-    int64_t span = 1;
+    const int64_t ng = (int64_t)lo.size();
+    if (ng == 0) return SPMV_SUCCESS;
+    for (int si = 0; si < 3; ++si) {
+        const int64_t S = (int64_t)1 << si;
+        int64_t span = 1;
 #pragma omp parallel for schedule(static) reduction(max : span)
-    for (int64_t b = 0; b < nwg; ++b) {
-        const int64_t e0 = A.row_ptr[b * kCsrWinRows], e1 = A.row_ptr[std::min<int64_t>(A.m, (b + 1) * kCsrWinRows)];
-        int32_t lo = std::numeric_limits<int32_t>::max(), hi = -1;
-        for (int64_t j = e0; j < e1; ++j) {
-            lo = std::min(lo, A.col[j]);
-            hi = std::max(hi, A.col[j]);
+        for (int64_t b = 0; b < ng; b += S) {
+            int32_t l = std::numeric_limits<int32_t>::max(), h = -1;
+            for (int64_t g = b; g < std::min(ng, b + S); ++g) {
+                if (hi[(size_t)g] < 0) continue;  // no entries
+                l = std::min(l, lo[(size_t)g]);
+                h = std::max(h, hi[(size_t)g]);
+            }
+            if (h >= 0) span = std::max<int64_t>(span, (int64_t)h - l + 1);
         }
-        if (hi < 0) lo = hi = 0;
-        w0[(size_t)b] = lo;
-        span = std::max<int64_t>(span, (int64_t)hi - lo + 1);
+        c.win_s[si] = span <= kCsrMaxWin ? (int32_t)span : 0;
     }
-    if (span > kCsrMaxWin || nwg == 0) return SPMV_SUCCESS;
-    c.win = (int32_t)span;
-    return upload(p, &c.win0, w0.data(), nwg);
+    const int sd = kCsrSlabsPerWave == 4 ? 2 : kCsrSlabsPerWave == 2 ? 1 : 0;
+    if (!c.win_s[sd]) return SPMV_SUCCESS;
+    c.win = c.win_s[sd];
+    std::vector<int32_t> w0(lo);
+    for (int64_t g = 0; g < ng; ++g)
+        if (hi[(size_t)g] < 0) w0[(size_t)g] = std::numeric_limits<int32_t>::max();  // empty: no lower bound
+    return upload(p, &c.win0, w0.data(), ng);
+}
+
+static int csr_x_windows(spmv_plan_s *p, const HostCsr &A) {
+    const int64_t ng = (A.m + kCsrWinGroup - 1) / kCsrWinGroup;
+    std::vector<int32_t> lo((size_t)ng), hi((size_t)ng);
+#pragma omp parallel for schedule(static)
+    for (int64_t b = 0; b < ng; ++b) {
+        const int64_t e0 = A.row_ptr[b * kCsrWinGroup];
+        const int64_t e1 = A.row_ptr[std::min<int64_t>(A.m, (b + 1) * kCsrWinGroup)];
+        int32_t l = std::numeric_limits<int32_t>::max(), h = -1;
+        for (int64_t j = e0; j < e1; ++j) {
+            l = std::min(l, A.col[j]);
+            h = std::max(h, A.col[j]);
+        }
+        lo[(size_t)b] = h < 0 ? 0 : l;
+        hi[(size_t)b] = h;
+    }
+    return csr_windows_finish(p, lo, hi);
 }
 
 int build_csr(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {

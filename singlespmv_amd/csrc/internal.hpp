@@ -124,7 +124,8 @@ constexpr int kPad = 8;
 constexpr int kCsrBins = 8;
 constexpr int kCsrBinLanes[kCsrBins] = {1, 2, 4, 8, 16, 32, 64, 256};
 constexpr int kCsrMaxWin = 4096;   // columns of a csr_slabx / ell_slicex x window (32 KB of LDS)
-constexpr int kCsrWinRows = 512;  // rows of a csr_slabx workgroup (4 waves x 2 slabs of 64)
+constexpr int kCsrWinGroup = 256;  // rows of one x-window granule (4 waves x 1 slab of 64)
+constexpr int kCsrSlabsPerWave = 1;  // csr_slabx default: a workgroup owns 1 granule (256 rows)
 struct CsrDev {
     void *row_ptr = nullptr;  // int32 or int64 [m+1]
     bool rp64 = false;
@@ -133,8 +134,9 @@ struct CsrDev {
     int lanes = 4;            // lanes per row (1..64); 0 = adaptive (bins)
     bool off32 = false;       // every 64-row slab spans < 2^28 entries and n < 2^29:
                               // 32-bit byte offsets in csr_slab2 (k_csr.hip)
-    int32_t *win0 = nullptr;  // [ceil(m / kCsrWinRows)]: first column of each workgroup's
-    int32_t win = 0;          //   x window of `win` columns (null: no window fits kCsrMaxWin)
+    int32_t *win0 = nullptr;  // [ceil(m / kCsrWinGroup)]: first column of each 256-row granule's
+    int32_t win = 0;          //   x window; win = the widest window of kCsrSlabsPerWave granules
+    int32_t win_s[3] = {};    //   ... of 1, 2, 4 granules (0: wider than kCsrMaxWin); null: none fits
     int32_t *bin_rows = nullptr;        // rows of every bin, ascending within a bin
     int64_t bin_off[kCsrBins + 1] = {};  // host: bin b = bin_rows[bin_off[b], bin_off[b+1])
 };
@@ -434,6 +436,8 @@ int build_ss_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, c
 int choose_format(const HostCsr &A, const spmv_options_t &o);
 int auto_csr_lanes(double mean_row);
 int csr_plan_lanes(spmv_plan_s *p, const int64_t *row_ptr, int64_t m, const spmv_options_t &o);
+// x windows of csr_slabx from each granule's column range (lo, hi; hi < 0: no entries)
+int csr_windows_finish(spmv_plan_s *p, const std::vector<int32_t> &lo, const std::vector<int32_t> &hi);
 void csr_finish_info(spmv_plan_s *p);
 int auto_ss_sigma(double mean_row);
 

@@ -249,15 +249,15 @@ int build_csr_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, 
     return SPMV_SUCCESS;
 }
 
-// csr_x_windows on the device (formats.cpp): the column span [lo, hi] of each
-// kCsrWinRows-row workgroup's entries, one workgroup per window
+// csr_x_windows on the device (formats.cpp): the column range [lo, hi] of
+// each kCsrWinGroup-row granule's entries (hi = -1: none), one workgroup each
 __global__ __launch_bounds__(256) void csr_window_kernel(const int64_t *__restrict__ rp, int64_t m,
                                                          const int32_t *__restrict__ col, int32_t *__restrict__ lo,
-                                                         int32_t *__restrict__ span) {
+                                                         int32_t *__restrict__ hi) {
     __shared__ int32_t smin[256], smax[256];
     const int64_t b = blockIdx.x;
-    const int64_t e0 = rp[b * kCsrWinRows];
-    const int64_t r1 = (b + 1) * kCsrWinRows < m ? (b + 1) * kCsrWinRows : m;
+    const int64_t e0 = rp[b * kCsrWinGroup];
+    const int64_t r1 = (b + 1) * kCsrWinGroup < m ? (b + 1) * kCsrWinGroup : m;
     const int64_t e1 = rp[r1];
     int32_t mn = INT32_MAX, mx = -1;
     for (int64_t j = e0 + threadIdx.x; j < e1; j += 256) {
@@ -276,34 +276,25 @@ __global__ __launch_bounds__(256) void csr_window_kernel(const int64_t *__restri
         __syncthreads();
     }
     if (threadIdx.x == 0) {
-        const bool empty = smax[0] < 0;
-        lo[b] = empty ? 0 : smin[0];
-        span[b] = empty ? 1 : smax[0] - smin[0] + 1;
+        lo[b] = smax[0] < 0 ? 0 : smin[0];
+        hi[b] = smax[0];
     }
 }
 
 int csr_x_windows_device(spmv_plan_s *p, const int64_t *d_rp) {
-    CsrDev &c = p->csr;
-    const int64_t nwg = (p->m + kCsrWinRows - 1) / kCsrWinRows;
-    if (nwg == 0) return SPMV_SUCCESS;
-    int32_t *lo = nullptr, *span = nullptr;
-    SPMV_RETURN_IF(p->arena.alloc((void **)&lo, sizeof(int32_t) * (size_t)nwg));
-    SPMV_HIP_TRY(hipMalloc(&span, sizeof(int32_t) * (size_t)nwg));
-    hipLaunchKernelGGL(csr_window_kernel, dim3((unsigned)nwg), dim3(256), 0, p->stream, d_rp, p->m, c.col, lo, span);
-    std::vector<int32_t> hs((size_t)nwg);
-    const hipError_t e1 = hipGetLastError();
-    const hipError_t e2 = e1 == hipSuccess ? hipMemcpy(hs.data(), span, sizeof(int32_t) * (size_t)nwg,
-                                                       hipMemcpyDeviceToHost) : e1;
-    (void)hipFree(span);
-    SPMV_HIP_TRY(e2);
-    const int32_t w = *std::max_element(hs.begin(), hs.end());
-    if (w > kCsrMaxWin) {
-        p->arena.free(lo);
-        return SPMV_SUCCESS;
-    }
-    c.win0 = lo;
-    c.win = w;
-    return SPMV_SUCCESS;
+    const int64_t ng = (p->m + kCsrWinGroup - 1) / kCsrWinGroup;
+    if (ng == 0) return SPMV_SUCCESS;
+    int32_t *d = nullptr;
+    SPMV_HIP_TRY(hipMalloc(&d, 2 * sizeof(int32_t) * (size_t)ng));
+    hipLaunchKernelGGL(csr_window_kernel, dim3((unsigned)ng), dim3(256), 0, p->stream, d_rp, p->m, p->csr.col, d,
+                       d + ng);
+    std::vector<int32_t> lo((size_t)ng), hi((size_t)ng);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipMemcpy(lo.data(), d, sizeof(int32_t) * (size_t)ng, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(hi.data(), d + ng, sizeof(int32_t) * (size_t)ng, hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    SPMV_HIP_TRY(e);
+    return csr_windows_finish(p, lo, hi);
 }
 
 int build_ss_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, const double *d_val,

@@ -186,8 +186,8 @@ __global__ __launch_bounds__(256) void csr_slab2_kernel(int64_t m, const RP *__r
 // csr_slabx<L, U, S, O32>: csr_slab2 for matrices whose rows stay near the
 // diagonal (banded, config 4).  A workgroup owns 256 S consecutive rows (each
 // wave S consecutive 64-row slabs) and reads x over one column window
-// [win0[wg], win0[wg] + win) (host-computed, CsrDev::win0 for 256 S-row
-// groups); it is staged into LDS once, so the x reads are LDS reads
+// [c0, c0 + win), the union of its S 256-row granules' windows
+// (host- or device-computed, CsrDev::win0); it is staged into LDS once, so the x reads are LDS reads
 // (lgkmcnt) and no longer share the in-order vmcnt queue with the col / val
 // stream -- which lets the stream run one batch ahead: batch i + 1's loads
 // (the next slab's first one included) are in flight while batch i's x reads
@@ -257,7 +257,16 @@ __global__ __launch_bounds__(256) void csr_slabx_kernel(int64_t m, const RP *__r
             }
         }
     };
-    const int64_t c0 = win0[blockIdx.x];
+    // the workgroup's window: the union of its S granules' (win0: per
+    // 256-row granule, INT32_MAX when a granule has no entries)
+    const int64_t ng = (m + kCsrWinGroup - 1) / kCsrWinGroup;
+    int64_t c0 = INT32_MAX;
+#pragma unroll
+    for (int k = 0; k < S; ++k) {
+        const int64_t gk = (int64_t)blockIdx.x * S + k;
+        if (gk < ng) c0 = c0 < win0[gk] ? c0 : (int64_t)win0[gk];
+    }
+    if (c0 == INT32_MAX) c0 = 0;
     const uint32_t wmax = (uint32_t)win - 1;
     auto xw = [&](int c) -> double {
         const uint32_t i = (uint32_t)((int64_t)c - c0);
@@ -509,21 +518,26 @@ static void launch_slab_u(const spmv_plan_s *p, int kind, size_t lds, const doub
     const int64_t waves = (p->m + 63) / 64;
     const CsrDev &c = p->csr;
     if (kind >= 3 && c.win0) {  // x window in LDS, stream one batch ahead
-        constexpr int S = kCsrWinRows / 256;
-        const size_t wl = std::max(lds, sizeof(double) * (size_t)c.win);
-        const unsigned grid = (unsigned)((p->m + kCsrWinRows - 1) / kCsrWinRows);
+        // S granules (64-row slabs per wave) per workgroup: kCsrSlabsPerWave;
+        // probe build: SPMV_LAUNCH_CSR_S = 1, 2 or 4 where that window fits
+        int S = kCsrSlabsPerWave;
+        if (const char *e = probe_env("SPMV_LAUNCH_CSR_S")) S = std::atoi(e);
+        const int si = S == 4 ? 2 : S == 1 ? 0 : 1;
+        if (!c.win_s[si]) S = kCsrSlabsPerWave;
+        const int32_t win = c.win_s[S == 4 ? 2 : S == 1 ? 0 : 1];
+        const size_t wl = std::max(lds, sizeof(double) * (size_t)win);
+        const unsigned grid = (unsigned)((p->m + 256 * S - 1) / (256 * S));
         auto go = [&](auto kern) {
             hipLaunchKernelGGL(kern, dim3(grid), dim3(256), wl, p->stream, p->m, (const RP *)c.row_ptr, c.col, c.val,
-                               x, y, c.win0, c.win, p->n);
+                               x, y, c.win0, win, p->n);
         };
-#ifdef SPMV_PROBES
-        if (kind == 5 && c.off32) {  // probe A/B: cached col / val loads
-            go(csr_slabx_kernel<L, RP, UU, S, true, false>);
-            return;
+        if (c.off32) {
+            if (S == 1) go(csr_slabx_kernel<L, RP, UU, 1, true>);
+            else if (S == 4) go(csr_slabx_kernel<L, RP, UU, 4, true>);
+            else go(csr_slabx_kernel<L, RP, UU, 2, true>);
+        } else {
+            go(csr_slabx_kernel<L, RP, UU, kCsrSlabsPerWave, false>);
         }
-#endif
-        if (c.off32) go(csr_slabx_kernel<L, RP, UU, S, true>);
-        else go(csr_slabx_kernel<L, RP, UU, S, false>);
         return;
     }
     if (p->csr.off32)
