@@ -132,10 +132,11 @@ int launch_dia(const spmv_plan_s *p, const double *x, double *y) {
     // 1.476-1.527 ms at 1 per CU, 1.500-1.594 at 2, 1.537-1.641 at 8
     // (profiles/round3/probe/dia_occupancy_paired_c4.jsonl,
     // dia_unroll_occupancy_c4.jsonl)
-    // The cap is measured on config 4 only (10 GB of values); below the size
-    // at which DIA values take VMM handles (kDiaVmmMinBytes, 256 MB) the
-    // launch keeps the x window's own occupancy (more latency hiding for
-    // small matrices)
+    // Below the size at which DIA values take VMM handles (kDiaVmmMinBytes,
+    // 256 MB) the launch keeps the x window's own occupancy: 64 diagonals,
+    // same plans, 200 K rows (100 MB) 0.0166 ms uncapped vs 0.0188 capped;
+    // 2 M rows (1 GB) 0.163 vs 0.159; 6 M rows (3 GB) 0.486 vs 0.466
+    // (profiles/round4/probe/dia_cap_{200k,2m,6m}.jsonl)
     const bool big = (size_t)d.n_diags * (size_t)d.mp * sizeof(double) >= kDiaVmmMinBytes;
     int kb = d.lds_kb >= 0 ? d.lds_kb : (big ? kDiaLdsKb : 0);
     if (const char *e = probe_env("SPMV_LAUNCH_DIA_LDS_KB")) kb = std::atoi(e);
