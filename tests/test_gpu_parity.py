@@ -167,6 +167,37 @@ def test_csr_window_kernel(lanes, empty):
     check_close(y2, yo, what=f"slab2 lanes {lanes}")
 
 
+@pytest.mark.parametrize("m,n", [(1, 1), (7, 7), (255, 255), (256, 300), (257, 257), (513, 40), (1000, 5000)])
+@pytest.mark.parametrize("lanes", [1, 4])
+def test_csr_window_kernel_small_shapes(m, n, lanes):
+    """csr_slabx at the edges: fewer rows than a workgroup, a partial last
+    granule, rectangular matrices whose windows touch column 0 or n - 1,
+    empty rows; y against the oracle (bit for bit with one lane)."""
+    rng = np.random.default_rng(m * 7 + n)
+    rows, cols = [], []
+    for r in range(m):
+        c = r * n // max(m, 1)
+        cs = sorted({min(n - 1, max(0, c + d)) for d in range(-3, 4) if rng.random() < 0.8})
+        if r % 11 == 5:
+            cs = []  # empty rows
+        rows += [r] * len(cs)
+        cols += cs
+    rp = np.zeros(m + 1, np.int64)
+    np.add.at(rp, np.asarray(rows, np.int64) + 1, 1)
+    rp = np.cumsum(rp)
+    col = np.asarray(cols, np.int32)
+    val = rng.random(len(col)) + 0.5
+    x = rng.random(n)
+    plan = sp.Plan.from_csr(m, n, rp, col, val, "csr", csr_lanes=lanes)
+    assert plan.info()["kernel"].startswith("csr_slabx_kernel"), plan.info()["kernel"]
+    y = run_plan(plan, x, m)
+    yo = oracle_y(rp, col, val, x)
+    if lanes == 1:
+        assert np.array_equal(y, yo)
+    else:
+        check_close(y, yo, what=f"{m}x{n}")
+
+
 @pytest.mark.parametrize("sigma", [4, 8, 12, 16, 20, 24, 32])
 @pytest.mark.parametrize("kind", ["powerlaw", "uniform", "empty_rows"])
 def test_ss_sigma(sigma, kind):
