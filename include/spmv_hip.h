@@ -123,7 +123,7 @@ typedef struct spmv_options {
 /* Placement of the large buffers of a plan (the BIN product buffer, the DIA
  * values, the streamed col / val arrays of CSR, ELL, HYB, JDS, SS, COO, CSS).  The BIN Mul ran ~15 % slower with one
  * plain hipMalloc on most plans than with the same buffer built from 2-MB
- * physical handles (DESIGN §4a "Placement, round 3").
+ * physical handles (profiles/round1/README.md §4a "Placement, round 3").
  *
  * Known limitation: placement is not fully under the library's control.  In
  * a long-lived process that builds several large plans, about one plan in
@@ -131,7 +131,7 @@ typedef struct spmv_options {
  * config 4 varies 1.48-1.54 ms), VMM or not; the first plan of a process has
  * been fast on three boxes of four.  A caller who needs the best time should
  * build its hot plan first (or rebuild a slow one); no API exposes the
- * placement the hardware picked (DESIGN §4a, profiles/round3/probe/
+ * placement the hardware picked (DESIGN §3.6, profiles/round3/probe/
  * mulorder_plans_arena_vmm_n8.jsonl). */
 #define SPMV_PLACEMENT_AUTO 0   /* BIN products >= 32 MB, DIA values >= 256 MB and
                                    the streamed arrays (col / val / slots) of the

@@ -739,7 +739,7 @@ static int bin_place_prod(spmv_plan_s *p, int64_t n, size_t prod_bytes, const sp
     // slow mode on most plans (config 2 Mul 0.61-0.62 vs 0.53 ms; 10 M x 80 M
     // rank shape 0.84 vs 0.72-0.73), the 2-MB handles were fast in 8 of 8
     // plans, first plan of a fresh process included, for no transient memory
-    // (profiles/round3/probe/placement_vmm_*.jsonl, DESIGN §4a "Placement,
+    // (profiles/round3/probe/placement_vmm_*.jsonl, profiles/round1/README.md §4a "Placement,
     // round 3").
     if (mode == SPMV_PLACEMENT_AUTO)
         mode = prod_bytes >= kBinVmmMinBytes ? SPMV_PLACEMENT_VMM : SPMV_PLACEMENT_PLAIN;

@@ -814,7 +814,7 @@ int build_dia(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
     // AUTO: values of >= 256 MB go straight into 2-MB VMM handles mapped at a
     // 1-GB-aligned VA (config 4: 1.537-1.61 ms against 1.665-1.677 with one
     // plain hipMalloc, profiles/round3/probe/dia_placement_vmm.jsonl; the
-    // same placement as BIN's product buffer, DESIGN §4a)
+    // same placement as BIN's product buffer, DESIGN §3.6)
     const size_t vbytes = (size_t)std::max<int64_t>(slots, 1) * sizeof(double);
     spmv_options_t oo = o;
     SPMV_RETURN_IF(placement_mode_check(oo.placement));

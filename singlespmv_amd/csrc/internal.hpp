@@ -65,7 +65,7 @@ inline int launch_dbg(int plan_dbg) {
     return plan_dbg;
 }
 
-// The placement search (SPMV_PLACEMENT_SEARCH; DESIGN §4a) exists only in
+// The placement search (SPMV_PLACEMENT_SEARCH; DESIGN §3.6) exists only in
 // the probe build: the product library holds no transient device memory at
 // create and times nothing.  SPMV_PLACEMENT_VMM (2-MB physical handles mapped
 // into one 1-GB-aligned VA range) is what AUTO uses for large BIN product

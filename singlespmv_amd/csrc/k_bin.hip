@@ -23,12 +23,12 @@
 //  * Mul order (BinDev::mo, the wide multi-GPU rank shapes whose segments
 //    are short): the Mul writes entry e's product to prod[e] instead, and
 //    bin_sum_bin_kernel gathers each bin's Sum order back in 8-entry chunks
-//    through a chunk table (same add order, same y).
+//    through a chunk table (same add order, same y; DESIGN §3.5, profiles/round3/README.md §4c).
 //
 // HBM bytes per nnz: Mul 8 (val) + 2 (column in strip) + 0.25-0.5
 // (destination) + 8 (product), Sum 8 (product) + 2 (row in bin): ~28.5 B,
 // streamed and fully coalesced, against 12 B + an uncoalesced gather for
-// row-parallel kernels (the Infinity Cache gives the product
+// row-parallel kernels (profiles/round1/README.md §4a: the Infinity Cache gives the product
 // round trip no re-read benefit, so row groups (G > 1) only bound the buffer).
 //
 // Determinism / exactness: a bin is owned by one wave, which adds its

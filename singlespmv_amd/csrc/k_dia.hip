@@ -131,7 +131,7 @@ int launch_dia(const spmv_plan_s *p, const double *x, double *y) {
     // placements fall into.  Config 4, launch variants on the same plans:
     // 1.476-1.527 ms at 1 per CU, 1.500-1.594 at 2, 1.537-1.641 at 8
     // (profiles/round3/probe/dia_occupancy_paired_c4.jsonl,
-    // dia_unroll_occupancy_c4.jsonl)
+    // dia_unroll_occupancy_c4.jsonl; profiles/round3/README.md)
     // Below the size at which DIA values take VMM handles (kDiaVmmMinBytes,
     // 256 MB) the launch keeps the x window's own occupancy: 64 diagonals,
     // same plans, 200 K rows (100 MB) 0.0166 ms uncapped vs 0.0188 capped;

@@ -459,7 +459,7 @@ def test_dropin_optimizeproblem_spmv(fmt, gpus, monkeypatch):
 def test_dropin_exact_switch(exact, monkeypatch):
     """SPMV_HIP_EXACT=1 keeps the drop-in's BIN plan off the run path: a
     power-law matrix's long rows are then the sequential opt_crs sum bit for
-    bit; without it they are within 1e-12 (DESIGN §4b)."""
+    bit; without it they are within 1e-12 (DESIGN §3.5)."""
     monkeypatch.setenv("SPMV_HIP_FORMAT", "bin")
     if exact:
         monkeypatch.setenv("SPMV_HIP_EXACT", exact)
@@ -728,7 +728,7 @@ def test_bin_bit_exact(shape, kind, opts):
 @pytest.mark.parametrize("long_len,opts", [(6, {}), (64, {}), (1000, {}), (64, {"bin_strip_cols": 3001}),
                                            (200, {"bin_sum_waves": 2, "bin_pad": 8}), (64, {"bin_sum_waves": 8})])
 def test_bin_long_rows_run_path(long_len, opts):
-    """The run path (DESIGN §4b) at explicit thresholds: rows with >=
+    """The run path (DESIGN §3.5) at explicit thresholds: rows with >=
     long_len entries are reduced per strip run in the Mul (pieces cut at
     64-entry blocks -- rows of 5000 entries over 2-17 strips give runs far
     longer than a block), the rest stay bit-exact; two plans agree bit for
@@ -848,7 +848,7 @@ def test_plan_create_holds_only_the_plan(fmt, kind):
     memory never drops by more than the plan's own bytes (+128 MB of runtime
     slack); ten plans built in a row behave the same.  The placement search
     is refused by the product library: it exists only in the probe build
-    (DESIGN §4a)."""
+    (DESIGN §3.6)."""
     m = 4_000_000
     spec = sp.gen_spec(kind, m, per_row=16, band_lo=-20, band_hi=20, seed=21)
     rp, col, val = sp.generate_csr(spec)

@@ -2,7 +2,7 @@
 // products in Mul order ([strip][bin], contiguous, no segment padding) and the
 // Sum gathered each bin's segments back in 8-entry chunks?
 //
-// at the 10 M x 80 M rank shape ~100 us of the Mul is the scatter
+// profiles/round3/README.md (round-3 open items): at the 10 M x 80 M rank shape ~100 us of the Mul is the scatter
 // of its product writes into the Sum-ordered (bin, strip) segments (336-B
 // runs); products written in Mul order would also drop the segment padding
 // (174.0 M stored entries -> 160 M) and the destination array.  The price is

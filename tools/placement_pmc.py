@@ -2,7 +2,7 @@
 """Which hardware counter separates a slow-mode BIN Mul from a fast one?
 
 Builds K BIN plans of the same matrix in one process (library default
-placement, so some land in the slow mode) and runs each plan's
+placement, so some land in the slow mode, profiles/round1/README.md §4a) and runs each plan's
 execute `reps` times, plan after plan, so the k-th block of `reps`
 bin_mul_kernel dispatches belongs to plan k.  Run it under
 `rocprofv3 --kernel-trace --pmc <counters>`: within ONE pass the kernel trace

@@ -1,4 +1,4 @@
-// region_probe.hip -- is the BIN Mul / DIA "slow placement"  a
+// region_probe.hip -- is the BIN Mul / DIA "slow placement" (profiles/round1/README.md §4a) a
 // property of physical HBM regions, and which access patterns feel it?
 //
 // Allocates the device memory in equal chunks (hipMalloc, in order, until
@@ -407,7 +407,7 @@ static int alloc_mode(int reps) {
 // `nalloc` separate allocations of `gb` GB each, kept (so each is new
 // memory), three times each; next to the same bytes read grid-stride.
 // Does the rate vary from allocation to allocation like dia_kernel's
-// (1.51-1.68 ms at config 4), and which pattern is immune?
+// (1.51-1.68 ms at config 4, profiles/round1/README.md §4a), and which pattern is immune?
 __global__ __launch_bounds__(256) void rd_dia(const f64x2 *__restrict__ a, long long blk2, double *__restrict__ out) {
     const f64x2 *b = a + (long long)blockIdx.x * blk2 + threadIdx.x;
     double s = 0;

@@ -2,7 +2,7 @@
 // The wide rank shapes (10 M x N*10 M, N >= 4) get short Mul segments from
 // the two-wave Sum's 10239-row bins; one wave per workgroup would allow
 // 20479-row bins (segments twice as long), but that Sum ran 0.57 ms against
-// 0.35.  This probe streams products (8 B) + row slots (2 B, read
+// 0.35 (profiles/round1/README.md §4a).  This probe streams products (8 B) + row slots (2 B, read
 // 8 per 16-byte load) per wave, two 64x32-entry batches in flight, and adds
 // each product into a 20479-double LDS slice with ds_add_f64:
 //   slots "random"  : uniform over the slice (bank conflicts as in the Sum)
