@@ -414,27 +414,6 @@ int build_ell(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &, int cap,
         }
     }
     SPMV_RETURN_IF(upload(p, &e.slice_off, off.data(), e.n_slices + 1));
-    if (!order) {  // x windows of 4-slice workgroups (ell_slicex, k_ell.hip); the slots' columns
-        const int64_t nwg = (e.n_slices + 3) / 4;  // are real columns of their rows (padding repeats one)
-        std::vector<int32_t> w0((size_t)std::max<int64_t>(nwg, 1), 0);
-        int64_t span = 1;
-#pragma omp parallel for schedule(static) reduction(max : span)
-        for (int64_t b = 0; b < nwg; ++b) {
-            const int64_t j0 = off[(size_t)(4 * b)], j1 = off[(size_t)std::min<int64_t>(e.n_slices, 4 * b + 4)];
-            int32_t lo = std::numeric_limits<int32_t>::max(), hi = -1;
-            for (int64_t j = j0; j < j1; ++j) {
-                lo = std::min(lo, col[(size_t)j]);
-                hi = std::max(hi, col[(size_t)j]);
-            }
-            if (hi < 0) lo = hi = 0;
-            w0[(size_t)b] = lo;
-            span = std::max<int64_t>(span, (int64_t)hi - lo + 1);
-        }
-        if (span <= kCsrMaxWin && nwg > 0) {
-            e.win = (int32_t)span;
-            SPMV_RETURN_IF(upload(p, &e.win0, w0.data(), nwg));
-        }
-    }
     SPMV_RETURN_IF(upload(p, &e.col, col.data(), total));
     SPMV_RETURN_IF(upload(p, &e.val, val.data(), total));
     e.max_width = maxw;

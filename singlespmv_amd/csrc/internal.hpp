@@ -123,7 +123,7 @@ constexpr int kPad = 8;
 // bin b summed by kCsrBinLanes[b] lanes per row (256 = one workgroup per row).
 constexpr int kCsrBins = 8;
 constexpr int kCsrBinLanes[kCsrBins] = {1, 2, 4, 8, 16, 32, 64, 256};
-constexpr int kCsrMaxWin = 4096;   // columns of a csr_slabx / ell_slicex x window (32 KB of LDS)
+constexpr int kCsrMaxWin = 4096;   // columns of a csr_slabx x window (32 KB of LDS)
 constexpr int kCsrWinGroup = 256;  // rows of one x-window granule (4 waves x 1 slab of 64)
 constexpr int kCsrSlabsPerWave = 1;  // csr_slabx default: a workgroup owns 1 granule (256 rows)
 struct CsrDev {
@@ -155,8 +155,6 @@ struct EllDev {
     int32_t *col = nullptr;
     double *val = nullptr;
     int max_width = 0;
-    int32_t *win0 = nullptr;       // [ceil(n_slices / 4)]: x window of each 4-slice workgroup
-    int32_t win = 0;               //   (columns; null: no window fits kCsrMaxWin)
     int unroll = 2;  // quads per lane per iteration (SPMV_ELL_UNROLL, internal;
                      // 2 beat 4 by 28 % at config 4, 5 % at config 2)
 };

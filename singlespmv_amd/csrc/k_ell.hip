@@ -97,93 +97,6 @@ __global__ __launch_bounds__(256) void ell_slice_kernel(int64_t m, int64_t n_sli
     }
 }
 
-// ell_slicex<UNROLL>: ell_slice for matrices whose rows stay near the
-// diagonal (EllDev::win0: each 4-slice workgroup's columns fit one window of
-// <= kCsrMaxWin).  The window is staged into LDS once, the x reads become LDS
-// reads, and the slot stream runs one iteration ahead (A / B ping-pong: the
-// next quads' col / val loads are in flight while this iteration's x reads
-// and adds run; the LDS reads do not wait on the in-order vmcnt queue).
-// Same slots, same order: bit-identical to ell_slice.
-template <int UNROLL>
-struct EllBatch {
-    i32x4 c[UNROLL];
-    f64x2 a[UNROLL], b[UNROLL];
-};
-
-template <int UNROLL>
-__global__ __launch_bounds__(256) void ell_slicex_kernel(int64_t m, int64_t n_slices,
-                                                         const int64_t *__restrict__ slice_off,
-                                                         const int32_t *__restrict__ col,
-                                                         const double *__restrict__ val,
-                                                         const double *__restrict__ x, double *__restrict__ y,
-                                                         const int32_t *__restrict__ win0, int32_t win, int64_t n) {
-    extern __shared__ double xs[];  // [win]
-    const int64_t c0 = win0[blockIdx.x];
-    for (int i = threadIdx.x; i < win; i += 256) xs[i] = x[c0 + i < n ? c0 + i : n - 1];
-    __syncthreads();
-    const int64_t slice = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    if (slice >= n_slices) return;
-    const int64_t base = slice_off[slice];
-    const int64_t quads = (slice_off[slice + 1] - base) >> 8;  // (width/4)
-    const int32_t *cs = col + base;
-    const double *vs = val + base;
-    const uint32_t wmax = (uint32_t)win - 1;
-    auto xw = [&](int c) -> double {
-        const uint32_t i = (uint32_t)((int64_t)c - c0);
-        return xs[i < wmax ? i : wmax];
-    };
-    auto load = [&](EllBatch<UNROLL> &B, int64_t q) {
-#pragma unroll
-        for (int u = 0; u < UNROLL; ++u) {
-            B.c[u] = ld_stream4((const int32_t *)((const char *)cs + (uint32_t)(((q + u) * 256 + lane * 4) * 4)));
-            B.a[u] = ld_stream2((const double *)((const char *)vs + (uint32_t)(((q + u) * 256 + lane * 2) * 8)));
-            B.b[u] = ld_stream2((const double *)((const char *)vs + (uint32_t)(((q + u) * 256 + 128 + lane * 2) * 8)));
-        }
-    };
-    double acc = 0.0;
-    auto compute = [&](const EllBatch<UNROLL> &B) {
-        double g[UNROLL][4];
-#pragma unroll
-        for (int u = 0; u < UNROLL; ++u) {
-            g[u][0] = xw(B.c[u].x);
-            g[u][1] = xw(B.c[u].y);
-            g[u][2] = xw(B.c[u].z);
-            g[u][3] = xw(B.c[u].w);
-        }
-#pragma unroll
-        for (int u = 0; u < UNROLL; ++u) {
-            acc = madd(B.a[u].x, g[u][0], acc);
-            acc = madd(B.a[u].y, g[u][1], acc);
-            acc = madd(B.b[u].x, g[u][2], acc);
-            acc = madd(B.b[u].y, g[u][3], acc);
-        }
-    };
-    const int64_t full = quads / UNROLL * UNROLL;
-    EllBatch<UNROLL> A, B;
-    if (full > 0) load(A, 0);
-    for (int64_t q = 0; q < full; q += 2 * UNROLL) {
-        if (q + UNROLL < full) load(B, q + UNROLL);
-        compute(A);
-        if (q + UNROLL >= full) break;
-        if (q + 2 * UNROLL < full) load(A, q + 2 * UNROLL);
-        compute(B);
-    }
-    for (int64_t q = full; q < quads; ++q) {  // the last width % (4 UNROLL) slots
-        EllBatch<1> T;
-        T.c[0] = ld_stream4((const int32_t *)((const char *)cs + (uint32_t)((q * 256 + lane * 4) * 4)));
-        T.a[0] = ld_stream2((const double *)((const char *)vs + (uint32_t)((q * 256 + lane * 2) * 8)));
-        T.b[0] = ld_stream2((const double *)((const char *)vs + (uint32_t)((q * 256 + 128 + lane * 2) * 8)));
-        const double g0 = xw(T.c[0].x), g1 = xw(T.c[0].y), g2 = xw(T.c[0].z), g3 = xw(T.c[0].w);
-        acc = madd(T.a[0].x, g0, acc);
-        acc = madd(T.a[0].y, g1, acc);
-        acc = madd(T.b[0].x, g2, acc);
-        acc = madd(T.b[0].y, g3, acc);
-    }
-    const int64_t row = slice * 64 + lane;
-    if (row < m) __builtin_nontemporal_store(acc, y + row);
-}
-
 template <int U, bool O32>
 static void launch_ell_uo(const spmv_plan_s *p, const double *x, double *y, size_t lds) {
     const EllDev &e = p->ell;
@@ -198,15 +111,6 @@ static void launch_ell_uo(const spmv_plan_s *p, const double *x, double *y, size
 
 template <int U>
 static void launch_ell_u(const spmv_plan_s *p, const double *x, double *y, size_t lds) {
-    const EllDev &e = p->ell;
-    // probe build: SPMV_LAUNCH_ELL_X=1 takes the LDS x window where the plan has one
-    if (const char *v = probe_env("SPMV_LAUNCH_ELL_X"))
-        if (std::atoi(v) && e.win0 && !e.perm) {
-            const size_t wl = std::max(lds, sizeof(double) * (size_t)e.win);
-            hipLaunchKernelGGL((ell_slicex_kernel<U>), dim3((unsigned)((e.n_slices + 3) / 4)), dim3(256), wl,
-                               p->stream, p->m, e.n_slices, e.slice_off, e.col, e.val, x, y, e.win0, e.win, p->n);
-            return;
-        }
     // 32-bit offsets: x below 4 GB and a slice's values below 2 GB
     bool o32 = p->n < ((int64_t)1 << 29) && (int64_t)p->ell.max_width * 64 * 8 < ((int64_t)1 << 31);
     if (const char *v = probe_env("SPMV_LAUNCH_ELL_O32")) o32 = o32 && std::atoi(v) != 0;
