@@ -23,9 +23,8 @@
 
 namespace spmv {
 
-// LIST: the rows come from a length bin (rows[]), not 0..m-1 (adaptive CSR)
-template <int L, typename RP, bool LIST>
-__global__ __launch_bounds__(256) void csr_vec4_kernel(int64_t m, const int32_t *__restrict__ rows,
+template <int L, typename RP>
+__global__ __launch_bounds__(256) void csr_vec4_kernel(int64_t m,
                                                        const RP *__restrict__ rp,
                                                        const int32_t *__restrict__ col,
                                                        const double *__restrict__ val,
@@ -35,7 +34,7 @@ __global__ __launch_bounds__(256) void csr_vec4_kernel(int64_t m, const int32_t 
     const int64_t g = gtid / L;
     const int lane = threadIdx.x & (L - 1);
     if (g >= m) return;  // whole groups exit together (L | 256)
-    const int64_t row = LIST ? (int64_t)rows[g] : g;
+    const int64_t row = g;
     const int64_t s = rp[row];
     const int64_t e = rp[row + 1];
     double acc = 0.0;
@@ -562,8 +561,8 @@ static int launch_csr_t(const spmv_plan_s *p, int64_t nrows, const double *x, do
             default: launch_slab_u<L, RP, 4>(p, sh.slab, sh.lds, x, y);
         }
     } else {
-        hipLaunchKernelGGL((csr_vec4_kernel<L, RP, false>), dim3((unsigned)blocks), dim3(256), sh.lds, p->stream,
-                           nrows, nullptr, (const RP *)p->csr.row_ptr, p->csr.col, p->csr.val, x, y);
+        hipLaunchKernelGGL((csr_vec4_kernel<L, RP>), dim3((unsigned)blocks), dim3(256), sh.lds, p->stream, nrows,
+                           (const RP *)p->csr.row_ptr, p->csr.col, p->csr.val, x, y);
     }
     SPMV_HIP_TRY(hipGetLastError());
     return SPMV_SUCCESS;
