@@ -203,16 +203,13 @@ struct CsrBatch {
     bool full;
 };
 
-template <int L, typename RP, int U, int S, bool O32, bool NT = true>
-__global__ __launch_bounds__(256) void csr_slabx_kernel(int64_t m, const RP *__restrict__ rp,
-                                                        const int32_t *__restrict__ col,
-                                                        const double *__restrict__ val,
-                                                        const double *__restrict__ x, double *__restrict__ y,
-                                                        const int32_t *__restrict__ win0, int32_t win, int64_t n) {
+template <int L, typename RP, int U, int S, bool O32>
+__device__ __forceinline__ void csr_slabx_body(int64_t m, const RP *__restrict__ rp, const int32_t *__restrict__ col,
+                                               const double *__restrict__ val, const double *__restrict__ x,
+                                               double *__restrict__ y, const int32_t *__restrict__ win0, int32_t win,
+                                               int64_t n, double *xs, double (*ysl)[64]) {
     constexpr int R = 64 / L;   // rows per step
     constexpr int NB = L / U;   // batches per slab
-    extern __shared__ double xs[];  // [win]
-    __shared__ double ysl[4][64];
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const int g = lane / L, gl = lane & (L - 1);
@@ -245,15 +242,9 @@ __global__ __launch_bounds__(256) void csr_slabx_kernel(int64_t m, const RP *__r
             B.full = B.full && (s & 3) == 0 && B.len[u] == 4 * L;
             const int j0 = a0 + 4 * gl;
             const int jl = j0 < e ? j0 : a0;
-            if constexpr (NT) {
-                B.c[u] = ld_stream4((const int32_t *)at_bytes<O32>(cb, jl, 4));
-                B.a[u] = ld_stream2((const double *)at_bytes<O32>(vb, jl, 8));
-                B.b[u] = ld_stream2((const double *)at_bytes<O32>(vb, jl + 2, 8));
-            } else {  // probe A/B: cached loads
-                B.c[u] = *(const i32x4 *)at_bytes<O32>(cb, jl, 4);
-                B.a[u] = *(const f64x2 *)at_bytes<O32>(vb, jl, 8);
-                B.b[u] = *(const f64x2 *)at_bytes<O32>(vb, jl + 2, 8);
-            }
+            B.c[u] = ld_stream4((const int32_t *)at_bytes<O32>(cb, jl, 4));
+            B.a[u] = ld_stream2((const double *)at_bytes<O32>(vb, jl, 8));
+            B.b[u] = ld_stream2((const double *)at_bytes<O32>(vb, jl + 2, 8));
         }
     };
     // the workgroup's window: the union of its S granules' (win0: per
@@ -360,6 +351,17 @@ __global__ __launch_bounds__(256) void csr_slabx_kernel(int64_t m, const RP *__r
         if (i + 2 < nb) load(A, i + 2);
         compute(B, i + 1);
     }
+}
+
+template <int L, typename RP, int U, int S, bool O32>
+__global__ __launch_bounds__(256) void csr_slabx_kernel(int64_t m, const RP *__restrict__ rp,
+                                                        const int32_t *__restrict__ col,
+                                                        const double *__restrict__ val,
+                                                        const double *__restrict__ x, double *__restrict__ y,
+                                                        const int32_t *__restrict__ win0, int32_t win, int64_t n) {
+    extern __shared__ double xs[];  // [win]
+    __shared__ double ysl[4][64];
+    csr_slabx_body<L, RP, U, S, O32>(m, rp, col, val, x, y, win0, win, n, xs, ysl);
 }
 
 // Adaptive CSR in ONE launch: workgroup ranges map to the length bins
