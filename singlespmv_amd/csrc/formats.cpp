@@ -417,6 +417,7 @@ int build_ell(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &, int cap,
     SPMV_RETURN_IF(upload(p, &e.col, col.data(), total));
     SPMV_RETURN_IF(upload(p, &e.val, val.data(), total));
     e.max_width = maxw;
+    e.slots = total;
     p->stored_slots = total;
     p->algo_bytes = 12 * A.nnz + 8 * A.n + 8 * A.m;
     p->n_kernels = 1;

@@ -155,6 +155,7 @@ struct EllDev {
     int32_t *col = nullptr;
     double *val = nullptr;
     int max_width = 0;
+    int64_t slots = 0;             // stored slots of the ELL part (HYB / JDS: without the overflow)
     int unroll = 2;  // quads per lane per iteration (SPMV_ELL_UNROLL, internal;
                      // 2 beat 4 by 28 % at config 4, 5 % at config 2)
 };

@@ -130,7 +130,7 @@ int launch_ell(const spmv_plan_s *p, const double *x, double *y) {
     // profiles/round4/probe/c4_ell_window_variants.jsonl).
     // Probe build: launch-time unroll / LDS request.
     int unroll = e.unroll;
-    size_t lds = (size_t)p->stored_slots * sizeof(double) >= kStreamVmmMinBytes ? kEllLdsKb * 1024 : 0;
+    size_t lds = (size_t)e.slots * sizeof(double) >= kStreamVmmMinBytes ? kEllLdsKb * 1024 : 0;
     if (const char *v = probe_env("SPMV_LAUNCH_ELL_UNROLL")) unroll = std::atoi(v);
     if (const char *v = probe_env("SPMV_LAUNCH_ELL_LDS_KB")) lds = (size_t)std::atoi(v) * 1024;
     switch (unroll) {  // quads (4 slots each) per lane per iteration
