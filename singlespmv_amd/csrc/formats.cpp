@@ -296,7 +296,7 @@ int csr_plan_lanes(spmv_plan_s *p, const int64_t *row_ptr, int64_t m, const spmv
 int csr_windows_finish(spmv_plan_s *p, const std::vector<int32_t> &lo, const std::vector<int32_t> &hi) {
     CsrDev &c = p->csr;
     const int64_t ng = (int64_t)lo.size();
-    if (ng == 0) return SPMV_SUCCESS;
+    if (ng == 0 || p->n == 0 || p->nnz == 0) return SPMV_SUCCESS;  // no x to stage
     for (int si = 0; si < 3; ++si) {
         const int64_t S = (int64_t)1 << si;
         int64_t span = 1;
