@@ -607,8 +607,9 @@ int build_ss(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
             const int64_t i = t * T + li;
             const int64_t lane = li / s.sigma, k = li % s.sigma;
             const int64_t pos = t * T + (k >> 2) * 256 + lane * 4 + (k & 3);
+            const int64_t vpos = t * T + (k >> 2) * 256 + ((k & 2) ? 128 : 0) + lane * 2 + (k & 1);
             col[pos] = i < A.nnz ? A.col[i] : 0;
-            val[pos] = i < A.nnz ? A.val[i] : 0.0;
+            val[vpos] = i < A.nnz ? A.val[i] : 0.0;
         }
     }
     SPMV_RETURN_IF(upload(p, &s.col, col.data(), total));

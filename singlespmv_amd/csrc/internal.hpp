@@ -175,8 +175,9 @@ struct HybDev {
 };
 
 // Segmented sum (opt_ss / CSR5): tiles of 64 lanes x sigma nnz.  Lane l of
-// tile t owns nnz t*64*sigma + l*sigma + k, k in [0, sigma), stored at
-//   t*64*sigma + (k/4)*256 + l*4 + (k%4).
+// tile t owns nnz t*64*sigma + l*sigma + k, k in [0, sigma), its column
+// stored at t*64*sigma + (k/4)*256 + l*4 + (k%4) and its value at
+//   t*64*sigma + (k/4)*256 + (k%4/2)*128 + l*2 + (k%2).
 // flags[t*64 + l] bit k: that nnz is the first entry of a non-empty row.
 // tile_ord[t]: ordinal (among non-empty rows) of the first row that starts
 // inside tile t.  Rows that cross tiles are finished by a fixup kernel from

@@ -129,7 +129,8 @@ __global__ void tile_ordinals(const int64_t *__restrict__ rp, int64_t m, const i
     }
 }
 
-// tile transpose: position t*T + (k/4)*256 + lane*4 + k%4 <- nnz t*T + lane*sigma + k
+// tile transpose: col position t*T + (k/4)*256 + lane*4 + k%4, val position
+// t*T + (k/4)*256 + (k%4/2)*128 + lane*2 + k%2 <- nnz t*T + lane*sigma + k
 __global__ void tile_transpose(const int32_t *__restrict__ col, const double *__restrict__ val, int64_t nnz,
                                int sigma, int64_t total, int32_t *__restrict__ tcol, double *__restrict__ tval) {
     const int64_t T = 64 * (int64_t)sigma;
@@ -139,7 +140,9 @@ __global__ void tile_transpose(const int32_t *__restrict__ col, const double *__
         const int64_t q = w >> 8, lane = (w >> 2) & 63, k = q * 4 + (w & 3);
         const int64_t i = t * T + lane * sigma + k;
         tcol[pos] = i < nnz ? col[i] : 0;
-        tval[pos] = i < nnz ? val[i] : 0.0;
+        const int64_t r = w & 255, vlane = (r & 127) >> 1, vk = q * 4 + (r >> 7) * 2 + (r & 1);
+        const int64_t vi = t * T + vlane * sigma + vk;
+        tval[pos] = vi < nnz ? val[vi] : 0.0;
     }
 }
 

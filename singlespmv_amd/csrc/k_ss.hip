@@ -6,7 +6,8 @@
 //
 // ss_tile_kernel<SIGMA>: one wave = one tile of 64 lanes x SIGMA nnz.  Lane l
 // owns SIGMA consecutive nnz (see SsDev layout: every wave load instruction is
-// 1 KiB contiguous).  Products never touch memory (no val_buf: opt_ss's extra
+// 1 KiB contiguous -- col as 4 ints per lane, val as two 1-KiB halves of 2
+// doubles per lane, like ELL's values).  Products never touch memory (no val_buf: opt_ss's extra
 // 16 B/nnz is gone).  Per lane: sequential segmented sums split by the row
 // start bit-flags; rows that start and end in the lane are written directly.
 // Across the wave: a segmented scan (fixed tree) carries open rows from lane
@@ -45,7 +46,7 @@ __global__ __launch_bounds__(256) void ss_tile_kernel(
     const int64_t base = tile * 64 * SIGMA;
     const uint32_t f = flags[tile * 64 + lane];
     const int32_t *cp = col + base + lane * 4;
-    const double *vp = val + base + lane * 4;
+    const double *vp = val + base + lane * 2;  // entries k%4 < 2 of step k/4, then k%4 >= 2 128 later
 
     i32x4 c[Q];
     f64x2 a[Q], b[Q];
@@ -53,7 +54,7 @@ __global__ __launch_bounds__(256) void ss_tile_kernel(
     for (int q = 0; q < Q; ++q) {
         c[q] = ld_stream4(cp + q * 256);
         a[q] = ld_stream2(vp + q * 256);
-        b[q] = ld_stream2(vp + q * 256 + 2);
+        b[q] = ld_stream2(vp + q * 256 + 128);
     }
     double g[SIGMA];
 #pragma unroll
