@@ -19,6 +19,9 @@ __device__ __forceinline__ i32x4 ld_stream4(const int32_t *p) {
 __device__ __forceinline__ f64x2 ld_stream2(const double *p) {
     return __builtin_nontemporal_load(reinterpret_cast<const f64x2 *>(p));
 }
+__device__ __forceinline__ i32x2 ld_stream2(const int32_t *p) {
+    return __builtin_nontemporal_load(reinterpret_cast<const i32x2 *>(p));
+}
 __device__ __forceinline__ double ld_stream(const double *p) {
     return __builtin_nontemporal_load(p);
 }

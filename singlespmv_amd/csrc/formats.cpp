@@ -496,17 +496,20 @@ int build_jds(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
 // per entry.
 int build_coo(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &) {
     CooDev &c = p->coo;
-    std::vector<int32_t> row((size_t)std::max<int64_t>(A.nnz, 1));
+    // padded to whole 128-entry units; padding rows are -1 (no atomic)
+    c.n_units = (A.nnz + kCooUnit - 1) / kCooUnit;
+    const int64_t total = c.n_units * kCooUnit;
+    std::vector<int32_t> row((size_t)std::max<int64_t>(total, 1), -1);
 #pragma omp parallel for schedule(dynamic, 1024)
     for (int64_t r = 0; r < A.m; ++r)
         for (int64_t j = A.row_ptr[r]; j < A.row_ptr[r + 1]; ++j) row[(size_t)j] = (int32_t)r;
-    SPMV_RETURN_IF(upload(p, &c.row, row.data(), A.nnz));
-    SPMV_RETURN_IF(upload(p, &c.col, A.col, A.nnz));
-    SPMV_RETURN_IF(upload(p, &c.val, A.val, A.nnz));
-    p->stored_slots = A.nnz;
+    SPMV_RETURN_IF(upload(p, &c.row, row.data(), total));
+    SPMV_RETURN_IF(upload(p, &c.col, A.col, A.nnz, total - A.nnz));
+    SPMV_RETURN_IF(upload(p, &c.val, A.val, A.nnz, total - A.nnz));
+    p->stored_slots = total;
     p->algo_bytes = 16 * A.nnz + 8 * A.n + 8 * A.m;
     p->n_kernels = 2;
-    p->kernel_name = "coo_segment_kernel";
+    p->kernel_name = "coo_pair_kernel";
     return SPMV_SUCCESS;
 }
 

@@ -198,13 +198,16 @@ struct SsDev {
     int64_t n_empty = 0;
 };
 
-// COO (opt_coo, src/opt_coo.cpp): sorted (row, col, val); one wave handles
-// 64 consecutive entries per step, reduces equal-row runs in registers and
-// issues one f64 atomic add per run (y zeroed first).
+// COO (opt_coo, src/opt_coo.cpp): sorted (row, col, val), padded to whole
+// units of kCooUnit entries (row -1, col 0, val 0); one wave handles a unit
+// per step (lane l: entries 2l, 2l+1), reduces equal-row runs in registers
+// and issues one f64 atomic add per run (y zeroed first).
+constexpr int64_t kCooUnit = 128;
 struct CooDev {
     int32_t *row = nullptr;
     int32_t *col = nullptr;
     double *val = nullptr;
+    int64_t n_units = 0;
 };
 
 // DIA (opt_dia, src/opt_dia.cpp), row-indexed and blocked by workgroup:
