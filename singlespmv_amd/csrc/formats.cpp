@@ -353,8 +353,20 @@ int build_csr(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
         SPMV_RETURN_IF(upload(p, (int32_t **)&c.row_ptr, rp32.data(), A.m + 1));
     }
     SPMV_RETURN_IF(upload(p, &c.col, A.col, A.nnz, kPad));
-    SPMV_RETURN_IF(upload(p, &c.val, A.val, A.nnz, kPad));
     SPMV_RETURN_IF(csr_plan_lanes(p, A.row_ptr, A.m, o));
+    c.val_halves = csr_val_halves_wanted(c);
+    if (c.val_halves) {
+        const int64_t total = (A.nnz + 255) / 256 * 256;
+        std::vector<double> vh((size_t)total);
+#pragma omp parallel for schedule(static)
+        for (int64_t pos = 0; pos < total; ++pos) {
+            const int64_t e = csr_val_halves_entry(pos);
+            vh[(size_t)pos] = e < A.nnz ? A.val[e] : 0.0;
+        }
+        SPMV_RETURN_IF(upload(p, &c.val, vh.data(), total, kPad));
+    } else {
+        SPMV_RETURN_IF(upload(p, &c.val, A.val, A.nnz, kPad));
+    }
     if (c.lanes > 0) SPMV_RETURN_IF(csr_x_windows(p, A));
     csr_finish_info(p);
     return SPMV_SUCCESS;

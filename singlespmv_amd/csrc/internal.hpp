@@ -130,7 +130,9 @@ struct CsrDev {
     void *row_ptr = nullptr;  // int32 or int64 [m+1]
     bool rp64 = false;
     int32_t *col = nullptr;   // [nnz + kPad]
-    double *val = nullptr;    // [nnz + kPad]
+    double *val = nullptr;    // [nnz + kPad]; val_halves: [roundup(nnz, 256) + kPad], each
+                              //   256-entry chunk as ELL slots (k_csr.hip csr_vpos)
+    bool val_halves = false;  // = lanes > 0 (the row-group kernels); adaptive plans keep CSR order
     int lanes = 4;            // lanes per row (1..64); 0 = adaptive (bins)
     bool off32 = false;       // every 64-row slab spans < 2^28 entries and n < 2^29:
                               // 32-bit byte offsets in csr_slab2 (k_csr.hip)
@@ -140,6 +142,18 @@ struct CsrDev {
     int32_t *bin_rows = nullptr;        // rows of every bin, ascending within a bin
     int64_t bin_off[kCsrBins + 1] = {};  // host: bin b = bin_rows[bin_off[b], bin_off[b+1])
 };
+
+// the entry stored at position pos of a val_halves array (inverse of csr_vpos)
+__host__ __device__ inline int64_t csr_val_halves_entry(int64_t pos) {
+    const int64_t r = pos & 255;
+    return (pos & ~(int64_t)255) + ((r & 127) >> 1) * 4 + (r >> 7) * 2 + (r & 1);
+}
+// row-group plans store their values in halves (probe build:
+// SPMV_CSR_VAL_PLAIN=1 keeps CSR order, for A/Bs)
+inline bool csr_val_halves_wanted(const CsrDev &c) {
+    if (const char *e = probe_env("SPMV_CSR_VAL_PLAIN")) return c.lanes > 0 && std::atoi(e) == 0;
+    return c.lanes > 0;
+}
 
 // Sliced ELL (opt_ell, src/opt_ell.cpp): slices of 64 consecutive rows (one
 // wave); slice s has width w_s (multiple of 4) = max row length in the slice

@@ -146,6 +146,16 @@ __global__ void tile_transpose(const int32_t *__restrict__ col, const double *__
     }
 }
 
+// CSR values of a row-group plan in halves (CsrDev::val_halves)
+__global__ void csr_val_halves_kernel(const double *__restrict__ val, int64_t nnz, int64_t total,
+                                      double *__restrict__ out) {
+    for (int64_t pos = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; pos < total;
+         pos += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t e = csr_val_halves_entry(pos);
+        out[pos] = e < nnz ? val[e] : 0.0;
+    }
+}
+
 // input checks of validate_csr (capi.cpp) on device data: bad[0] counts
 // decreasing row pointers, bad[1] columns outside [0, n)
 __global__ void check_csr(const int64_t *__restrict__ rp, int64_t m, const int32_t *__restrict__ col, int64_t nnz,
@@ -233,20 +243,27 @@ int build_csr_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, 
     else hipLaunchKernelGGL(rp_to_i32, dim3(grid_for(p->m + 1)), dim3(256), 0, st, d_rp, p->m + 1, (int32_t *)q);
     SPMV_RETURN_IF(p->arena.alloc(&q, sizeof(int32_t) * (size_t)(p->nnz + kPad)));
     c.col = (int32_t *)q;
-    SPMV_RETURN_IF(p->arena.alloc(&q, sizeof(double) * (size_t)(p->nnz + kPad)));
-    c.val = (double *)q;
-    if (p->nnz) {
-        SPMV_HIP_TRY(hipMemcpyAsync(c.col, d_col, 4 * (size_t)p->nnz, hipMemcpyDeviceToDevice, st));
-        SPMV_HIP_TRY(hipMemcpyAsync(c.val, d_val, 8 * (size_t)p->nnz, hipMemcpyDeviceToDevice, st));
-    }
+    if (p->nnz) SPMV_HIP_TRY(hipMemcpyAsync(c.col, d_col, 4 * (size_t)p->nnz, hipMemcpyDeviceToDevice, st));
     SPMV_HIP_TRY(hipMemsetAsync(c.col + p->nnz, 0, 4 * kPad, st));
-    SPMV_HIP_TRY(hipMemsetAsync(c.val + p->nnz, 0, 8 * kPad, st));
     SPMV_HIP_TRY(hipStreamSynchronize(st));
     (void)mean_row;
     // lanes per row / length bins from the row pointers (m+1 values to the host)
     std::vector<int64_t> hrp((size_t)p->m + 1);
     SPMV_HIP_TRY(hipMemcpy(hrp.data(), d_rp, 8 * (size_t)(p->m + 1), hipMemcpyDeviceToHost));
     SPMV_RETURN_IF(csr_plan_lanes(p, hrp.data(), p->m, o));
+    c.val_halves = csr_val_halves_wanted(c);
+    const int64_t vtotal = c.val_halves ? (p->nnz + 255) / 256 * 256 : p->nnz;
+    SPMV_RETURN_IF(p->arena.alloc(&q, sizeof(double) * (size_t)(vtotal + kPad)));
+    c.val = (double *)q;
+    if (c.val_halves) {
+        hipLaunchKernelGGL(csr_val_halves_kernel, dim3(grid_for(vtotal)), dim3(256), 0, st, d_val, p->nnz, vtotal,
+                           c.val);
+    } else if (p->nnz) {
+        SPMV_HIP_TRY(hipMemcpyAsync(c.val, d_val, 8 * (size_t)p->nnz, hipMemcpyDeviceToDevice, st));
+    }
+    SPMV_HIP_TRY(hipMemsetAsync(c.val + vtotal, 0, 8 * kPad, st));
+    SPMV_HIP_TRY(hipGetLastError());
+    SPMV_HIP_TRY(hipStreamSynchronize(st));
     if (c.lanes > 0) SPMV_RETURN_IF(csr_x_windows_device(p, d_rp));
     csr_finish_info(p);
     return SPMV_SUCCESS;

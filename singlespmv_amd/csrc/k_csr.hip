@@ -23,13 +23,24 @@
 
 namespace spmv {
 
+// Values of a row-group plan (CsrDev::val_halves, CsrDev::lanes > 0): every
+// aligned 256-entry chunk is laid as ELL's slots -- entries 4t, 4t+1 of the
+// chunk at 2t, entries 4t+2, 4t+3 at 128 + 2t -- so the two 16-byte value
+// loads of a lane's aligned 4-entry group j (at csr_vpos(j) and 128 later)
+// each read whole lines across the wave instead of every other 16 bytes of
+// every line (config 4: SS's values the same way, 3.08-3.26 -> 2.59-2.70 ms).
+template <typename I>
+__device__ __forceinline__ I csr_vpos(I j) {  // j % 4 == 0
+    return (j & ~(I)255) + ((j & 255) >> 1);
+}
+
 template <int L, typename RP>
 __global__ __launch_bounds__(256) void csr_vec4_kernel(int64_t m,
                                                        const RP *__restrict__ rp,
                                                        const int32_t *__restrict__ col,
                                                        const double *__restrict__ val,
                                                        const double *__restrict__ x,
-                                                       double *__restrict__ y) {
+                                                       double *__restrict__ y, bool vh) {
     const int64_t gtid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t g = gtid / L;
     const int lane = threadIdx.x & (L - 1);
@@ -40,8 +51,9 @@ __global__ __launch_bounds__(256) void csr_vec4_kernel(int64_t m,
     double acc = 0.0;
     for (int64_t j = (s & ~(int64_t)3) + 4 * lane; j < e; j += 4 * L) {
         const i32x4 c = ld_stream4(col + j);
-        const f64x2 v01 = ld_stream2(val + j);
-        const f64x2 v23 = ld_stream2(val + j + 2);
+        const int64_t vj = vh ? csr_vpos(j) : j;
+        const f64x2 v01 = ld_stream2(val + vj);
+        const f64x2 v23 = ld_stream2(val + vj + (vh ? 128 : 2));
         // masked gathers: only entries of this row
         const double x0 = (j + 0 >= s && j + 0 < e) ? ld_x(x, c.x) : 0.0;
         const double x1 = (j + 1 >= s && j + 1 < e) ? ld_x(x, c.y) : 0.0;
@@ -87,7 +99,7 @@ template <int L, typename RP, int U, bool O32>
 __global__ __launch_bounds__(256) void csr_slab2_kernel(int64_t m, const RP *__restrict__ rp,
                                                         const int32_t *__restrict__ col,
                                                         const double *__restrict__ val,
-                                                        const double *__restrict__ x, double *__restrict__ y) {
+                                                        const double *__restrict__ x, double *__restrict__ y, bool vh) {
     constexpr int R = 64 / L;  // rows per step
     __shared__ double ysl[4][64];
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR)
@@ -103,7 +115,10 @@ __global__ __launch_bounds__(256) void csr_slab2_kernel(int64_t m, const RP *__r
     const int rpl = (int)((int64_t)rp[rl < m ? rl : m] - base);            // lane t: row r0 + t's start
     const int rpe = (int)((int64_t)rp[r0 + 64 < m ? r0 + 64 : m] - base);  // the slab's end
     const int32_t *cb = col + base;
-    const double *vb = val + base;
+    const int64_t vbase = vh ? base & ~(int64_t)255 : base;
+    const double *vb = val + vbase;
+    const int vo = (int)(base - vbase), vstep = vh ? 128 : 2;
+    auto vpos = [&](int j) -> int { return vh ? csr_vpos(j + vo) : j; };
     for (int st = 0; st < L; st += U) {
         int j0[U], rel[U], len[U];
         bool full = true;
@@ -122,8 +137,9 @@ __global__ __launch_bounds__(256) void csr_slab2_kernel(int64_t m, const RP *__r
             full = full && (s & 3) == 0 && len[u] == 4 * L;
             const int jl = j0[u] < e ? j0[u] : a0;
             c[u] = ld_stream4((const int32_t *)at_bytes<O32>(cb, jl, 4));
-            a[u] = ld_stream2((const double *)at_bytes<O32>(vb, jl, 8));
-            b[u] = ld_stream2((const double *)at_bytes<O32>(vb, jl + 2, 8));
+            const int vj = vpos(jl);
+            a[u] = ld_stream2((const double *)at_bytes<O32>(vb, vj, 8));
+            b[u] = ld_stream2((const double *)at_bytes<O32>(vb, vj + vstep, 8));
         }
         double gx[U][4];
 #pragma unroll
@@ -160,8 +176,9 @@ __global__ __launch_bounds__(256) void csr_slab2_kernel(int64_t m, const RP *__r
                 const int e = j0[u] - rel[u] + len[u];  // the row's end
                 for (int jj = j0[u] + 4 * L; jj < e; jj += 4 * L) {
                     const i32x4 cc = ld_stream4((const int32_t *)at_bytes<O32>(cb, jj, 4));
-                    const f64x2 v01 = ld_stream2((const double *)at_bytes<O32>(vb, jj, 8));
-                    const f64x2 v23 = ld_stream2((const double *)at_bytes<O32>(vb, jj + 2, 8));
+                    const int vj = vpos(jj);
+                    const f64x2 v01 = ld_stream2((const double *)at_bytes<O32>(vb, vj, 8));
+                    const f64x2 v23 = ld_stream2((const double *)at_bytes<O32>(vb, vj + vstep, 8));
                     const double x0 = ldx(cc.x), x1 = ldx(cc.y), x2 = ldx(cc.z), x3 = ldx(cc.w);
                     acc = madd(v01.x, x0, acc);
                     t = madd(v01.y, x1, acc);
@@ -207,7 +224,7 @@ template <int L, typename RP, int U, int S, bool O32>
 __device__ __forceinline__ void csr_slabx_body(int64_t m, const RP *__restrict__ rp, const int32_t *__restrict__ col,
                                                const double *__restrict__ val, const double *__restrict__ x,
                                                double *__restrict__ y, const int32_t *__restrict__ win0, int32_t win,
-                                               int64_t n, double *xs, double (*ysl)[64]) {
+                                               int64_t n, bool vh, double *xs, double (*ysl)[64]) {
     constexpr int R = 64 / L;   // rows per step
     constexpr int NB = L / U;   // batches per slab
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -226,7 +243,10 @@ __device__ __forceinline__ void csr_slabx_body(int64_t m, const RP *__restrict__
         rpe[k] = (int)((int64_t)rp[ek < m ? ek : m] - base);
     }
     const int32_t *cb = col + base;
-    const double *vb = val + base;
+    const int64_t vbase = vh ? base & ~(int64_t)255 : base;
+    const double *vb = val + vbase;
+    const int vo = (int)(base - vbase), vstep = vh ? 128 : 2;
+    auto vpos = [&](int j) -> int { return vh ? csr_vpos(j + vo) : j; };
     auto load = [&](CsrBatch<L, U> &B, int i) {  // batch i: slab i / NB, steps (i % NB) U ..
         const int k = i / NB, st = (i % NB) * U;
         B.full = true;
@@ -243,8 +263,9 @@ __device__ __forceinline__ void csr_slabx_body(int64_t m, const RP *__restrict__
             const int j0 = a0 + 4 * gl;
             const int jl = j0 < e ? j0 : a0;
             B.c[u] = ld_stream4((const int32_t *)at_bytes<O32>(cb, jl, 4));
-            B.a[u] = ld_stream2((const double *)at_bytes<O32>(vb, jl, 8));
-            B.b[u] = ld_stream2((const double *)at_bytes<O32>(vb, jl + 2, 8));
+            const int vj = vpos(jl);
+            B.a[u] = ld_stream2((const double *)at_bytes<O32>(vb, vj, 8));
+            B.b[u] = ld_stream2((const double *)at_bytes<O32>(vb, vj + vstep, 8));
         }
     };
     // the workgroup's window: the union of its S granules' (win0: per
@@ -298,8 +319,9 @@ __device__ __forceinline__ void csr_slabx_body(int64_t m, const RP *__restrict__
                 // rows longer than one chunk of the group: the rest in order
                 for (int jj = a0 + 4 * gl + 4 * L; jj < e; jj += 4 * L) {
                     const i32x4 cc = ld_stream4((const int32_t *)at_bytes<O32>(cb, jj, 4));
-                    const f64x2 v01 = ld_stream2((const double *)at_bytes<O32>(vb, jj, 8));
-                    const f64x2 v23 = ld_stream2((const double *)at_bytes<O32>(vb, jj + 2, 8));
+                    const int vj = vpos(jj);
+                    const f64x2 v01 = ld_stream2((const double *)at_bytes<O32>(vb, vj, 8));
+                    const f64x2 v23 = ld_stream2((const double *)at_bytes<O32>(vb, vj + vstep, 8));
                     const double x0 = xw(cc.x), x1 = xw(cc.y), x2 = xw(cc.z), x3 = xw(cc.w);
                     acc = madd(v01.x, x0, acc);
                     t = madd(v01.y, x1, acc);
@@ -358,10 +380,11 @@ __global__ __launch_bounds__(256) void csr_slabx_kernel(int64_t m, const RP *__r
                                                         const int32_t *__restrict__ col,
                                                         const double *__restrict__ val,
                                                         const double *__restrict__ x, double *__restrict__ y,
-                                                        const int32_t *__restrict__ win0, int32_t win, int64_t n) {
+                                                        const int32_t *__restrict__ win0, int32_t win, int64_t n,
+                                                        bool vh) {
     extern __shared__ double xs[];  // [win]
     __shared__ double ysl[4][64];
-    csr_slabx_body<L, RP, U, S, O32>(m, rp, col, val, x, y, win0, win, n, xs, ysl);
+    csr_slabx_body<L, RP, U, S, O32>(m, rp, col, val, x, y, win0, win, n, vh, xs, ysl);
 }
 
 // Adaptive CSR in ONE launch: workgroup ranges map to the length bins
@@ -530,7 +553,7 @@ static void launch_slab_u(const spmv_plan_s *p, int kind, size_t lds, const doub
         const unsigned grid = (unsigned)((p->m + 256 * S - 1) / (256 * S));
         auto go = [&](auto kern) {
             hipLaunchKernelGGL(kern, dim3(grid), dim3(256), wl, p->stream, p->m, (const RP *)c.row_ptr, c.col, c.val,
-                               x, y, c.win0, win, p->n);
+                               x, y, c.win0, win, p->n, c.val_halves);
         };
         if (c.off32) {
             if (S == 1) go(csr_slabx_kernel<L, RP, UU, 1, true>);
@@ -543,10 +566,10 @@ static void launch_slab_u(const spmv_plan_s *p, int kind, size_t lds, const doub
     }
     if (p->csr.off32)
         hipLaunchKernelGGL((csr_slab2_kernel<L, RP, UU, true>), dim3((unsigned)((waves + 3) / 4)), dim3(256), lds,
-                           p->stream, p->m, (const RP *)p->csr.row_ptr, p->csr.col, p->csr.val, x, y);
+                           p->stream, p->m, (const RP *)p->csr.row_ptr, p->csr.col, p->csr.val, x, y, c.val_halves);
     else
         hipLaunchKernelGGL((csr_slab2_kernel<L, RP, UU, false>), dim3((unsigned)((waves + 3) / 4)), dim3(256), lds,
-                           p->stream, p->m, (const RP *)p->csr.row_ptr, p->csr.col, p->csr.val, x, y);
+                           p->stream, p->m, (const RP *)p->csr.row_ptr, p->csr.col, p->csr.val, x, y, c.val_halves);
 }
 
 template <int L, typename RP>
@@ -564,7 +587,7 @@ static int launch_csr_t(const spmv_plan_s *p, int64_t nrows, const double *x, do
         }
     } else {
         hipLaunchKernelGGL((csr_vec4_kernel<L, RP>), dim3((unsigned)blocks), dim3(256), sh.lds, p->stream, nrows,
-                           (const RP *)p->csr.row_ptr, p->csr.col, p->csr.val, x, y);
+                           (const RP *)p->csr.row_ptr, p->csr.col, p->csr.val, x, y, p->csr.val_halves);
     }
     SPMV_HIP_TRY(hipGetLastError());
     return SPMV_SUCCESS;
