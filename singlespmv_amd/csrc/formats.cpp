@@ -180,10 +180,15 @@ int auto_csr_lanes(double mean_row) {
 
 int auto_ss_sigma(double mean_row) {
     // ~one row boundary per lane keeps the in-lane branch count low while
-    // each lane keeps SIGMA*12 bytes of loads in flight
+    // each lane keeps SIGMA*12 bytes of loads in flight; long rows stop at 20:
+    // with the x window SIGMA = 32 needs 172 VGPRs (2 waves per SIMD) and was
+    // the slowest of 16 / 20 / 24 / 32 on three banded shapes (32, 40, 128
+    // per row), 20 within 3 % of the best on each; at config 4 (64 per row)
+    // plan placement alone moves a launch by up to 8 %, more than SIGMA does
+    // (profiles/round4/probe/ss_sigma_window_*.jsonl)
     if (mean_row <= 6) return 8;
     if (mean_row <= 24) return 16;
-    return 32;
+    return 20;
 }
 
 // ---------------------------------------------------------------- CSR

@@ -15,6 +15,14 @@
 // the tile end leaves (tail partial, its ordinal); the partial of the tile's
 // first row continuing from earlier tiles leaves as head partial.
 //
+// x window: when a tile's columns span fewer than kSsWin, the wave first
+// copies x[lo, hi] into its own LDS slice (coalesced, mostly L2 hits) and
+// reads its SIGMA values per lane from there; a gather per entry touches up to
+// 64 lines per instruction (lanes own different rows).  Same values, same
+// arithmetic: bit-identical.  Same plans: config 4 (SIGMA 20) -5 to -6 %,
+// config 3 -4 %, config 2 -0.7 %; SIGMA 32 (172 VGPRs with the window)
+// -1 to +1 % (profiles/round4/probe/ss_sigma_window_*, ss_window_default_c4).
+//
 // ss_fixup_kernel: one thread per tile whose tail is open adds the heads of
 // the following tiles up to the next tile that starts a row (fixed order --
 // no atomics, unlike the CAS atomicAdd calibrator of CSR5,
@@ -31,7 +39,9 @@ __device__ __forceinline__ void ss_store(double *y, const int32_t *nzrow, int64_
     if (ord < n_nonempty) y[nzrow ? (int64_t)nzrow[ord] : ord] = v;
 }
 
-template <int SIGMA>
+constexpr int kSsWin = 512;  // x window per wave (doubles) of the WIN instance
+
+template <int SIGMA, bool WIN>
 __global__ __launch_bounds__(256) void ss_tile_kernel(
     int64_t n_tiles, const int32_t *__restrict__ col, const double *__restrict__ val,
     const uint32_t *__restrict__ flags, const int32_t *__restrict__ tile_ord,
@@ -57,12 +67,49 @@ __global__ __launch_bounds__(256) void ss_tile_kernel(
         b[q] = ld_stream2(vp + q * 256 + 128);
     }
     double g[SIGMA];
+    bool gathered = false;
+    if constexpr (WIN) {
+        // the tile's column range; when it fits kSsWin, x comes through a
+        // per-wave LDS window (coalesced loads, then LDS reads) instead of
+        // SIGMA gathers that each touch up to 64 lines
+        __shared__ double xs[4][kSsWin];
+        int lo = INT32_MAX, hi = -1;
 #pragma unroll
-    for (int q = 0; q < Q; ++q) {
-        g[4 * q + 0] = ld_x(x, c[q].x);
-        g[4 * q + 1] = ld_x(x, c[q].y);
-        g[4 * q + 2] = ld_x(x, c[q].z);
-        g[4 * q + 3] = ld_x(x, c[q].w);
+        for (int q = 0; q < Q; ++q) {
+            lo = min(lo, min(min(c[q].x, c[q].y), min(c[q].z, c[q].w)));
+            hi = max(hi, max(max(c[q].x, c[q].y), max(c[q].z, c[q].w)));
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            lo = min(lo, __shfl_xor(lo, o, 64));
+            hi = max(hi, __shfl_xor(hi, o, 64));
+        }
+        lo = __builtin_amdgcn_readfirstlane(lo);
+        hi = __builtin_amdgcn_readfirstlane(hi);
+        if (hi - lo < kSsWin) {  // wave-uniform
+            const int wv = threadIdx.x >> 6;
+            for (int i = lane; i <= hi - lo; i += 64) xs[wv][i] = ld_x(x, lo + i);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (int q = 0; q < Q; ++q) {
+                g[4 * q + 0] = xs[wv][c[q].x - lo];
+                g[4 * q + 1] = xs[wv][c[q].y - lo];
+                g[4 * q + 2] = xs[wv][c[q].z - lo];
+                g[4 * q + 3] = xs[wv][c[q].w - lo];
+            }
+            gathered = true;
+        }
+    }
+    if (!gathered) {
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            g[4 * q + 0] = ld_x(x, c[q].x);
+            g[4 * q + 1] = ld_x(x, c[q].y);
+            g[4 * q + 2] = ld_x(x, c[q].z);
+            g[4 * q + 3] = ld_x(x, c[q].w);
+        }
     }
 
     const int pc = __builtin_popcount(f);
@@ -132,9 +179,16 @@ template <int SIGMA>
 static void launch_ss_t(const spmv_plan_s *p, const double *x, double *y) {
     const SsDev &s = p->ss;
     const int64_t blocks = (s.n_tiles + 3) / 4;
-    hipLaunchKernelGGL((ss_tile_kernel<SIGMA>), dim3((unsigned)blocks), dim3(256), 0, p->stream,
-                       s.n_tiles, s.col, s.val, s.flags, s.tile_ord, s.nzrow, s.n_nonempty, x, y,
-                       s.head, s.tail, s.tail_ord);
+    bool win = true;  // probe build: SPMV_LAUNCH_SS_WIN=0 gathers x from memory always
+    if (const char *v = probe_env("SPMV_LAUNCH_SS_WIN")) win = std::atoi(v) != 0;
+    if (win)
+        hipLaunchKernelGGL((ss_tile_kernel<SIGMA, true>), dim3((unsigned)blocks), dim3(256), 0, p->stream,
+                           s.n_tiles, s.col, s.val, s.flags, s.tile_ord, s.nzrow, s.n_nonempty, x, y,
+                           s.head, s.tail, s.tail_ord);
+    else
+        hipLaunchKernelGGL((ss_tile_kernel<SIGMA, false>), dim3((unsigned)blocks), dim3(256), 0, p->stream,
+                           s.n_tiles, s.col, s.val, s.flags, s.tile_ord, s.nzrow, s.n_nonempty, x, y,
+                           s.head, s.tail, s.tail_ord);
 }
 
 int launch_ss(const spmv_plan_s *p, const double *x, double *y) {

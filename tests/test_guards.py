@@ -33,7 +33,7 @@ PROBE_VARS = ["SPMV_BIN_DEBUG", "SPMV_BIN_PADLOG", "SPMV_BIN_SUMWAVES", "SPMV_BI
               "SPMV_DIA_LDS_KB", "SPMV_LAUNCH_DIA_LDS_KB", "SPMV_ARENA_VMM_MB", "SPMV_LAUNCH_CSR",
               "SPMV_LAUNCH_CSR_U", "SPMV_LAUNCH_CSR_LDS_KB", "SPMV_LAUNCH_CSR_S", "SPMV_LAUNCH_ELL_O32", "SPMV_LAUNCH_ELL_UNROLL", "SPMV_LAUNCH_ELL_LDS_KB",
               "SPMV_BIN_MUL_PERM", "SPMV_BIN_PLACEMENT_GAP_MB", "SPMV_CSR_VAL_PLAIN", "SPMV_LAUNCH_COO_U",
-              "SPMV_LAUNCH_COO_BLOCKS"]
+              "SPMV_LAUNCH_COO_BLOCKS", "SPMV_LAUNCH_SS_WIN"]
 
 
 def _strings(path):

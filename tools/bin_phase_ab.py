@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--ncols", type=int, default=0)
     ap.add_argument("--per-row", type=int, default=16)
     ap.add_argument("--max-len", type=int, default=10000)
+    ap.add_argument("--band", default="-32,31", help="banded: lowest,highest diagonal offset")
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--placement", default="plain", help="default placement (a variant's placement=K overrides)")
@@ -42,7 +43,8 @@ def main():
     import singlespmv_amd as sp
     m = a.rows
     n = a.ncols or m
-    spec = sp.gen_spec(a.kind, n, n, per_row=a.per_row, max_len=a.max_len, seed=42)
+    blo, bhi = (int(v) for v in a.band.split(","))
+    spec = sp.gen_spec(a.kind, n, n, per_row=a.per_row, max_len=a.max_len, band_lo=blo, band_hi=bhi, seed=42)
     rp, col, val = sp.generate_csr(spec, 0, m)
     x = torch.from_numpy(sp.generate_vector(n, seed=43)).cuda()
     y = torch.empty(m, dtype=torch.float64, device="cuda")
