@@ -496,14 +496,20 @@ int build_jds(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
     const double mean = A.m ? (double)A.nnz / (double)A.m : 0.0;
     const int K = o.ell_width > 0 ? (int)round_up(o.ell_width, 4)
                                   : (int)std::max<int64_t>(64, round_up((int64_t)std::ceil(4.0 * mean), 4));
-    SPMV_RETURN_IF(build_ell(p, A, o, K, order.data()));
+    // rows already in non-increasing length order (equal lengths: config 4):
+    // the permutation is the identity, so the slices store rows in matrix
+    // order and the kernel writes y directly (no perm[] load, coalesced y)
+    bool identity = true;
+    for (int64_t r = 0; r < A.m && identity; ++r) identity = order[(size_t)r] == r;
+    SPMV_RETURN_IF(build_ell(p, A, o, K, identity ? nullptr : order.data()));
     const int64_t ell_slots = p->stored_slots;
-    SPMV_RETURN_IF(upload(p, &p->ell.perm, order.data(), A.m));
+    if (!identity) SPMV_RETURN_IF(upload(p, &p->ell.perm, order.data(), A.m));
     SPMV_RETURN_IF(build_overflow(p, A, K));
     p->stored_slots = ell_slots + p->hyb.nnz;
-    p->algo_bytes = 12 * A.nnz + 8 * A.n + 8 * A.m + 4 * A.m + 12 * p->hyb.n_rows;
+    p->algo_bytes = 12 * A.nnz + 8 * A.n + 8 * A.m + (identity ? 0 : 4 * A.m) + 12 * p->hyb.n_rows;
     p->n_kernels = p->hyb.n_rows ? 2 : 1;
-    p->kernel_name = p->hyb.n_rows ? "ell_slice_kernel<perm>+csr_adaptive_kernel" : "ell_slice_kernel<perm>";
+    const std::string ek = identity ? "ell_slice_kernel" : "ell_slice_kernel<perm>";
+    p->kernel_name = p->hyb.n_rows ? ek + "+csr_adaptive_kernel" : ek;
     return SPMV_SUCCESS;
 }
 

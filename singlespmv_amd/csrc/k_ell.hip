@@ -39,6 +39,10 @@ __global__ __launch_bounds__(256) void ell_slice_kernel(int64_t m, int64_t n_sli
     const int64_t slice = (int64_t)blockIdx.x * (blockDim.x / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (slice >= n_slices) return;
+    const int64_t srow = slice * 64 + lane;
+    // JDS: the matrix row, loaded before the slots so its latency hides
+    // behind them instead of trailing the wave
+    const int64_t row = PERM ? (srow < m ? (int64_t)perm[srow] : 0) : srow;
     const int64_t base = slice_off[slice];
     const int64_t quads = (slice_off[slice + 1] - base) >> 8;  // (width/4)
     const int32_t *cs = col + base;  // wave-uniform slice bases
@@ -88,11 +92,8 @@ __global__ __launch_bounds__(256) void ell_slice_kernel(int64_t m, int64_t n_sli
         acc = madd(b.x, g2, acc);
         acc = madd(b.y, g3, acc);
     }
-    const int64_t srow = slice * 64 + lane;
     if (srow < m) {
-        const int64_t row = PERM ? (int64_t)perm[srow] : srow;  // JDS: back to matrix order
         if (ADD) y[row] = __dadd_rn(y[row], acc);
-        else if (PERM) y[row] = acc;
         else __builtin_nontemporal_store(acc, y + row);  // not re-read: streamed out
     }
 }

@@ -306,8 +306,8 @@ def test_css_multi_pass():
 def test_jds_permutation_and_coo_atomics():
     """JDS (rows sorted by length, y permuted back) is the sequential row sum
     for rows up to its jagged-diagonal cap, within 1e-12 beyond;
-    COO (one f64 atomic per row run per wave) is within 1e-12 and
-    reproducible for every row that sits inside one 64-entry step."""
+    COO (one f64 atomic per row run per 128-entry unit) is within 1e-12 and
+    reproducible for every row that sits inside one unit."""
     m = 50000
     spec = sp.gen_spec("powerlaw", m, max_len=1500, seed=73)
     rp, col, val = sp.generate_csr(spec)
@@ -325,12 +325,28 @@ def test_jds_permutation_and_coo_atomics():
     y = np.full(m, np.nan)
     pc.execute(x, y)
     check_close(y, yo, what="coo")
-    # a row inside one 64-entry step gets exactly one atomic: reproducible
+    # a row inside one 128-entry unit gets exactly one atomic: reproducible
     lens = np.diff(rp)
-    inside = (rp[:-1] // 64 == (rp[1:] - 1) // 64) & (lens > 0)
+    inside = (rp[:-1] // 128 == (rp[1:] - 1) // 128) & (lens > 0)
     y2 = np.full(m, np.nan)
     pc.execute(x, y2)
     assert np.array_equal(y[inside], y2[inside])
+
+
+def test_jds_identity_order_is_ell():
+    """Rows already in non-increasing length order (equal lengths here): JDS
+    keeps matrix order -- no permutation array, ELL's kernel and y, bit for
+    bit; the oracle's sequential row sums too."""
+    m = 30000
+    rp, col, val = sp.generate_csr(sp.gen_spec("uniform", m, per_row=16, seed=5))
+    assert len(set(np.diff(rp).tolist())) == 1
+    x = sp.generate_vector(m, seed=6)
+    pj = sp.Plan.from_csr(m, m, rp, col, val, "jds")
+    pe = sp.Plan.from_csr(m, m, rp, col, val, "ell")
+    assert pj.info()["kernel"] == "ell_slice_kernel"
+    yj, ye = run_plan(pj, x, m), run_plan(pe, x, m)
+    assert np.array_equal(yj, ye)
+    assert np.array_equal(yj, oracle_y(rp, col, val, x))
 
 
 def test_integer_exact_all_formats():
