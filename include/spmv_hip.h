@@ -185,13 +185,16 @@ int spmv_plan_create_csr32(int32_t m, int32_t n, int32_t nnz, const int32_t *row
                            const spmv_options_t *opt, spmv_plan_t *plan);
 
 /* Plan from a CSR that already lives in device memory (64-bit row pointers;
- * all three arrays on the plan's device, only read).  CSR and SS are
- * converted on the device (the CSR5 conversion pipeline,
- * CSR5_cuda/detail/cuda/format_cuda.h:21-718), and so is BIN when every
- * row's columns are ascending by 20480-column strip (only the row pointers
- * and the (bin, strip) counts visit the host); every other format, and
- * AUTO, copies the CSR to the host and takes the host builder.  The input is
- * validated on the device like spmv_plan_create_csr's host check. */
+ * all three arrays on the plan's device, only read).  Every format but CSS
+ * is built on the device (the CSR5 conversion pipeline's role,
+ * CSR5_cuda/detail/cuda/format_cuda.h:21-718): only the row pointers (and,
+ * for BIN, the (bin, strip) counts) visit the host, for the layout decisions
+ * that depend on row lengths alone; AUTO is resolved there too, its diagonal
+ * census run on the device.  The layouts are byte-identical to the host
+ * builders' (spmv_plan_digest).  CSS, and BIN when some row's columns are not
+ * ascending by 20480-column strip, copy the CSR to the host and take the
+ * host builder.  The input is validated on the device like
+ * spmv_plan_create_csr's host check. */
 int spmv_plan_create_csr_device(int64_t m, int64_t n, int64_t nnz, const int64_t *d_row_ptr,
                                 const int32_t *d_col_idx, const double *d_val,
                                 const spmv_options_t *opt, spmv_plan_t *plan);
@@ -336,6 +339,16 @@ typedef struct spmv_plan_info {
 
 int spmv_plan_info(spmv_plan_t plan, spmv_plan_info_t *info);
 
+/* Layout digest (new; a check, not a compute path): one 64-bit hash per
+ * device array of the plan (its logical bytes, position-keyed), so two plans
+ * of one matrix -- e.g. a host build and a device build -- can be compared
+ * array by array without copying them out.  *n_arrays = the plan's array
+ * count (digests beyond `cap` are not written); spmv_plan_digest_name(plan,
+ * k) names array k.  CSR, ELL, HYB, JDS, SS, DIA and COO plans; BIN and CSS
+ * return SPMV_ERROR_NOT_SUPPORTED. */
+int spmv_plan_digest(spmv_plan_t plan, uint64_t *digests, int32_t cap, int32_t *n_arrays);
+const char *spmv_plan_digest_name(spmv_plan_t plan, int32_t k);
+
 const char *spmv_status_string(int status);
 /* Detail of the last failure on the calling thread ("" if none). */
 const char *spmv_last_error(void);
@@ -355,6 +368,19 @@ typedef struct spmv_dist_s *spmv_dist_t;
 /* The row cut a dist plan uses: cuts[parts+1] (spmv_partition_rows) and the
  * padded slice length (the longest range, >= 1).  Host only. */
 int spmv_dist_layout(const int64_t *row_ptr, int64_t m, int32_t parts, int64_t *cuts, int64_t *slice_rows);
+
+/* Host halves of a dist plan's data movement, exported so the reassembly can
+ * be checked without a second GPU (the same code runs inside
+ * spmv_dist_create_csr / spmv_dist_execute):
+ *   spmv_dist_shard     part k's rows [cuts[k], cuts[k+1]): rp (rows + 1
+ *                       entries) = row_ptr rebased to the part's first entry,
+ *                       *entry0 = that entry (its col / val start there)
+ *   spmv_dist_assemble  y (m doubles) from the all-gathered buffer of `parts`
+ *                       slices of `slice` rows each (part k's rows at the
+ *                       start of slice k, padding after them) */
+int spmv_dist_shard(const int64_t *row_ptr, const int64_t *cuts, int32_t parts, int32_t k, int64_t *rp,
+                    int64_t *entry0);
+int spmv_dist_assemble(const double *gathered, const int64_t *cuts, int32_t parts, int64_t slice, double *y);
 
 /* devices: n_devices distinct ordinals, or NULL for 0..n_devices-1.  opt
  * applies to every per-device plan (opt->device is ignored). */

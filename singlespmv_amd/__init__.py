@@ -106,6 +106,7 @@ EXPORTS = [
     "spmv_load_csr_bin", "spmv_lds_order_probe", "spmv_dist_layout", "spmv_dist_create_csr",
     "spmv_dist_execute", "spmv_dist_time", "spmv_dist_info", "spmv_dist_destroy", "spmv_stream_write_probe",
     "spmv_mixed_probe", "spmv_graph_create", "spmv_graph_launch", "spmv_graph_time", "spmv_graph_destroy",
+    "spmv_plan_digest", "spmv_plan_digest_name", "spmv_dist_shard", "spmv_dist_assemble",
 ]
 
 _lib = None
@@ -153,6 +154,8 @@ def lib():
     L.spmv_gather_probe.argtypes = [i32, i64, i64, C.POINTER(f64)]
     L.spmv_lds_order_probe.argtypes = [i32, i32, _I32P, _F64P, _F64P]
     L.spmv_dist_layout.argtypes = [_I64P, i64, i32, _I64P, C.POINTER(i64)]
+    L.spmv_dist_shard.argtypes = [_I64P, _I64P, i32, i32, _I64P, C.POINTER(i64)]
+    L.spmv_dist_assemble.argtypes = [_F64P, _I64P, i32, i64, _F64P]
     L.spmv_dist_create_csr.argtypes = [i32, vp, i64, i64, i64, vp, vp, vp, C.POINTER(Options), C.POINTER(vp)]
     L.spmv_dist_execute.argtypes = [vp, vp, vp, C.c_uint32]
     L.spmv_dist_time.argtypes = [vp, i32, C.POINTER(f64), C.POINTER(f64)]
@@ -161,6 +164,9 @@ def lib():
     L.spmv_phase_name.argtypes = [vp, i32]
     L.spmv_phase_name.restype = C.c_char_p
     L.spmv_plan_info.argtypes = [vp, C.POINTER(PlanInfo)]
+    L.spmv_plan_digest.argtypes = [vp, C.POINTER(C.c_uint64), i32, C.POINTER(i32)]
+    L.spmv_plan_digest_name.argtypes = [vp, i32]
+    L.spmv_plan_digest_name.restype = C.c_char_p
     L.spmv_status_string.argtypes = [C.c_int]
     L.spmv_status_string.restype = C.c_char_p
     L.spmv_last_error.restype = C.c_char_p
@@ -470,8 +476,8 @@ class Plan:
     @classmethod
     def from_device_csr(cls, m: int, n: int, row_ptr, col, val, fmt="auto", **opts) -> "Plan":
         """Plan from torch CUDA tensors (int64 row_ptr, int32 col, float64
-        val): CSR, SS and BIN are converted on the device, other formats
-        stage through the host (spmv_plan_create_csr_device)."""
+        val): every format but CSS is built on the device, AUTO resolved
+        there (spmv_plan_create_csr_device); CSS stages through the host."""
         for name, t, dt in (("row_ptr", row_ptr, torch.int64), ("col", col, torch.int32),
                             ("val", val, torch.float64)):
             if not _is_device(t) or t.dtype != dt or not t.is_contiguous():
@@ -565,6 +571,15 @@ class Plan:
         _check(lib().spmv_plan_info(self._h, C.byref(i)), "spmv_plan_info")
         return i.as_dict()
 
+    def digest(self) -> dict:
+        """{array name: 64-bit layout digest} (spmv_plan_digest): equal dicts
+        = byte-identical device layouts."""
+        n = C.c_int32(0)
+        _check(lib().spmv_plan_digest(self._h, None, 0, C.byref(n)), "spmv_plan_digest")
+        buf = (C.c_uint64 * max(1, n.value))()
+        _check(lib().spmv_plan_digest(self._h, buf, n.value, C.byref(n)), "spmv_plan_digest")
+        return {lib().spmv_plan_digest_name(self._h, k).decode(): int(buf[k]) for k in range(n.value)}
+
     def destroy(self) -> None:
         if self._h is not None and self._h.value:
             lib().spmv_plan_destroy(self._h)
@@ -575,6 +590,26 @@ class Plan:
             self.destroy()
         except Exception:
             pass
+
+
+def dist_shard(row_ptr, cuts, k: int):
+    """(rebased row pointers, first entry) of part k of a dist plan
+    (spmv_dist_shard, host only)."""
+    rp = np.ascontiguousarray(row_ptr, np.int64)
+    c = np.ascontiguousarray(cuts, np.int64)
+    out = np.empty(int(c[k + 1] - c[k]) + 1, np.int64)
+    e0 = C.c_int64(0)
+    _check(lib().spmv_dist_shard(rp, c, len(c) - 1, k, out, C.byref(e0)), "spmv_dist_shard")
+    return out, e0.value
+
+
+def dist_assemble(gathered, cuts, slice_rows: int) -> np.ndarray:
+    """y from the all-gathered padded slices (spmv_dist_assemble, host only)."""
+    g = np.ascontiguousarray(gathered, np.float64)
+    c = np.ascontiguousarray(cuts, np.int64)
+    y = np.empty(int(c[-1]), np.float64)
+    _check(lib().spmv_dist_assemble(g, c, len(c) - 1, slice_rows, y), "spmv_dist_assemble")
+    return y
 
 
 def dist_layout(row_ptr, parts: int):

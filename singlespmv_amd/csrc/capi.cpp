@@ -219,39 +219,76 @@ int spmv_plan_create_csr_device(int64_t m, int64_t n, int64_t nnz, const int64_t
         }
     }
     SPMV_RETURN_IF(validate_csr_device(d_row_ptr, m, d_col_idx, nnz, n));
-    const bool on_device = o.format == SPMV_FORMAT_CSR || o.format == SPMV_FORMAT_SS ||
-                           (o.format == SPMV_FORMAT_BIN && !probe_env("SPMV_BIN_HOST_BUILD"));
-    if (on_device) {
-        spmv_plan_s *p = new (std::nothrow) spmv_plan_s;
-        if (!p) {
-            set_error("host allocation of the plan failed");
-            return SPMV_ERROR_OUT_OF_MEMORY;
+    spmv_plan_s *p = new (std::nothrow) spmv_plan_s;
+    if (!p) {
+        set_error("host allocation of the plan failed");
+        return SPMV_ERROR_OUT_OF_MEMORY;
+    }
+    p->device = dev;
+    p->arena.device = dev;
+    if (const char *e = probe_env("SPMV_ARENA_VMM_MB")) p->arena.vmm_min = (size_t)std::max(0, std::atoi(e)) << 20;
+    p->m = m;
+    p->n = n;
+    p->nnz = nnz;
+    // the row pointers are the only part of the matrix the host sees: row
+    // lengths drive AUTO and every slice / bin / overflow decision
+    std::vector<int64_t> hrp;
+    const bool need_rp = o.format == SPMV_FORMAT_AUTO || o.format == SPMV_FORMAT_ELL || o.format == SPMV_FORMAT_HYB ||
+                         o.format == SPMV_FORMAT_JDS;
+    if (need_rp) {
+        hrp.resize((size_t)m + 1);
+        const hipError_t e = hipMemcpy(hrp.data(), d_row_ptr, 8 * (size_t)(m + 1), hipMemcpyDeviceToHost);
+        if (e != hipSuccess) {
+            delete p;
+            set_error(std::string("row_ptr to host: ") + hipGetErrorString(e));
+            (void)hipGetLastError();
+            return SPMV_ERROR_HIP;
         }
-        p->device = dev;
-        p->arena.device = dev;
-        if (const char *e = probe_env("SPMV_ARENA_VMM_MB")) p->arena.vmm_min = (size_t)std::max(0, std::atoi(e)) << 20;
-        p->m = m;
-        p->n = n;
-        p->nnz = nnz;
-        stream_placement(p, o.format, o);
-        const double mean = m ? (double)nnz / (double)m : 0.0;
-        int st;
-        switch (o.format) {
+    }
+    const DevCsr A{m, n, nnz, hrp.data(), d_row_ptr, d_col_idx, d_val};
+    int fmt = o.format, st = SPMV_SUCCESS;
+    if (fmt == SPMV_FORMAT_AUTO) {
+        int census = SPMV_SUCCESS;
+        fmt = choose_format_rp(m, n, nnz, hrp.data(), o, [&]() {
+            std::vector<int32_t> offs;
+            census = dia_offsets_device(p, A, 256, 1.25, offs);
+            return census == SPMV_SUCCESS;
+        });
+        if (census != SPMV_SUCCESS && census != kDiaRefused) st = census;
+    }
+    const double mean = m ? (double)nnz / (double)m : 0.0;
+    bool host_build = false;
+    if (st == SPMV_SUCCESS) {
+        stream_placement(p, fmt, o);
+        switch (fmt) {
             case SPMV_FORMAT_CSR: st = build_csr_device(p, d_row_ptr, d_col_idx, d_val, o, mean); break;
             case SPMV_FORMAT_SS: st = build_ss_device(p, d_row_ptr, d_col_idx, d_val, o, mean); break;
-            default: st = build_bin_device(p, d_row_ptr, d_col_idx, d_val, o); break;
+            case SPMV_FORMAT_DIA: st = build_dia_device(p, A, o); break;
+            case SPMV_FORMAT_ELL: st = build_ell_device(p, A, o); break;
+            case SPMV_FORMAT_HYB: st = build_hyb_device(p, A, o); break;
+            case SPMV_FORMAT_JDS: st = build_jds_device(p, A, o); break;
+            case SPMV_FORMAT_COO: st = build_coo_device(p, A, o); break;
+            case SPMV_FORMAT_BIN:
+                if (probe_env("SPMV_BIN_HOST_BUILD")) host_build = true;
+                else st = build_bin_device(p, d_row_ptr, d_col_idx, d_val, o);
+                // BIN's device fill needs every row's column strips
+                // non-decreasing; other CSRs take the host builder below
+                if (st == kBinNeedHostBuild) host_build = true;
+                break;
+            case SPMV_FORMAT_CSS: host_build = true; break;  // CSS: host builder only
+            default:
+                set_error("unknown format");
+                st = SPMV_ERROR_INVALID_VALUE;
         }
-        if (st == SPMV_SUCCESS) {
-            p->format = o.format;
-            *out = p;
-            return SPMV_SUCCESS;
-        }
-        p->arena.release();
-        delete p;
-        // BIN's device fill needs every row's column strips non-decreasing;
-        // other CSRs take the host builder below
-        if (st != kBinNeedHostBuild) return st;
     }
+    if (st == SPMV_SUCCESS && !host_build) {
+        p->format = fmt;
+        *out = p;
+        return SPMV_SUCCESS;
+    }
+    p->arena.release();
+    delete p;
+    if (!host_build) return st;
     {
         // host builders: stage the CSR through host memory
         std::vector<int64_t> rp((size_t)m + 1);
@@ -263,8 +300,9 @@ int spmv_plan_create_csr_device(int64_t m, int64_t n, int64_t nnz, const int64_t
             SPMV_HIP_TRY(hipMemcpy(val.data(), d_val, 8 * (size_t)nnz, hipMemcpyDeviceToHost));
         }
         o.device = dev;
-        HostCsr A{m, n, nnz, rp.data(), col.data(), val.data()};
-        return create_from_csr(A, &o, out);
+        o.format = fmt;  // AUTO resolved above
+        HostCsr H{m, n, nnz, rp.data(), col.data(), val.data()};
+        return create_from_csr(H, &o, out);
     }
 }
 

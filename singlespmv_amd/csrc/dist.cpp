@@ -105,6 +105,30 @@ static int dist_gather_y(spmv_dist_s *d) {
     return SPMV_SUCCESS;
 }
 
+// The y reassembly of a dist plan: part k's rows [cuts[k], cuts[k+1]) sit at
+// the start of its slice in the all-gathered buffer (k * slice); one copy per
+// non-empty part.  Shared by spmv_dist_execute (device -> host copies) and
+// spmv_dist_assemble (host, testable without a second GPU).
+struct SliceCopy {
+    int64_t src, dst, rows;
+};
+static std::vector<SliceCopy> dist_copies(const int64_t *cuts, int32_t parts, int64_t slice) {
+    std::vector<SliceCopy> c;
+    for (int k = 0; k < parts; ++k) {
+        const int64_t rows = cuts[k + 1] - cuts[k];
+        if (rows > 0) c.push_back(SliceCopy{(int64_t)k * slice, cuts[k], rows});
+    }
+    return c;
+}
+
+// Part k's CSR: rows [cuts[k], cuts[k+1]) with row pointers rebased to its
+// first entry (global column indices kept); *entry0 = that entry's index.
+static void dist_shard_rows(const int64_t *row_ptr, const int64_t *cuts, int32_t k, int64_t *rp, int64_t *entry0) {
+    const int64_t r0 = cuts[k], r1 = cuts[k + 1], b = row_ptr[r0];
+    for (int64_t r = r0; r <= r1; ++r) rp[r - r0] = row_ptr[r] - b;
+    *entry0 = b;
+}
+
 static int dist_sync(spmv_dist_s *d) {
     for (int k = 0; k < d->nd; ++k) {
         SPMV_HIP_TRY(hipSetDevice(d->devs[k]));
@@ -125,6 +149,23 @@ int spmv_dist_layout(const int64_t *row_ptr, int64_t m, int32_t parts, int64_t *
     int64_t s = 1;
     for (int k = 0; k < parts; ++k) s = std::max<int64_t>(s, cuts[k + 1] - cuts[k]);
     *slice_rows = s;
+    return SPMV_SUCCESS;
+}
+
+int spmv_dist_shard(const int64_t *row_ptr, const int64_t *cuts, int32_t parts, int32_t k, int64_t *rp,
+                    int64_t *entry0) {
+    SPMV_CHECK_ARG(row_ptr && cuts && rp && entry0 && parts > 0 && k >= 0 && k < parts, "bad arguments");
+    SPMV_CHECK_ARG(cuts[k] <= cuts[k + 1], "cuts are not non-decreasing");
+    dist_shard_rows(row_ptr, cuts, k, rp, entry0);
+    return SPMV_SUCCESS;
+}
+
+int spmv_dist_assemble(const double *gathered, const int64_t *cuts, int32_t parts, int64_t slice, double *y) {
+    SPMV_CHECK_ARG(gathered && cuts && y && parts > 0 && slice >= 1, "bad arguments");
+    for (int k = 0; k < parts; ++k)
+        SPMV_CHECK_ARG(cuts[k] <= cuts[k + 1] && cuts[k + 1] - cuts[k] <= slice, "a part is longer than the slice");
+    for (const SliceCopy &c : dist_copies(cuts, parts, slice))
+        std::memcpy(y + c.dst, gathered + c.src, 8 * (size_t)c.rows);
     return SPMV_SUCCESS;
 }
 
@@ -182,9 +223,10 @@ int spmv_dist_create_csr(int32_t n_devices, const int32_t *devices, int64_t m, i
         }
         d->streams.push_back(s);
         // this device's rows: rebased row pointers, global columns
-        const int64_t r0 = d->cuts[k], r1 = d->cuts[k + 1], b = row_ptr[r0];
+        const int64_t r0 = d->cuts[k], r1 = d->cuts[k + 1];
+        int64_t b = 0;
         rp.resize((size_t)(r1 - r0 + 1));
-        for (int64_t r = r0; r <= r1; ++r) rp[(size_t)(r - r0)] = row_ptr[r] - b;
+        dist_shard_rows(row_ptr, d->cuts.data(), k, rp.data(), &b);
         o.device = dev;
         spmv_plan_t p = nullptr;
         st = spmv_plan_create_csr(r1 - r0, n, row_ptr[r1] - b, rp.data(), col_idx ? col_idx + b : nullptr,
@@ -249,12 +291,9 @@ int spmv_dist_execute(spmv_dist_t d, const double *x, double *y, uint32_t flags)
     if (y) {
         SPMV_HIP_TRY(hipSetDevice(d->devs[0]));
         const double *full = d->d_yfull[0];
-        for (int k = 0; k < d->nd; ++k) {
-            const int64_t rows = d->cuts[k + 1] - d->cuts[k];
-            if (rows)
-                SPMV_HIP_TRY(hipMemcpyAsync(y + d->cuts[k], full + (int64_t)k * d->slice, 8 * (size_t)rows,
-                                            hipMemcpyDeviceToHost, d->streams[0]));
-        }
+        for (const SliceCopy &c : dist_copies(d->cuts.data(), d->nd, d->slice))
+            SPMV_HIP_TRY(hipMemcpyAsync(y + c.dst, full + c.src, 8 * (size_t)c.rows, hipMemcpyDeviceToHost,
+                                        d->streams[0]));
     }
     return dist_sync(d);
 }

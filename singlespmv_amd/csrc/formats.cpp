@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <limits>
 #include <numeric>
 #include <queue>
@@ -242,11 +243,18 @@ int csr_plan_lanes(spmv_plan_s *p, const int64_t *row_ptr, int64_t m, const spmv
     for (int64_t r = 0; r < m; r += 64)
         slab_max = std::max<int64_t>(slab_max, row_ptr[std::min<int64_t>(r + 64, m)] - row_ptr[r]);
     c.off32 = slab_max + 512 < ((int64_t)1 << 28) && p->n < ((int64_t)1 << 29);
+    c.slab_max = slab_max;
     if (o.csr_lanes > 0) {
         c.lanes = o.csr_lanes;
         if (c.lanes < 1 || c.lanes > 64 || (c.lanes & (c.lanes - 1))) {
             set_error("csr_lanes must be a power of two in [1, 64]");
             return SPMV_ERROR_INVALID_VALUE;
+        }
+        // the row-group kernels hold a slab's row starts and entry index in
+        // 32 bits, measured from the slab's first entry
+        if (slab_max + 512 >= (int64_t)INT32_MAX) {
+            set_error("csr_lanes: a 64-row slab holds >= 2^31 entries; use csr_lanes = 0 (adaptive)");
+            return SPMV_ERROR_NOT_SUPPORTED;
         }
         return SPMV_SUCCESS;
     }
@@ -378,6 +386,38 @@ int build_csr(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
 }
 
 // ---------------------------------------------------------------- ELL
+// Slice offsets of the sliced-ELL layout from the row pointers alone (shared
+// by the host and the device builders): slice s of 64 rows (rows order[i] when
+// order is given) has width round_up(min(longest row, cap), 4); off[s] is its
+// first slot, off[n_slices] the total.  Returns the widest slice.
+int ell_slice_offsets(const int64_t *row_ptr, int64_t m, int cap, const int32_t *order, std::vector<int64_t> &off) {
+    auto src = [&](int64_t r) -> int64_t { return order ? (int64_t)order[r] : r; };
+    const int64_t ns = (m + 63) / 64;
+    off.assign((size_t)ns + 1, 0);
+    int maxw = 0;
+#pragma omp parallel for schedule(static) reduction(max : maxw)
+    for (int64_t s = 0; s < ns; ++s) {
+        int64_t w = 0;
+        const int64_t r1 = std::min<int64_t>(m, (s + 1) * 64);
+        for (int64_t r = s * 64; r < r1; ++r) w = std::max<int64_t>(w, row_ptr[src(r) + 1] - row_ptr[src(r)]);
+        w = std::min<int64_t>(w, cap);
+        w = round_up(w, 4);
+        off[s + 1] = 64 * w;
+        maxw = std::max<int>(maxw, (int)w);
+    }
+    for (int64_t s = 0; s < ns; ++s) off[s + 1] += off[s];
+    return maxw;
+}
+
+void ell_finish_info(spmv_plan_s *p, int maxw, int64_t total) {
+    p->ell.max_width = maxw;
+    p->ell.slots = total;
+    p->stored_slots = total;
+    p->algo_bytes = 12 * p->nnz + 8 * p->n + 8 * p->m;
+    p->n_kernels = 1;
+    p->kernel_name = "ell_slice_kernel";
+}
+
 // cap: maximum slots per row kept in the ELL part (HYB); INT32_MAX for ELL.
 // order (JDS): slice row i is matrix row order[i]; nullptr = identity.
 int build_ell(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &, int cap, const int32_t *order) {
@@ -385,19 +425,8 @@ int build_ell(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &, int cap,
     if (const char *u = probe_env("SPMV_ELL_UNROLL")) e.unroll = std::atoi(u);
     auto src = [&](int64_t r) -> int64_t { return order ? (int64_t)order[r] : r; };
     e.n_slices = (A.m + 63) / 64;
-    std::vector<int64_t> off((size_t)e.n_slices + 1, 0);
-    int maxw = 0;
-#pragma omp parallel for schedule(static) reduction(max : maxw)
-    for (int64_t s = 0; s < e.n_slices; ++s) {
-        int64_t w = 0;
-        const int64_t r1 = std::min<int64_t>(A.m, (s + 1) * 64);
-        for (int64_t r = s * 64; r < r1; ++r) w = std::max<int64_t>(w, A.row_ptr[src(r) + 1] - A.row_ptr[src(r)]);
-        w = std::min<int64_t>(w, cap);
-        w = round_up(w, 4);
-        off[s + 1] = 64 * w;
-        maxw = std::max<int>(maxw, (int)w);
-    }
-    for (int64_t s = 0; s < e.n_slices; ++s) off[s + 1] += off[s];
+    std::vector<int64_t> off;
+    const int maxw = ell_slice_offsets(A.row_ptr, A.m, cap, order, off);
     const int64_t total = off[e.n_slices];
     std::vector<int32_t> col((size_t)total);
     std::vector<double> val((size_t)total);
@@ -433,32 +462,43 @@ int build_ell(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &, int cap,
     SPMV_RETURN_IF(upload(p, &e.slice_off, off.data(), e.n_slices + 1));
     SPMV_RETURN_IF(upload(p, &e.col, col.data(), total));
     SPMV_RETURN_IF(upload(p, &e.val, val.data(), total));
-    e.max_width = maxw;
-    e.slots = total;
-    p->stored_slots = total;
-    p->algo_bytes = 12 * A.nnz + 8 * A.n + 8 * A.m;
-    p->n_kernels = 1;
-    p->kernel_name = "ell_slice_kernel";
+    ell_finish_info(p, maxw, total);
     return SPMV_SUCCESS;
 }
 
-// ---------------------------------------------------------------- JDS
-// opt_jds (src/opt_jds.cpp:29-71): rows sorted by decreasing length (stable),
-// stored as 64-row jagged slices of the sliced-ELL layout; y is written back
-// through the permutation.  Each row is still summed in its own order.
+// ---------------------------------------------------------------- HYB / JDS overflow
 // The entries of rows longer than K beyond their first K go to a CSR over
-// those rows only (the HYB overflow), finished by hyb_overflow_kernel.
-static int build_overflow(spmv_plan_s *p, const HostCsr &A, int K) {
-    HybDev &h = p->hyb;
-    std::vector<int32_t> rows;
-    std::vector<int64_t> rp(1, 0);
-    for (int64_t r = 0; r < A.m; ++r) {
-        const int64_t len = A.row_ptr[r + 1] - A.row_ptr[r];
+// those rows only (finished by the adaptive CSR kernel in y += mode).  The
+// row list and its row pointers come from the matrix's row pointers alone.
+void overflow_layout(const int64_t *row_ptr, int64_t m, int K, std::vector<int32_t> &rows, std::vector<int64_t> &rp) {
+    rows.clear();
+    rp.assign(1, 0);
+    for (int64_t r = 0; r < m; ++r) {
+        const int64_t len = row_ptr[r + 1] - row_ptr[r];
         if (len > K) {
             rows.push_back((int32_t)r);
             rp.push_back(rp.back() + (len - K));
         }
     }
+}
+
+// the overflow rows' index arrays (rows, row pointers, length bins) to the device
+int overflow_upload_index(spmv_plan_s *p, const std::vector<int32_t> &rows, const std::vector<int64_t> &rp) {
+    HybDev &h = p->hyb;
+    h.n_rows = (int64_t)rows.size();
+    h.nnz = rp.back();
+    SPMV_RETURN_IF(upload(p, &h.rows, rows.data(), h.n_rows));
+    SPMV_RETURN_IF(upload(p, &h.row_ptr, rp.data(), h.n_rows + 1));
+    std::vector<int32_t> binned;
+    csr_bin_rows(rp.data(), h.n_rows, binned, h.bin_off);
+    return upload(p, &h.bin_rows, binned.data(), h.n_rows);
+}
+
+static int build_overflow(spmv_plan_s *p, const HostCsr &A, int K) {
+    HybDev &h = p->hyb;
+    std::vector<int32_t> rows;
+    std::vector<int64_t> rp;
+    overflow_layout(A.row_ptr, A.m, K, rows, rp);
     h.n_rows = (int64_t)rows.size();
     h.nnz = rp.back();
     std::vector<int32_t> col((size_t)h.nnz);
@@ -469,12 +509,8 @@ static int build_overflow(spmv_plan_s *p, const HostCsr &A, int K) {
         std::memcpy(&col[rp[i]], A.col + src, sizeof(int32_t) * (size_t)(rp[i + 1] - rp[i]));
         std::memcpy(&val[rp[i]], A.val + src, sizeof(double) * (size_t)(rp[i + 1] - rp[i]));
     }
-    SPMV_RETURN_IF(upload(p, &h.rows, rows.data(), h.n_rows));
-    SPMV_RETURN_IF(upload(p, &h.row_ptr, rp.data(), h.n_rows + 1));
     // overflow rows binned by overflow length (adaptive kernel, y +=)
-    std::vector<int32_t> binned;
-    csr_bin_rows(rp.data(), h.n_rows, binned, h.bin_off);
-    SPMV_RETURN_IF(upload(p, &h.bin_rows, binned.data(), h.n_rows));
+    SPMV_RETURN_IF(overflow_upload_index(p, rows, rp));
     SPMV_RETURN_IF(upload(p, &h.col, col.data(), h.nnz, kPad));
     SPMV_RETURN_IF(upload(p, &h.val, val.data(), h.nnz, kPad));
     return SPMV_SUCCESS;
@@ -487,29 +523,59 @@ static int build_overflow(spmv_plan_s *p, const HostCsr &A, int K) {
 // (default max(64, 4 x mean row length)); the entries of longer rows beyond K
 // are finished by the overflow kernel, so the longest-row slices do not run
 // as single waves.  Rows of length <= K are the sequential sum, bit for bit.
-int build_jds(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
-    std::vector<int32_t> order((size_t)std::max<int64_t>(A.m, 1));
-    std::iota(order.begin(), order.begin() + A.m, 0);
-    std::stable_sort(order.begin(), order.begin() + A.m, [&](int32_t a, int32_t b) {
-        return A.row_ptr[a + 1] - A.row_ptr[a] > A.row_ptr[b + 1] - A.row_ptr[b];
-    });
-    const double mean = A.m ? (double)A.nnz / (double)A.m : 0.0;
-    const int K = o.ell_width > 0 ? (int)round_up(o.ell_width, 4)
-                                  : (int)std::max<int64_t>(64, round_up((int64_t)std::ceil(4.0 * mean), 4));
-    // rows already in non-increasing length order (equal lengths: config 4):
-    // the permutation is the identity, so the slices store rows in matrix
-    // order and the kernel writes y directly (no perm[] load, coalesced y)
+// JDS row order (rows by decreasing length, stable -- std::stable_sort's
+// order, by a counting sort over the lengths) and the jagged-diagonal cap K
+// (default max(64, 4 x mean row length)).  Returns true when the order is the
+// identity (rows already in non-increasing length order, config 4): the
+// slices then store rows in matrix order and the kernel writes y directly (no
+// perm[] load, coalesced y).
+bool jds_layout(const int64_t *row_ptr, int64_t m, int64_t nnz, const spmv_options_t &o, std::vector<int32_t> &order,
+                int *K) {
+    order.assign((size_t)std::max<int64_t>(m, 1), 0);
+    int64_t maxlen = 0;
     bool identity = true;
-    for (int64_t r = 0; r < A.m && identity; ++r) identity = order[(size_t)r] == r;
+    for (int64_t r = 0; r < m; ++r) {
+        const int64_t len = row_ptr[r + 1] - row_ptr[r];
+        if (r && len > row_ptr[r] - row_ptr[r - 1]) identity = false;
+        maxlen = std::max(maxlen, len);
+    }
+    if (identity) {
+        std::iota(order.begin(), order.begin() + m, 0);
+    } else if (maxlen <= ((int64_t)1 << 24)) {
+        // bucket start of length L = rows longer than L (descending, stable)
+        std::vector<int64_t> start((size_t)maxlen + 2, 0);
+        for (int64_t r = 0; r < m; ++r) ++start[(size_t)(maxlen - (row_ptr[r + 1] - row_ptr[r]) + 1)];
+        for (int64_t k = 1; k <= maxlen + 1; ++k) start[(size_t)k] += start[(size_t)k - 1];
+        for (int64_t r = 0; r < m; ++r) order[(size_t)start[(size_t)(maxlen - (row_ptr[r + 1] - row_ptr[r]))]++] = (int32_t)r;
+    } else {
+        std::iota(order.begin(), order.begin() + m, 0);
+        std::stable_sort(order.begin(), order.begin() + m, [&](int32_t a, int32_t b) {
+            return row_ptr[a + 1] - row_ptr[a] > row_ptr[b + 1] - row_ptr[b];
+        });
+    }
+    const double mean = m ? (double)nnz / (double)m : 0.0;
+    *K = o.ell_width > 0 ? (int)round_up(o.ell_width, 4)
+                         : (int)std::max<int64_t>(64, round_up((int64_t)std::ceil(4.0 * mean), 4));
+    return identity;
+}
+
+void jds_finish_info(spmv_plan_s *p, bool identity, int64_t ell_slots) {
+    p->stored_slots = ell_slots + p->hyb.nnz;
+    p->algo_bytes = 12 * p->nnz + 8 * p->n + 8 * p->m + (identity ? 0 : 4 * p->m) + 12 * p->hyb.n_rows;
+    p->n_kernels = p->hyb.n_rows ? 2 : 1;
+    const std::string ek = identity ? "ell_slice_kernel" : "ell_slice_kernel<perm>";
+    p->kernel_name = p->hyb.n_rows ? ek + "+csr_adaptive_kernel" : ek;
+}
+
+int build_jds(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
+    std::vector<int32_t> order;
+    int K = 0;
+    const bool identity = jds_layout(A.row_ptr, A.m, A.nnz, o, order, &K);
     SPMV_RETURN_IF(build_ell(p, A, o, K, identity ? nullptr : order.data()));
     const int64_t ell_slots = p->stored_slots;
     if (!identity) SPMV_RETURN_IF(upload(p, &p->ell.perm, order.data(), A.m));
     SPMV_RETURN_IF(build_overflow(p, A, K));
-    p->stored_slots = ell_slots + p->hyb.nnz;
-    p->algo_bytes = 12 * A.nnz + 8 * A.n + 8 * A.m + (identity ? 0 : 4 * A.m) + 12 * p->hyb.n_rows;
-    p->n_kernels = p->hyb.n_rows ? 2 : 1;
-    const std::string ek = identity ? "ell_slice_kernel" : "ell_slice_kernel<perm>";
-    p->kernel_name = p->hyb.n_rows ? ek + "+csr_adaptive_kernel" : ek;
+    jds_finish_info(p, identity, ell_slots);
     return SPMV_SUCCESS;
 }
 
@@ -529,17 +595,22 @@ int build_coo(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &) {
     SPMV_RETURN_IF(upload(p, &c.row, row.data(), total));
     SPMV_RETURN_IF(upload(p, &c.col, A.col, A.nnz, total - A.nnz));
     SPMV_RETURN_IF(upload(p, &c.val, A.val, A.nnz, total - A.nnz));
-    p->stored_slots = total;
-    p->algo_bytes = 16 * A.nnz + 8 * A.n + 8 * A.m;
-    p->n_kernels = 2;
-    p->kernel_name = "coo_pair_kernel";
+    coo_finish_info(p);
     return SPMV_SUCCESS;
 }
 
+void coo_finish_info(spmv_plan_s *p) {
+    p->stored_slots = p->coo.n_units * kCooUnit;
+    p->algo_bytes = 16 * p->nnz + 8 * p->n + 8 * p->m;
+    p->n_kernels = 2;
+    p->kernel_name = "coo_pair_kernel";
+}
+
 // ---------------------------------------------------------------- HYB
-static int choose_hyb_width(const HostCsr &A) {
+int choose_hyb_width(const int64_t *row_ptr, int64_t m) {
     // minimise modelled bytes: ELL slots (incl. padding) + overflow entries
     // + per-overflow-row overhead, over K in {4, 8, ..., 256}
+    const HostCsr A{m, 0, 0, row_ptr, nullptr, nullptr};
     const int64_t ns = (A.m + 63) / 64;
     std::vector<int64_t> smax((size_t)ns);
 #pragma omp parallel for schedule(static)
@@ -566,18 +637,26 @@ static int choose_hyb_width(const HostCsr &A) {
     return bestK;
 }
 
-int build_hyb(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
-    const int K = o.ell_width > 0 ? (int)round_up(o.ell_width, 4) : choose_hyb_width(A);
-    SPMV_RETURN_IF(build_ell(p, A, o, K));
-    const int64_t ell_slots = p->stored_slots;
-    HybDev &h = p->hyb;
-    SPMV_RETURN_IF(build_overflow(p, A, K));
+int hyb_width(const int64_t *row_ptr, int64_t m, const spmv_options_t &o) {
+    return o.ell_width > 0 ? (int)round_up(o.ell_width, 4) : choose_hyb_width(row_ptr, m);
+}
+
+void hyb_finish_info(spmv_plan_s *p, int K, int64_t ell_slots) {
+    const HybDev &h = p->hyb;
     p->ell.max_width = K;
     p->stored_slots = ell_slots + h.nnz;
-    p->algo_bytes = 12 * A.nnz + 8 * A.n + 8 * A.m + 12 * h.n_rows;
+    p->algo_bytes = 12 * p->nnz + 8 * p->n + 8 * p->m + 12 * h.n_rows;
     p->n_kernels = h.n_rows ? 2 : 1;
     // every kernel of one execute ("a+b": the PMC traffic of an execute sums them)
     p->kernel_name = h.n_rows ? "ell_slice_kernel+csr_adaptive_kernel" : "ell_slice_kernel";
+}
+
+int build_hyb(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
+    const int K = hyb_width(A.row_ptr, A.m, o);
+    SPMV_RETURN_IF(build_ell(p, A, o, K));
+    const int64_t ell_slots = p->stored_slots;
+    SPMV_RETURN_IF(build_overflow(p, A, K));
+    hyb_finish_info(p, K, ell_slots);
     return SPMV_SUCCESS;
 }
 
@@ -678,7 +757,7 @@ static bool dia_offsets(const HostCsr &A, int max_diags, double max_fill, std::v
 // profiles/round1/probe/dia_placement.jsonl).  Copies of the values in up to
 // 8 allocations spread over the free device memory are timed with one
 // launch each over a zero x; the fastest is kept.
-static int dia_placement(spmv_plan_s *p, int64_t m, int64_t n, size_t bytes, const spmv_options_t &o) {
+int dia_placement(spmv_plan_s *p, int64_t m, int64_t n, size_t bytes, const spmv_options_t &o) {
     DiaDev &d = p->dia;
     int mode = o.placement;
     SPMV_RETURN_IF(placement_mode_check(mode));
@@ -837,10 +916,15 @@ int build_dia(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
         SPMV_RETURN_IF(upload(p, &d.val, val.data(), slots));
         SPMV_RETURN_IF(dia_placement(p, A.m, A.n, vbytes, oo));
     }
-    p->algo_bytes = 8 * A.nnz + 4 * (int64_t)d.n_diags + 8 * A.n + 8 * A.m;
+    dia_finish_info(p);
+    return SPMV_SUCCESS;
+}
+
+void dia_finish_info(spmv_plan_s *p) {
+    p->stored_slots = (int64_t)p->dia.n_diags * p->dia.mp;
+    p->algo_bytes = 8 * p->nnz + 4 * (int64_t)p->dia.n_diags + 8 * p->n + 8 * p->m;
     p->n_kernels = 1;
     p->kernel_name = "dia_kernel";
-    return SPMV_SUCCESS;
 }
 
 // ---------------------------------------------------------------- CSS
@@ -1115,16 +1199,25 @@ int build_css(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
 
 // ---------------------------------------------------------------- AUTO
 int choose_format(const HostCsr &A, const spmv_options_t &o) {
+    return choose_format_rp(A.m, A.n, A.nnz, A.row_ptr, o, [&]() {
+        std::vector<int32_t> offs;
+        return dia_offsets(A, 256, 1.25, offs);
+    });
+}
+
+// AUTO from the row-length histogram (row pointers only) plus, for short
+// rows, the diagonal census `dia_ok` (host: dia_offsets; a device CSR:
+// dia_offsets_device) -- the same decision for a host and a device CSR.
+int choose_format_rp(int64_t m, int64_t n, int64_t nnz, const int64_t *row_ptr, const spmv_options_t &o,
+                     const std::function<bool()> &dia_ok) {
+    const HostCsr A{m, n, nnz, row_ptr, nullptr, nullptr};
     if (A.m == 0 || A.nnz == 0) return SPMV_FORMAT_CSR;
     const double mean = (double)A.nnz / (double)A.m;
     int64_t maxlen = 0;
 #pragma omp parallel for schedule(static) reduction(max : maxlen)
     for (int64_t r = 0; r < A.m; ++r) maxlen = std::max<int64_t>(maxlen, A.row_ptr[r + 1] - A.row_ptr[r]);
     // banded: few, well-filled diagonals -> DIA moves 8 instead of 12 B/nnz
-    if (maxlen <= 512) {
-        std::vector<int32_t> offs;
-        if (dia_offsets(A, 256, 1.25, offs)) return SPMV_FORMAT_DIA;
-    }
+    if (maxlen <= 512 && dia_ok()) return SPMV_FORMAT_DIA;
     (void)o;
     // x beyond one XCD's 4 MiB L2 and enough rows to fill every CU: random
     // gathers dominate -> column-slab sweep (L2-resident x slabs).  Measured

@@ -7,6 +7,7 @@
 
 #include <cstdint>
 #include <cstdlib>
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -136,6 +137,7 @@ struct CsrDev {
     int lanes = 4;            // lanes per row (1..64); 0 = adaptive (bins)
     bool off32 = false;       // every 64-row slab spans < 2^28 entries and n < 2^29:
                               // 32-bit byte offsets in csr_slab2 (k_csr.hip)
+    int64_t slab_max = 0;     // entries of the widest 64-row slab
     int32_t *win0 = nullptr;  // [ceil(m / kCsrWinGroup)]: first column of each 256-row granule's
     int32_t win = 0;          //   x window; win = the widest window of kCsrSlabsPerWave granules
     int32_t win_s[3] = {};    //   ... of 1, 2, 4 granules (0: wider than kCsrMaxWin); null: none fits
@@ -451,6 +453,37 @@ int build_csr_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, 
 int build_ss_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, const double *d_val,
                     const spmv_options_t &o, double mean_row);
 int choose_format(const HostCsr &A, const spmv_options_t &o);
+int choose_format_rp(int64_t m, int64_t n, int64_t nnz, const int64_t *row_ptr, const spmv_options_t &o,
+                     const std::function<bool()> &dia_ok);
+// layout decisions that need the row pointers only (host and device builders)
+int ell_slice_offsets(const int64_t *row_ptr, int64_t m, int cap, const int32_t *order, std::vector<int64_t> &off);
+void ell_finish_info(spmv_plan_s *p, int maxw, int64_t total);
+void overflow_layout(const int64_t *row_ptr, int64_t m, int K, std::vector<int32_t> &rows, std::vector<int64_t> &rp);
+int overflow_upload_index(spmv_plan_s *p, const std::vector<int32_t> &rows, const std::vector<int64_t> &rp);
+bool jds_layout(const int64_t *row_ptr, int64_t m, int64_t nnz, const spmv_options_t &o, std::vector<int32_t> &order,
+                int *K);
+void jds_finish_info(spmv_plan_s *p, bool identity, int64_t ell_slots);
+int hyb_width(const int64_t *row_ptr, int64_t m, const spmv_options_t &o);
+void hyb_finish_info(spmv_plan_s *p, int K, int64_t ell_slots);
+void coo_finish_info(spmv_plan_s *p);
+void dia_finish_info(spmv_plan_s *p);
+int dia_placement(spmv_plan_s *p, int64_t m, int64_t n, size_t bytes, const spmv_options_t &o);
+// k_devbuild.hip -- the other formats from a device CSR (f2): only the row
+// pointers visit the host (layout decisions); entries move HBM -> HBM.
+struct DevCsr {
+    int64_t m, n, nnz;
+    const int64_t *h_rp;  // host copy of the row pointers
+    const int64_t *d_rp;
+    const int32_t *d_col;
+    const double *d_val;
+};
+constexpr int kDiaRefused = -1001;  // dia_offsets_device: too many diagonals / too much fill
+int dia_offsets_device(spmv_plan_s *p, const DevCsr &A, int max_diags, double max_fill, std::vector<int32_t> &offs);
+int build_dia_device(spmv_plan_s *p, const DevCsr &A, const spmv_options_t &o);
+int build_ell_device(spmv_plan_s *p, const DevCsr &A, const spmv_options_t &o);
+int build_hyb_device(spmv_plan_s *p, const DevCsr &A, const spmv_options_t &o);
+int build_jds_device(spmv_plan_s *p, const DevCsr &A, const spmv_options_t &o);
+int build_coo_device(spmv_plan_s *p, const DevCsr &A, const spmv_options_t &o);
 int auto_csr_lanes(double mean_row);
 int csr_plan_lanes(spmv_plan_s *p, const int64_t *row_ptr, int64_t m, const spmv_options_t &o);
 // x windows of csr_slabx from each granule's column range (lo, hi; hi < 0: no entries)

@@ -555,12 +555,15 @@ static void launch_slab_u(const spmv_plan_s *p, int kind, size_t lds, const doub
             hipLaunchKernelGGL(kern, dim3(grid), dim3(256), wl, p->stream, p->m, (const RP *)c.row_ptr, c.col, c.val,
                                x, y, c.win0, win, p->n, c.val_halves);
         };
-        if (c.off32) {
+        // 32-bit offsets span the wave's S slabs (off32 is per single slab)
+        if (c.off32 && (S == 1 || (int64_t)S * c.slab_max + 512 < ((int64_t)1 << 28))) {
             if (S == 1) go(csr_slabx_kernel<L, RP, UU, 1, true>);
             else if (S == 4) go(csr_slabx_kernel<L, RP, UU, 4, true>);
             else go(csr_slabx_kernel<L, RP, UU, 2, true>);
         } else {
-            go(csr_slabx_kernel<L, RP, UU, kCsrSlabsPerWave, false>);
+            if (S == 1) go(csr_slabx_kernel<L, RP, UU, 1, false>);
+            else if (S == 4) go(csr_slabx_kernel<L, RP, UU, 4, false>);
+            else go(csr_slabx_kernel<L, RP, UU, 2, false>);
         }
         return;
     }
@@ -616,6 +619,10 @@ static int launch_csr_rp(const spmv_plan_s *p, const double *x, double *y) {
 }
 
 int launch_csr(const spmv_plan_s *p, const double *x, double *y) {
+    if (p->nnz == 0) {  // no entries: y = 0 without touching x (x may be NULL when n == 0)
+        if (p->m) SPMV_HIP_TRY(hipMemsetAsync(y, 0, sizeof(double) * (size_t)p->m, p->stream));
+        return SPMV_SUCCESS;
+    }
     return p->csr.rp64 ? launch_csr_rp<int64_t>(p, x, y) : launch_csr_rp<int32_t>(p, x, y);
 }
 

@@ -147,3 +147,37 @@ def test_iterative_allgather_step_matches_single_process():
         p.join(timeout=240)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     assert q.get(timeout=10), "iterated sharded x differs from the single-process iteration"
+
+
+@pytest.mark.parametrize("parts", [2, 3, 8])
+@pytest.mark.parametrize("kind", ["powerlaw", "uniform"])
+def test_cabi_dist_shard_and_assemble(parts, kind):
+    """The C-ABI multi-GPU plan's host data movement (dist.cpp), without a
+    second GPU: spmv_dist_shard's rebased per-part CSRs are the nnz-balanced
+    cuts of spmv_partition_rows (uneven on the power-law matrix), and
+    spmv_dist_assemble reassembles y from the all-gathered padded slices --
+    each part's y computed by the oracle over its shard alone -- into the
+    oracle's y over the whole matrix, bit for bit."""
+    m = 20011
+    spec = sp.gen_spec(kind, m, per_row=9, max_len=3000, seed=12)
+    rp, col, val = sp.generate_csr(spec)
+    x = sp.generate_vector(m, seed=13)
+    yref = oracle.csr_spmv(rp, col, val, x)
+    cuts, slice_rows = sp.dist_layout(rp, parts)
+    assert np.array_equal(cuts, sp.partition_rows(rp, parts))
+    lens = np.diff(cuts)
+    assert slice_rows == max(1, int(lens.max()))
+    if kind == "powerlaw":
+        assert len(set(lens.tolist())) > 1  # uneven cuts exercise the padding
+    gathered = np.full(parts * slice_rows, np.nan)  # padding must never reach y
+    for k in range(parts):
+        srp, e0 = sp.dist_shard(rp, cuts, k)
+        assert e0 == rp[cuts[k]] and srp[0] == 0
+        assert np.array_equal(srp, rp[cuts[k]:cuts[k + 1] + 1] - rp[cuts[k]])
+        nk = int(srp[-1])
+        yk = oracle.csr_spmv(srp, col[e0:e0 + nk], val[e0:e0 + nk], x)
+        gathered[k * slice_rows:k * slice_rows + lens[k]] = yk
+    y = sp.dist_assemble(gathered, cuts, slice_rows)
+    assert np.array_equal(y, yref)
+    with pytest.raises(sp.SpmvError):
+        sp.dist_assemble(gathered, cuts, slice_rows - 1 if slice_rows > 1 else 0)

@@ -14,6 +14,7 @@ Tolerances (BASELINE north star: within 1e-6 relative fp64):
 """
 import ctypes as C
 import os
+import time
 
 import numpy as np
 import pytest
@@ -384,6 +385,22 @@ def test_rectangular_and_empty():
     assert (y == 0).all()
 
 
+def test_no_columns_with_null_device_x():
+    """m > 0, n = 0 (so nnz = 0): the API allows a NULL device x; every
+    format writes y = 0 without reading x (the CSR row-group
+    kernels read x unconditionally)."""
+    import torch
+    m = 1000
+    rp = np.zeros(m + 1, np.int64)
+    for fmt in ["csr", "ell", "ss", "hyb", "css", "coo", "jds", "bin", "dia", "auto"]:
+        plan = sp.Plan.from_csr(m, 0, rp, np.zeros(0, np.int32), np.zeros(0), fmt)
+        y = torch.full((m,), 5.0, dtype=torch.float64, device="cuda")
+        st = sp.lib().spmv_execute(plan._h, None, C.c_void_p(y.data_ptr()), sp.X_DEVICE | sp.Y_DEVICE)
+        assert st == 0, (fmt, sp.lib().spmv_last_error())
+        assert (y.cpu().numpy() == 0).all(), fmt
+        plan.destroy()
+
+
 def test_device_pointers_and_streams():
     import torch
     m = 100000
@@ -561,10 +578,19 @@ def _with_empty_rows(rp, col, val, frac, seed):
     return rp2, np.ascontiguousarray(col[keep]), np.ascontiguousarray(val[keep])
 
 
-def test_device_conversion_matches_host_build():
-    """spmv_plan_create_csr_device: CSR/SS converted on the GPU give the same
-    layout as the host builders -> bit-identical y; other formats stage."""
+def _device_csr(rp, col, val):
     import torch
+    return (torch.from_numpy(np.ascontiguousarray(rp, np.int64)).cuda(),
+            torch.from_numpy(np.ascontiguousarray(col, np.int32)).cuda(),
+            torch.from_numpy(np.ascontiguousarray(val, np.float64)).cuda())
+
+
+DEVICE_FORMATS = [("csr", {}), ("csr", {"csr_lanes": 1}), ("ss", {"ss_sigma": 4}), ("ss", {"ss_sigma": 16}),
+                  ("ss", {"ss_sigma": 32}), ("ss", {}), ("ell", {}), ("hyb", {}), ("hyb", {"ell_width": 4}),
+                  ("jds", {}), ("jds", {"ell_width": 8}), ("dia", {}), ("coo", {}), ("auto", {})]
+
+
+def _device_build_cases():
     cases = []
     rp, col, val = sp.generate_csr(sp.gen_spec("powerlaw", 30011, max_len=700, seed=5))
     cases.append(("powerlaw", 30011, 30011, rp, col, val))
@@ -576,23 +602,61 @@ def test_device_conversion_matches_host_build():
     cases.append(("rect", 7, 1000, np.array([0, 2, 2, 5, 5, 6, 9, 9], np.int64),
                   np.array([1, 999, 3, 4, 500, 0, 7, 8, 9], np.int32), np.arange(1.0, 10.0)))
     cases.append(("all-empty", 4, 4, np.zeros(5, np.int64), np.zeros(0, np.int32), np.zeros(0)))
-    for name, m, n, rp, col, val in cases:
+    rp, col, val = sp.generate_csr(sp.gen_spec("banded", 70001, band_lo=-9, band_hi=6, seed=7))
+    cases.append(("banded", 70001, 70001, rp, col, val))
+    cases.append(("banded+empty", 70001, 70001) + _with_empty_rows(rp, col, val, 0.1, 4))
+    # duplicates, unsorted columns and -0.0 values inside a band: the DIA
+    # slots add duplicates in entry order from +0.0 (the host build's
+    # val[at] += v), every other format keeps the entries as they are
+    rng = np.random.default_rng(11)
+    m = 5003
+    lens = rng.integers(0, 9, m)
+    rp = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    rows = np.repeat(np.arange(m), lens)
+    col = np.clip(rows + rng.integers(-3, 4, rows.size), 0, m - 1).astype(np.int32)
+    val = rng.random(rows.size) + 0.01
+    val[rng.random(rows.size) < 0.05] = -0.0
+    cases.append(("banded dup/unsorted/-0", m, m, rp, col, val))
+    return cases
+
+
+def test_device_conversion_matches_host_build():
+    """spmv_plan_create_csr_device: every format built on the GPU (CSR, SS,
+    ELL, HYB, JDS, DIA, COO, and AUTO resolved from device data) gives the
+    host builder's layout byte for byte (spmv_plan_digest, array by array)
+    and so the same y; a format the host refuses is refused on the device."""
+    for name, m, n, rp, col, val in _device_build_cases():
         x = sp.generate_vector(n, seed=9)
         yo = oracle_y(rp, col, val, x)
-        drp = torch.from_numpy(np.ascontiguousarray(rp, np.int64)).cuda()
-        dcol = torch.from_numpy(np.ascontiguousarray(col, np.int32)).cuda()
-        dval = torch.from_numpy(np.ascontiguousarray(val, np.float64)).cuda()
-        for fmt, kw in [("csr", {}), ("csr", {"csr_lanes": 1}), ("ss", {"ss_sigma": 4}),
-                        ("ss", {"ss_sigma": 16}), ("ss", {"ss_sigma": 32}), ("ss", {}), ("ell", {})]:
-            ph = sp.Plan.from_csr(m, n, rp, col, val, fmt, **kw)
+        drp, dcol, dval = _device_csr(rp, col, val)
+        for fmt, kw in DEVICE_FORMATS:
+            try:
+                ph = sp.Plan.from_csr(m, n, rp, col, val, fmt, **kw)
+            except sp.SpmvError as e:
+                assert "not supported" in str(e), (name, fmt, e)
+                with pytest.raises(sp.SpmvError, match="not supported"):
+                    sp.Plan.from_device_csr(m, n, drp, dcol, dval, fmt, **kw)
+                continue
             pd = sp.Plan.from_device_csr(m, n, drp, dcol, dval, fmt, **kw)
-            assert pd.info()["kernel"] == ph.info()["kernel"]
-            assert pd.info()["empty_rows"] == ph.info()["empty_rows"]
+            ih, idv = ph.info(), pd.info()
+            for k in ("format", "kernel", "empty_rows", "stored_slots", "algo_bytes", "n_kernels", "ell_width",
+                      "n_diags", "overflow_nnz", "csr_lanes", "ss_sigma"):
+                assert idv[k] == ih[k], f"{name} {fmt} {kw}: info {k} {idv[k]} != {ih[k]}"
+            if ih["format"] not in ("bin", "css"):
+                dh, dd = ph.digest(), pd.digest()
+                assert list(dd) == list(dh), (name, fmt, list(dd), list(dh))
+                bad = [a for a in dh if dh[a] != dd[a]]
+                assert not bad, f"{name} {fmt} {kw}: device layout differs in {bad}"
             yh = run_plan(ph, x, m)
             yd = run_plan(pd, x, m)
-            assert np.array_equal(yh, yd), f"{name} {fmt} {kw}: device build differs from host build"
+            if ih["format"] == "coo":
+                check_close(yd, yh, what=f"{name} coo")
+            else:
+                assert np.array_equal(yh, yd), f"{name} {fmt} {kw}: device build differs from host build"
             if m:
                 check_close(yd, yo, what=f"{name} {fmt} {kw}")
+            ph.destroy()
+            pd.destroy()
     # the device-side validation refuses what the host path refuses
     rp = np.array([0, 2, 3], np.int64)
     bad_col = torch.tensor([0, 5, 1], dtype=torch.int32, device="cuda")
@@ -1123,8 +1187,25 @@ def test_full_size_c4_banded():
     assert plan.info()["n_diags"] == 64
     plan.execute(xd, y)
     assert np.array_equal(y.cpu().numpy(), yo)
+    # the same DIA plan built on the device from the CSR in HBM (f2): byte-
+    # identical layout, bit-exact y, and AUTO resolves to DIA there too
+    dh = plan.digest()
     plan.destroy()
     del plan
+    drp, dcol, dval = _device_csr(rp, col, val)
+    for fmt in ("dia", "auto"):
+        t0 = time.perf_counter()
+        pd = sp.Plan.from_device_csr(m, m, drp, dcol, dval, fmt)
+        t_build = time.perf_counter() - t0
+        assert pd.info()["format"] == "dia"
+        assert pd.digest() == dh, f"device {fmt}: layout differs from the host build"
+        y.fill_(float("nan"))
+        pd.execute(xd, y)
+        assert np.array_equal(y.cpu().numpy(), yo)
+        print(f"c4 device {fmt} plan built in {t_build:.3f} s")
+        pd.destroy()
+    del drp, dcol, dval, pd
+    torch.cuda.empty_cache()
     plan = sp.Plan.from_csr(m, m, rp, col, val, "csr")
     plan.execute(xd, y)
     check_close(y.cpu().numpy(), yo, what="c4 csr")

@@ -16,6 +16,7 @@
 #   prof:<cfg>:<fmt>  the same for ONE format of config <cfg> (c2|c3|c4)
 #   rehearsal8        bench.py --gpus 8 at the config-5 shape, 8 gloo ranks on one GPU
 #   gloo2_c3          the self-launched 2-rank bench (gloo, one GPU) with --verify
+#   pt:<selection>    pytest -m gpu on the named tests only ("tests/x.py::test_a tests/y.py")
 #   py:<script args>  python3 -u <script args> (a tools/ probe), stdout to <step>.log
 #   exe:<binary args>  a stand-alone probe binary (bin/region_probe ...)
 #   probe:<script args> the same against the probe build (make probes:
@@ -66,6 +67,11 @@ for step in "$@"; do
     gloo2_c3)
       BENCH_DIST_BACKEND=gloo timeout -k 10 400 python3 -u bench.py --gpus 2 --config c3 --rows 500000 \
           --formats auto --no-cpu --only-config --verify > "$O/$tag.json" 2> "$O/$tag.err" ;;
+    pt:*)
+      # pt:<pytest selection>: named GPU tests only
+      # shellcheck disable=SC2086
+      timeout -k 10 900 python3 -u -m pytest ${step#pt:} -m gpu -x -v -s --timeout 600 --timeout-method thread \
+          > "$O/$tag.log" 2>&1 ;;
     py:*)
       # shellcheck disable=SC2086
       timeout -k 10 600 python3 -u ${step#py:} > "$O/$tag.log" 2> "$O/$tag.err" ;;
