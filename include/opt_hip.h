@@ -13,11 +13,25 @@
  * (crs|csr|ell|ss|dia|hyb|css|coo|jds|bin|auto, case-insensitive; anything
  * else means auto) overrides it at run time.
  *
+ * CRS keeps opt_crs's semantics, not its storage: every row is the
+ * sequential column-order sum bit for bit (src/opt_crs.cpp:57-69) on the
+ * fastest layout that sums so for the matrix (spmv_options_t.crs_exact: DIA
+ * for a band, BIN for a wide random x -- 3.6x the CSR kernels at config 2 --,
+ * sliced ELL for near-uniform short rows, else one-lane CSR).  The layout is
+ * in SpMatOpt.format (spmv_plan_info).  SPMV_HIP_CRS_EXACT=0 selects the CSR
+ * kernels themselves (row groups of lanes with butterfly sums: within 1e-12,
+ * not bit-exact).
+ *
  * x handling follows the reference: x_opt.val aliases the caller's x
  * (src/opt_crs.cpp:11-12) and SpMV uploads it on every call the way
  * opt_cusparse does (src/opt_cusparse.cpp:72).  SPMV_HIP_X_RESIDENT=1 uploads
  * x only on the first call (the reference driver never changes x,
- * src/main.cpp:36-102).  y is downloaded on every call (opt_cusparse.cpp:82).
+ * src/main.cpp:36-102).  y is downloaded on every call (opt_cusparse.cpp:82)
+ * unless SPMV_HIP_Y_RESIDENT=1: y then stays on the device (SPMV_Y_STAGED)
+ * and the caller fetches it with SpMVFetch before reading it -- a driver
+ * change (tools/spmv_main.cpp --device-y), since the reference main.cpp
+ * reads y after SpMV; at config 2 the 80 MB download per call is 1.5 ms of
+ * PCIe against a 0.8 ms kernel.
  *
  * Multi-GPU: SPMV_HIP_GPUS=N (set, N >= 1) makes OptimizeProblem build a dist plan
  * over devices 0..N-1 (spmv_dist_create_csr: nnz-balanced row ranges, one
@@ -58,6 +72,8 @@ extern "C" {
 void SpMV(const SpMatOpt &A, const VecOpt &x, Vec &y);
 /* (new) release the plan -- the reference never frees its SpMatOpt */
 void SpMVRelease(SpMatOpt &A);
+/* (new) SPMV_HIP_Y_RESIDENT=1: copy the y of the last SpMV to the host */
+void SpMVFetch(const SpMatOpt &A, Vec &y);
 }
 
 #endif /* OPT_HIP_H */

@@ -55,7 +55,9 @@ extern "C" {
  * fields, round 2) and spmv_plan_info_t: a caller built against a version-1
  * header passes structs of the wrong size and must be rebuilt.  Version 3
  * (round 3) took bin_product_order from spmv_options_t's reserved words (same
- * size) and appended bin_sum_entries to spmv_plan_info_t.  Callers may
+ * size) and appended bin_sum_entries to spmv_plan_info_t.  crs_exact (round
+ * 5) took one more reserved word: same size, and 0 (spmv_options_default)
+ * keeps the version-3 behaviour.  Callers may
  * check spmv_api_version() == SPMV_HIP_API_VERSION once at startup; the
  * structs are only ever filled by spmv_options_default / spmv_plan_info of a
  * library with the same version. */
@@ -117,7 +119,16 @@ typedef struct spmv_options {
                                 (every row bit-exact)                         */
     int32_t bin_product_order; /* BIN: where the Mul writes its products
                                 (SPMV_BIN_ORDER_*; 0 = auto)                   */
-    int32_t reserved[2];
+    int32_t crs_exact;       /* CSR requests: 1 = opt_crs semantics -- every row
+                                the sequential column-order sum bit for bit
+                                (src/opt_crs.cpp:57-69) on the fastest layout
+                                that sums so for this matrix: DIA (AUTO's banded
+                                rule), BIN with no run path (AUTO's wide-x rule),
+                                ELL (near-uniform rows, none > 64), else CSR with
+                                one lane per row; spmv_plan_info reports the
+                                layout.  0 = the CSR kernels as configured
+                                (row groups of L lanes: butterfly sums)       */
+    int32_t reserved[1];
 } spmv_options_t;
 
 /* Placement of the large buffers of a plan (the BIN product buffer, the DIA
@@ -257,9 +268,17 @@ int spmv_lds_order_probe(int32_t device, int32_t rounds, const int32_t *slot, co
 #define SPMV_ASYNC 0x4u    /* device x and y: return without synchronising    */
 #define SPMV_X_STAGED 0x8u /* re-use the host x uploaded by the previous call
                               (x may be NULL); error if none was staged       */
+#define SPMV_Y_STAGED 0x10u /* leave y in the plan's device staging buffer (y
+                              may be NULL; no D2H copy): spmv_fetch_y copies it
+                              to the host when the caller reads it -- the
+                              per-call 8m-byte download of opt_cusparse
+                              (src/opt_cusparse.cpp:82) leaves the timed loop */
 
 /* y = A * x.  x holds n doubles, y holds m doubles. */
 int spmv_execute(spmv_plan_t plan, const double *x, double *y, uint32_t flags);
+
+/* Copy the y of the last SPMV_Y_STAGED execute to host memory (m doubles). */
+int spmv_fetch_y(spmv_plan_t plan, double *y_host);
 
 /* y = alpha * A * x (the CSR5 handle's spmv(alpha, y),
  * CSR5_cuda/anonymouslib_cuda.h:262-284); alpha is applied to the finished
@@ -394,6 +413,10 @@ int spmv_dist_create_csr(int32_t n_devices, const int32_t *devices, int64_t m, i
  * other flag bit (SPMV_X_DEVICE, SPMV_Y_DEVICE, SPMV_ASYNC) is refused with
  * SPMV_ERROR_INVALID_VALUE. */
 int spmv_dist_execute(spmv_dist_t dist, const double *x, double *y, uint32_t flags);
+
+/* The full y of the last spmv_dist_execute (as assembled on the first
+ * device) to host memory (m doubles) -- after a call made with y = NULL. */
+int spmv_dist_fetch_y(spmv_dist_t dist, double *y_host);
 
 /* Per-step times over `iters` steps with the staged x: the local SpMV (max
  * over devices of the event time on each device's stream) and, separately,

@@ -39,7 +39,7 @@ OPT_LIB_PATH = os.path.join(HERE, "libopt_hip.so")
 
 FORMATS = {"auto": 0, "csr": 1, "crs": 1, "ell": 2, "ss": 3, "dia": 4, "hyb": 5, "css": 6, "coo": 7, "jds": 8, "bin": 9}
 FORMAT_NAMES = {0: "auto", 1: "csr", 2: "ell", 3: "ss", 4: "dia", 5: "hyb", 6: "css", 7: "coo", 8: "jds", 9: "bin"}
-X_DEVICE, Y_DEVICE, ASYNC, X_STAGED = 0x1, 0x2, 0x4, 0x8
+X_DEVICE, Y_DEVICE, ASYNC, X_STAGED, Y_STAGED = 0x1, 0x2, 0x4, 0x8, 0x10
 GEN_UNIFORM, GEN_POWERLAW, GEN_BANDED = 1, 2, 3
 API_VERSION = 3  # SPMV_HIP_API_VERSION of the structs mirrored here
 
@@ -59,7 +59,7 @@ class Options(C.Structure):
                 ("css_pace", C.c_int32), ("bin_strip_cols", C.c_int32), ("bin_groups", C.c_int32),
                 ("bin_sum_waves", C.c_int32), ("bin_pad", C.c_int32), ("csr_row_ptr64", C.c_int32),
                 ("placement", C.c_int32), ("bin_long_len", C.c_int32), ("bin_product_order", C.c_int32),
-                ("reserved", C.c_int32 * 2)]
+                ("crs_exact", C.c_int32), ("reserved", C.c_int32 * 1)]
 
 
 PLACEMENTS = {"auto": 0, "plain": 1, "search": 2, "vmm": 3}
@@ -107,6 +107,7 @@ EXPORTS = [
     "spmv_dist_execute", "spmv_dist_time", "spmv_dist_info", "spmv_dist_destroy", "spmv_stream_write_probe",
     "spmv_mixed_probe", "spmv_graph_create", "spmv_graph_launch", "spmv_graph_time", "spmv_graph_destroy",
     "spmv_plan_digest", "spmv_plan_digest_name", "spmv_dist_shard", "spmv_dist_assemble",
+    "spmv_fetch_y", "spmv_dist_fetch_y",
 ]
 
 _lib = None
@@ -140,6 +141,8 @@ def lib():
     L.spmv_plan_destroy.argtypes = [vp]
     L.spmv_execute.argtypes = [vp, vp, vp, C.c_uint32]
     L.spmv_execute_alpha.argtypes = [vp, f64, vp, vp, C.c_uint32]
+    L.spmv_fetch_y.argtypes = [vp, vp]
+    L.spmv_dist_fetch_y.argtypes = [vp, vp]
     L.spmv_plan_create_csr32_device.argtypes = [i32, i32, i32, vp, vp, vp, C.POINTER(Options), C.POINTER(vp)]
     L.spmv_set_stream.argtypes = [vp, vp]
     L.spmv_time.argtypes = [vp, vp, vp, i32, C.POINTER(f64)]
@@ -372,7 +375,7 @@ def make_options(fmt="auto", device: int = -1, csr_lanes: int = 0, ell_width: in
                  css_slab_shift: int = 0, css_lag: int = 0, css_pace: int = 0,
                  bin_strip_cols: int = 0, bin_groups: int = 0, bin_sum_waves: int = 0,
                  bin_pad: int = 0, csr_row_ptr64: bool = False, placement="auto",
-                 bin_long_len: int = 0, bin_product_order: int = 0) -> Options:
+                 bin_long_len: int = 0, bin_product_order: int = 0, crs_exact: bool = False) -> Options:
     o = Options()
     lib().spmv_options_default(C.byref(o))
     o.format = FORMATS[fmt] if isinstance(fmt, str) else int(fmt)
@@ -384,6 +387,7 @@ def make_options(fmt="auto", device: int = -1, csr_lanes: int = 0, ell_width: in
     o.placement = PLACEMENTS[placement] if isinstance(placement, str) else int(placement)
     o.bin_long_len = bin_long_len
     o.bin_product_order = bin_product_order
+    o.crs_exact = 1 if crs_exact else 0
     return o
 
 

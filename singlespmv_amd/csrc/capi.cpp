@@ -100,6 +100,7 @@ static int create_from_csr(const HostCsr &A, const spmv_options_t *opt_in, spmv_
     p->n = A.n;
     p->nnz = A.nnz;
     int fmt = o.format == SPMV_FORMAT_AUTO ? choose_format(A, o) : o.format;
+    if (fmt == SPMV_FORMAT_CSR && o.crs_exact) fmt = choose_crs_exact(A, o);
     stream_placement(p, fmt, o);
     int st;
     switch (fmt) {
@@ -234,7 +235,7 @@ int spmv_plan_create_csr_device(int64_t m, int64_t n, int64_t nnz, const int64_t
     // lengths drive AUTO and every slice / bin / overflow decision
     std::vector<int64_t> hrp;
     const bool need_rp = o.format == SPMV_FORMAT_AUTO || o.format == SPMV_FORMAT_ELL || o.format == SPMV_FORMAT_HYB ||
-                         o.format == SPMV_FORMAT_JDS;
+                         o.format == SPMV_FORMAT_JDS || (o.format == SPMV_FORMAT_CSR && o.crs_exact);
     if (need_rp) {
         hrp.resize((size_t)m + 1);
         const hipError_t e = hipMemcpy(hrp.data(), d_row_ptr, 8 * (size_t)(m + 1), hipMemcpyDeviceToHost);
@@ -250,6 +251,15 @@ int spmv_plan_create_csr_device(int64_t m, int64_t n, int64_t nnz, const int64_t
     if (fmt == SPMV_FORMAT_AUTO) {
         int census = SPMV_SUCCESS;
         fmt = choose_format_rp(m, n, nnz, hrp.data(), o, [&]() {
+            std::vector<int32_t> offs;
+            census = dia_offsets_device(p, A, 256, 1.25, offs);
+            return census == SPMV_SUCCESS;
+        });
+        if (census != SPMV_SUCCESS && census != kDiaRefused) st = census;
+    }
+    if (st == SPMV_SUCCESS && fmt == SPMV_FORMAT_CSR && o.crs_exact) {
+        int census = SPMV_SUCCESS;
+        fmt = choose_crs_exact(m, n, nnz, hrp.data(), o, [&]() {
             std::vector<int32_t> offs;
             census = dia_offsets_device(p, A, 256, 1.25, offs);
             return census == SPMV_SUCCESS;
@@ -387,7 +397,10 @@ int spmv_execute_alpha(spmv_plan_t p, double alpha, const double *x, double *y, 
 static int execute_impl(spmv_plan_t p, double alpha, const double *x, double *y, uint32_t flags) {
     SPMV_CHECK_ARG(p != nullptr, "plan is NULL");
     const bool staged = (flags & SPMV_X_STAGED) != 0;
-    SPMV_CHECK_ARG((x != nullptr || p->n == 0 || staged) && (y != nullptr || p->m == 0), "x or y is NULL");
+    const bool y_staged = (flags & SPMV_Y_STAGED) != 0;
+    SPMV_CHECK_ARG((x != nullptr || p->n == 0 || staged) && (y != nullptr || p->m == 0 || y_staged),
+                   "x or y is NULL");
+    SPMV_CHECK_ARG(!(y_staged && (flags & SPMV_Y_DEVICE)), "SPMV_Y_STAGED with SPMV_Y_DEVICE");
     SPMV_CHECK_ARG(!staged || p->x_stage != nullptr, "SPMV_X_STAGED without a previously staged x");
     SPMV_RETURN_IF(bind_device(p));
     const double *dx = x;
@@ -415,13 +428,25 @@ static int execute_impl(spmv_plan_t p, double alpha, const double *x, double *y,
     }
     SPMV_RETURN_IF(dispatch(p, dx, dy));
     SPMV_RETURN_IF(launch_scale(p, dy, alpha));
-    if (!(flags & SPMV_Y_DEVICE)) {
+    if (y_staged) {
+        p->y_staged = true;
+        if (!(flags & SPMV_ASYNC) || !(flags & SPMV_X_DEVICE)) SPMV_HIP_TRY(hipStreamSynchronize(p->stream));
+    } else if (!(flags & SPMV_Y_DEVICE)) {
         // opt_cusparse.cpp:82 -- D2H copy of y on every call
         if (p->m) SPMV_HIP_TRY(hipMemcpyAsync(y, dy, sizeof(double) * p->m, hipMemcpyDeviceToHost, p->stream));
         SPMV_HIP_TRY(hipStreamSynchronize(p->stream));
     } else if (!(flags & SPMV_ASYNC) || !(flags & SPMV_X_DEVICE)) {
         SPMV_HIP_TRY(hipStreamSynchronize(p->stream));
     }
+    return SPMV_SUCCESS;
+}
+
+int spmv_fetch_y(spmv_plan_t p, double *y) {
+    SPMV_CHECK_ARG(p != nullptr && (y != nullptr || p->m == 0), "plan or y is NULL");
+    SPMV_CHECK_ARG(p->y_staged && p->y_stage, "spmv_fetch_y without a previous SPMV_Y_STAGED execute");
+    SPMV_RETURN_IF(bind_device(p));
+    if (p->m) SPMV_HIP_TRY(hipMemcpyAsync(y, p->y_stage, sizeof(double) * p->m, hipMemcpyDeviceToHost, p->stream));
+    SPMV_HIP_TRY(hipStreamSynchronize(p->stream));
     return SPMV_SUCCESS;
 }
 

@@ -298,6 +298,17 @@ int spmv_dist_execute(spmv_dist_t d, const double *x, double *y, uint32_t flags)
     return dist_sync(d);
 }
 
+int spmv_dist_fetch_y(spmv_dist_t d, double *y) {
+    SPMV_CHECK_ARG(d != nullptr && (y != nullptr || d->m == 0), "dist plan or y is NULL");
+    SPMV_CHECK_ARG(d->x_staged, "spmv_dist_fetch_y before any spmv_dist_execute");
+    SPMV_HIP_TRY(hipSetDevice(d->devs[0]));
+    const double *full = d->d_yfull[0];
+    for (const SliceCopy &c : dist_copies(d->cuts.data(), d->nd, d->slice))
+        SPMV_HIP_TRY(hipMemcpyAsync(y + c.dst, full + c.src, 8 * (size_t)c.rows, hipMemcpyDeviceToHost, d->streams[0]));
+    SPMV_HIP_TRY(hipStreamSynchronize(d->streams[0]));
+    return SPMV_SUCCESS;
+}
+
 int spmv_dist_time(spmv_dist_t d, int32_t iters, double *spmv_ms, double *gather_ms) {
     SPMV_CHECK_ARG(d != nullptr && iters > 0 && spmv_ms && gather_ms, "bad arguments");
     SPMV_CHECK_ARG(d->x_staged, "spmv_dist_time needs an x broadcast by spmv_dist_execute first");

@@ -1205,6 +1205,35 @@ int choose_format(const HostCsr &A, const spmv_options_t &o) {
     });
 }
 
+int choose_crs_exact(const HostCsr &A, spmv_options_t &o) {
+    return choose_crs_exact(A.m, A.n, A.nnz, A.row_ptr, o, [&]() {
+        std::vector<int32_t> offs;
+        return dia_offsets(A, 256, 1.25, offs);
+    });
+}
+
+// opt_crs semantics for a CSR request (spmv_options_t.crs_exact): the
+// fastest layout whose every row is the sequential column-order sum, bit for
+// bit -- DIA where AUTO finds a band, BIN (no run path) where AUTO's wide-x
+// rule holds, sliced ELL for near-uniform rows of <= 64 entries, else CSR
+// with one lane per row.  `o` is rewritten for the chosen layout.
+int choose_crs_exact(int64_t m, int64_t n, int64_t nnz, const int64_t *row_ptr, spmv_options_t &o,
+                     const std::function<bool()> &dia_ok) {
+    const int f = choose_format_rp(m, n, nnz, row_ptr, o, dia_ok);
+    if (f == SPMV_FORMAT_DIA) return f;
+    if (f == SPMV_FORMAT_BIN) {
+        o.bin_long_len = -1;  // every row on the segment path: sequential sums
+        return f;
+    }
+    int64_t maxlen = 0;
+#pragma omp parallel for schedule(static) reduction(max : maxlen)
+    for (int64_t r = 0; r < m; ++r) maxlen = std::max<int64_t>(maxlen, row_ptr[r + 1] - row_ptr[r]);
+    const double mean = m ? (double)nnz / (double)m : 0.0;
+    if (m > 0 && maxlen <= 64 && (double)maxlen <= 2.0 * mean + 8.0) return SPMV_FORMAT_ELL;
+    o.csr_lanes = 1;
+    return SPMV_FORMAT_CSR;
+}
+
 // AUTO from the row-length histogram (row pointers only) plus, for short
 // rows, the diagonal census `dia_ok` (host: dia_offsets; a device CSR:
 // dia_offsets_device) -- the same decision for a host and a device CSR.

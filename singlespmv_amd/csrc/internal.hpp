@@ -397,6 +397,7 @@ struct spmv_plan_s {
     spmv::BinDev bin;
     double *x_stage = nullptr;  // host-x staging (opt_cusparse.cpp:44-45)
     double *y_stage = nullptr;
+    bool y_staged = false;      // y_stage holds the y of an SPMV_Y_STAGED execute
     int64_t stored_slots = 0;
     int64_t empty_rows = 0;
     int64_t algo_bytes = 0;
@@ -454,6 +455,10 @@ int build_ss_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, c
                     const spmv_options_t &o, double mean_row);
 int choose_format(const HostCsr &A, const spmv_options_t &o);
 int choose_format_rp(int64_t m, int64_t n, int64_t nnz, const int64_t *row_ptr, const spmv_options_t &o,
+                     const std::function<bool()> &dia_ok);
+// spmv_options_t.crs_exact: the layout for a CSR request with opt_crs semantics
+int choose_crs_exact(const HostCsr &A, spmv_options_t &o);
+int choose_crs_exact(int64_t m, int64_t n, int64_t nnz, const int64_t *row_ptr, spmv_options_t &o,
                      const std::function<bool()> &dia_ok);
 // layout decisions that need the row pointers only (host and device builders)
 int ell_slice_offsets(const int64_t *row_ptr, int64_t m, int cap, const int32_t *order, std::vector<int64_t> &off);

@@ -67,6 +67,14 @@ void OptimizeProblem(const SpMat &A, const Vec &x, SpMatOpt &A_opt, VecOpt &x_op
     // BIN keeps long power-law rows off its run path (spmv_hip.h bin_long_len)
     if (const char *ex = std::getenv("SPMV_HIP_EXACT"))
         if (std::atoi(ex) != 0) o.bin_long_len = -1;
+    // CRS is the opt_crs plugin: its semantics (each row's sequential sum,
+    // src/opt_crs.cpp:57-69) on the fastest layout that keeps them
+    // (spmv_options_t.crs_exact); SPMV_HIP_CRS_EXACT=0 asks for the CSR
+    // kernels themselves (row groups of lanes, butterfly sums)
+    if (o.format == SPMV_FORMAT_CSR) {
+        const char *ce = std::getenv("SPMV_HIP_CRS_EXACT");
+        o.crs_exact = (ce && *ce && std::atoi(ce) == 0) ? 0 : 1;
+    }
     A_opt.nRow = A.nRow;
     A_opt.nCol = A.nCol;
     A_opt.nNnz = A.nNnz;
@@ -107,29 +115,35 @@ void OptimizeProblem(const SpMat &A, const Vec &x, SpMatOpt &A_opt, VecOpt &x_op
 
 extern "C" {
 
+static bool env_flag(const char *name) {
+    const char *e = std::getenv(name);
+    return e && *e == '1';
+}
+
 void SpMV(const SpMatOpt &A, const VecOpt &x, Vec &y) {
-    static int resident = -1;
+    static int resident = -1, y_resident = -1;
     if (resident < 0) {
-        const char *e = std::getenv("SPMV_HIP_X_RESIDENT");
-        resident = (e && *e == '1') ? 1 : 0;
+        resident = env_flag("SPMV_HIP_X_RESIDENT") ? 1 : 0;
+        y_resident = env_flag("SPMV_HIP_Y_RESIDENT") ? 1 : 0;
     }
     SpMatOpt &a = const_cast<SpMatOpt &>(A);  // the reference passes const& too
+    const bool staged_x = resident && a.x_uploaded;
     int st;
     if (a.dist) {  // SPMV_HIP_GPUS: H2D x, RCCL broadcast, local SpMVs, RCCL all-gather, D2H y
-        st = spmv_dist_execute(a.dist, (resident && a.x_uploaded) ? nullptr : x.val, y.val,
-                               (resident && a.x_uploaded) ? SPMV_X_STAGED : 0u);
-        a.x_uploaded = 1;
-    } else if (!resident) {
-        st = spmv_execute(a.plan, x.val, y.val, 0u);  // H2D x, kernels, D2H y
+        st = spmv_dist_execute(a.dist, staged_x ? nullptr : x.val, y_resident ? nullptr : y.val,
+                               staged_x ? SPMV_X_STAGED : 0u);
     } else {
-        if (!a.x_uploaded) {
-            st = spmv_execute(a.plan, x.val, y.val, 0u);
-            a.x_uploaded = 1;
-        } else {
-            st = spmv_execute(a.plan, nullptr, y.val, SPMV_X_STAGED);
-        }
+        // H2D x (or the staged copy), kernels, D2H y (or y left staged)
+        st = spmv_execute(a.plan, staged_x ? nullptr : x.val, y_resident ? nullptr : y.val,
+                          (staged_x ? SPMV_X_STAGED : 0u) | (y_resident ? SPMV_Y_STAGED : 0u));
     }
+    a.x_uploaded = 1;
     if (st != SPMV_SUCCESS) opt_hip_die("SpMV", st);
+}
+
+void SpMVFetch(const SpMatOpt &A, Vec &y) {
+    const int st = A.dist ? spmv_dist_fetch_y(A.dist, y.val) : spmv_fetch_y(A.plan, y.val);
+    if (st != SPMV_SUCCESS) opt_hip_die("SpMVFetch", st);
 }
 
 void SpMVRelease(SpMatOpt &A) {

@@ -488,6 +488,76 @@ def test_dropin_optimizeproblem_spmv(fmt, gpus, monkeypatch):
     L.SpMVRelease(C.byref(Ao))
 
 
+class _SpMatC(C.Structure):
+    _fields_ = [("nRow", C.c_int), ("nCol", C.c_int), ("nNnz", C.c_int),
+                ("row_idx", C.c_void_p), ("col_idx", C.c_void_p), ("val", C.c_void_p)]
+
+
+class _VecC(C.Structure):
+    _fields_ = [("size", C.c_int), ("val", C.c_void_p)]
+
+
+class _SpMatOptC(C.Structure):
+    _fields_ = [("nRow", C.c_int), ("nCol", C.c_int), ("nNnz", C.c_int), ("plan", C.c_void_p),
+                ("format", C.c_int), ("d_x", C.c_void_p), ("x_uploaded", C.c_int), ("dist", C.c_void_p),
+                ("n_gpus", C.c_int)]
+
+
+def _dropin_y(row, col, val, x, m, n, calls=2, fetch=False):
+    """OptimizeProblem + `calls` SpMV through libopt_hip.so (the drop-in);
+    fetch: SpMVFetch after each call (SPMV_HIP_Y_RESIDENT=1).  Returns (y,
+    the resolved layout)."""
+    sp.lib()
+    L = C.CDLL(sp.OPT_LIB_PATH)
+    opt = getattr(L, "_Z15OptimizeProblemRK5SpMatRK3VecR8SpMatOptR6VecOpt")
+    fetch_fn = getattr(L, "_Z9SpMVFetchRK8SpMatOptR3Vec", None) or getattr(L, "SpMVFetch")
+    row, col, val, x = (np.ascontiguousarray(a) for a in (row, col, val, x))
+    A = _SpMatC(m, n, len(val), row.ctypes.data, col.ctypes.data, val.ctypes.data)
+    xv = _VecC(n, x.ctypes.data)
+    y = np.full(m, 99.0)
+    yv = _VecC(m, y.ctypes.data)
+    Ao, xo = _SpMatOptC(), _VecC()
+    opt(C.byref(A), C.byref(xv), C.byref(Ao), C.byref(xo))
+    for _ in range(calls):
+        y.fill(99.0)
+        L.SpMV(C.byref(Ao), C.byref(xo), C.byref(yv))
+        if fetch:
+            fetch_fn(C.byref(Ao), C.byref(yv))
+    fmt = sp.FORMAT_NAMES[Ao.format]
+    L.SpMVRelease(C.byref(Ao))
+    return y, fmt
+
+
+@pytest.mark.parametrize("fetch", [False, True])
+def test_dropin_crs_is_opt_crs_bit_for_bit(fetch, monkeypatch):
+    """The drop-in's CRS (-DOPT_HIP_CRS / SPMV_HIP_FORMAT=crs) keeps opt_crs's
+    semantics on the fastest layout that does so (spmv_options_t.crs_exact):
+    y is the reference opt_crs y bit for bit on every golden fixture, and a
+    config-2-like matrix (1 M x 1 M, 16 per row: x beyond L2) gets the BIN
+    layout, bit-exact against the oracle.  With SPMV_HIP_Y_RESIDENT=1 y stays
+    on the device until SpMVFetch."""
+    monkeypatch.setenv("SPMV_HIP_FORMAT", "crs")
+    if fetch:
+        monkeypatch.setenv("SPMV_HIP_Y_RESIDENT", "1")
+    for name in golden_names():
+        g = load_golden(name)
+        m, n = int(g["m"]), int(g["n"])
+        y, fmt = _dropin_y(g["row"], g["col"], g["val"], g["x"], m, n, fetch=fetch)
+        assert np.array_equal(y, g["y_crs"]), f"{name}: drop-in CRS ({fmt}) differs from opt_crs"
+    m = 1_000_000
+    rp, col, val = sp.generate_csr(sp.gen_spec("uniform", m, per_row=16, seed=31))
+    x = sp.generate_vector(m, seed=32)
+    row = np.repeat(np.arange(m, dtype=np.int32), np.diff(rp))
+    y, fmt = _dropin_y(row, col, val, x, m, m, fetch=fetch)
+    assert fmt == "bin"
+    assert np.array_equal(y, oracle_y(rp, col, val, x))
+    # SPMV_HIP_CRS_EXACT=0: the CSR kernels themselves (butterfly sums)
+    monkeypatch.setenv("SPMV_HIP_CRS_EXACT", "0")
+    y, fmt = _dropin_y(row, col, val, x, m, m, fetch=fetch)
+    assert fmt == "csr"
+    check_close(y, oracle_y(rp, col, val, x))
+
+
 @pytest.mark.parametrize("exact", ["", "1"])
 def test_dropin_exact_switch(exact, monkeypatch):
     """SPMV_HIP_EXACT=1 keeps the drop-in's BIN plan off the run path: a
