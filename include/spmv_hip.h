@@ -123,7 +123,8 @@ typedef struct spmv_options {
                                 the sequential column-order sum bit for bit
                                 (src/opt_crs.cpp:57-69) on the fastest layout
                                 that sums so for this matrix: DIA (AUTO's banded
-                                rule), BIN with no run path (AUTO's wide-x rule),
+                                rule, rows strictly ascending: no duplicates),
+                                BIN with no run path (AUTO's wide-x rule),
                                 ELL (near-uniform rows, none > 64), else CSR with
                                 one lane per row; spmv_plan_info reports the
                                 layout.  0 = the CSR kernels as configured

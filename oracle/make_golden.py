@@ -137,5 +137,37 @@ def main():
          ["crs", "ss_opt"])
 
 
+def make_dups():
+    """mtx_dups: a Matrix Market file whose (row, col) keys repeat in runs
+    far longer than std::sort's 16-element insertion-sort threshold, entries
+    in shuffled file order -- the reference loader's std::sort (not stable,
+    src/util.cpp:51) leaves equal keys in an order of its own, which this
+    fixture pins (the COO is the REFERENCE loader's, via oracle/_ref)."""
+    rng = np.random.default_rng(20261018)
+    # n above the longest row: opt_ell pads with column = slot index
+    # (src/opt_ell.cpp:46-52), which must stay inside x
+    m, n = 90, 400
+    keys = [(r, c) for r in range(m) for c in rng.choice(n, size=rng.integers(0, 6), replace=False)]
+    ents = []
+    for (r, c) in keys:
+        reps = int(rng.choice([1, 1, 2, 3, 17, 40, 75]))
+        ents += [(r, c, float(1.0 - rng.random())) for _ in range(reps)]
+    order = rng.permutation(len(ents))
+    path = os.path.join(OUT, "mtx", "dups.mtx")
+    with open(path, "w") as f:
+        f.write("%%MatrixMarket matrix coordinate real general\n% duplicate-key runs\n")
+        f.write(f"{m} {n} {len(ents)}\n")
+        for i in order:
+            r, c, v = ents[i]
+            f.write(f"{r + 1} {c + 1} {v!r}\n")
+    m2, n2, row, col, val = oracle.ref_load_mtx(path)
+    x, y0 = oracle.ref_rand_vectors(n2, m2, seed=3)
+    save("mtx_dups", m2, n2, row, col, val, x, y0, ["crs", "ell", "ss_simple", "ss_opt"])
+
+
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["dups"]:
+        make_dups()
+    else:
+        main()
+        make_dups()

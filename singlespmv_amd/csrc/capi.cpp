@@ -259,11 +259,19 @@ int spmv_plan_create_csr_device(int64_t m, int64_t n, int64_t nnz, const int64_t
     }
     if (st == SPMV_SUCCESS && fmt == SPMV_FORMAT_CSR && o.crs_exact) {
         int census = SPMV_SUCCESS;
-        fmt = choose_crs_exact(m, n, nnz, hrp.data(), o, [&]() {
-            std::vector<int32_t> offs;
-            census = dia_offsets_device(p, A, 256, 1.25, offs);
-            return census == SPMV_SUCCESS;
-        });
+        fmt = choose_crs_exact(
+            m, n, nnz, hrp.data(), o,
+            [&]() {
+                std::vector<int32_t> offs;
+                census = dia_offsets_device(p, A, 256, 1.25, offs);
+                return census == SPMV_SUCCESS;
+            },
+            [&]() {
+                bool strict = false;
+                const int s2 = rows_strict_device(p, A, &strict);
+                if (s2 != SPMV_SUCCESS) census = s2;
+                return strict;
+            });
         if (census != SPMV_SUCCESS && census != kDiaRefused) st = census;
     }
     const double mean = m ? (double)nnz / (double)m : 0.0;

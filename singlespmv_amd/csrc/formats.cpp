@@ -1206,10 +1206,19 @@ int choose_format(const HostCsr &A, const spmv_options_t &o) {
 }
 
 int choose_crs_exact(const HostCsr &A, spmv_options_t &o) {
-    return choose_crs_exact(A.m, A.n, A.nnz, A.row_ptr, o, [&]() {
-        std::vector<int32_t> offs;
-        return dia_offsets(A, 256, 1.25, offs);
-    });
+    return choose_crs_exact(
+        A.m, A.n, A.nnz, A.row_ptr, o,
+        [&]() {
+            std::vector<int32_t> offs;
+            return dia_offsets(A, 256, 1.25, offs);
+        },
+        [&]() {
+            int64_t bad = 0;
+#pragma omp parallel for schedule(static) reduction(+ : bad)
+            for (int64_t r = 0; r < A.m; ++r)
+                for (int64_t j = A.row_ptr[r] + 1; j < A.row_ptr[r + 1]; ++j) bad += A.col[j] <= A.col[j - 1];
+            return bad == 0;
+        });
 }
 
 // opt_crs semantics for a CSR request (spmv_options_t.crs_exact): the
@@ -1218,9 +1227,11 @@ int choose_crs_exact(const HostCsr &A, spmv_options_t &o) {
 // rule holds, sliced ELL for near-uniform rows of <= 64 entries, else CSR
 // with one lane per row.  `o` is rewritten for the chosen layout.
 int choose_crs_exact(int64_t m, int64_t n, int64_t nnz, const int64_t *row_ptr, spmv_options_t &o,
-                     const std::function<bool()> &dia_ok) {
+                     const std::function<bool()> &dia_ok, const std::function<bool()> &rows_strict) {
     const int f = choose_format_rp(m, n, nnz, row_ptr, o, dia_ok);
-    if (f == SPMV_FORMAT_DIA) return f;
+    // DIA adds duplicate entries into one slot before the product: bit-exact
+    // only when every row's columns are strictly ascending
+    if (f == SPMV_FORMAT_DIA && rows_strict()) return f;
     if (f == SPMV_FORMAT_BIN) {
         o.bin_long_len = -1;  // every row on the segment path: sequential sums
         return f;

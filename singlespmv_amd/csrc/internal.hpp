@@ -459,7 +459,7 @@ int choose_format_rp(int64_t m, int64_t n, int64_t nnz, const int64_t *row_ptr, 
 // spmv_options_t.crs_exact: the layout for a CSR request with opt_crs semantics
 int choose_crs_exact(const HostCsr &A, spmv_options_t &o);
 int choose_crs_exact(int64_t m, int64_t n, int64_t nnz, const int64_t *row_ptr, spmv_options_t &o,
-                     const std::function<bool()> &dia_ok);
+                     const std::function<bool()> &dia_ok, const std::function<bool()> &rows_strict);
 // layout decisions that need the row pointers only (host and device builders)
 int ell_slice_offsets(const int64_t *row_ptr, int64_t m, int cap, const int32_t *order, std::vector<int64_t> &off);
 void ell_finish_info(spmv_plan_s *p, int maxw, int64_t total);
@@ -485,6 +485,8 @@ struct DevCsr {
 constexpr int kDiaRefused = -1001;  // dia_offsets_device: too many diagonals / too much fill
 int dia_offsets_device(spmv_plan_s *p, const DevCsr &A, int max_diags, double max_fill, std::vector<int32_t> &offs);
 int build_dia_device(spmv_plan_s *p, const DevCsr &A, const spmv_options_t &o);
+// every row's columns strictly ascending (no duplicates, no disorder)?
+int rows_strict_device(spmv_plan_s *p, const DevCsr &A, bool *strict);
 int build_ell_device(spmv_plan_s *p, const DevCsr &A, const spmv_options_t &o);
 int build_hyb_device(spmv_plan_s *p, const DevCsr &A, const spmv_options_t &o);
 int build_jds_device(spmv_plan_s *p, const DevCsr &A, const spmv_options_t &o);

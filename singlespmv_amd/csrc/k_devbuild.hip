@@ -193,6 +193,18 @@ __global__ __launch_bounds__(256) void overflow_copy_kernel(const int64_t *__res
     }
 }
 
+// rows whose columns are not strictly ascending (duplicates or disorder)
+__global__ __launch_bounds__(256) void rows_strict_kernel(const int64_t *__restrict__ rp,
+                                                          const int32_t *__restrict__ col, int64_t m,
+                                                          unsigned long long *__restrict__ bad) {
+    unsigned long long b = 0;
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < m; r += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t e = rp[r + 1];
+        for (int64_t j = rp[r] + 1; j < e; ++j) b += col[j] <= col[j - 1];
+    }
+    if (b) atomicAdd(bad, b);
+}
+
 // ---- COO row ids -------------------------------------------------------------------
 __global__ __launch_bounds__(256) void coo_rows_kernel(const int64_t *__restrict__ rp, int64_t m,
                                                        int32_t *__restrict__ row) {
@@ -311,6 +323,22 @@ int dia_offsets_device(spmv_plan_s *p, const DevCsr &A, int max_diags, double ma
     if (n_occ) SPMV_HIP_TRY(hipMemcpy(offs.data(), out, sizeof(int32_t) * (size_t)n_occ, hipMemcpyDeviceToHost));
     std::sort(offs.begin(), offs.end());
     if ((double)offs.size() * (double)A.m > max_fill * (double)std::max<int64_t>(A.nnz, 1)) return kDiaRefused;
+    return SPMV_SUCCESS;
+}
+
+int rows_strict_device(spmv_plan_s *p, const DevCsr &A, bool *strict) {
+    *strict = true;
+    if (A.m == 0 || A.nnz == 0) return SPMV_SUCCESS;
+    Scratch scratch{p->stream, {}};
+    unsigned long long *bad = nullptr, hb = 0;
+    SPMV_HIP_TRY(hipMalloc(&bad, sizeof(unsigned long long)));
+    scratch.v.push_back(bad);
+    SPMV_HIP_TRY(hipMemsetAsync(bad, 0, sizeof(hb), p->stream));
+    hipLaunchKernelGGL(rows_strict_kernel, dim3(grid_for(A.m)), dim3(256), 0, p->stream, A.d_rp, A.d_col, A.m, bad);
+    SPMV_HIP_TRY(hipGetLastError());
+    SPMV_HIP_TRY(hipMemcpyAsync(&hb, bad, sizeof(hb), hipMemcpyDeviceToHost, p->stream));
+    SPMV_HIP_TRY(hipStreamSynchronize(p->stream));
+    *strict = hb == 0;
     return SPMV_SUCCESS;
 }
 

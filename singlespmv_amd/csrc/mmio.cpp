@@ -283,6 +283,33 @@ int spmv_load_mtx(const char *path, int32_t *m, int32_t *n, int32_t *nnz, int32_
         }
     }
     sort_rows(rp.data(), M, ci, vv);
+    // Equal (row, col) keys: the reference's std::sort (src/util.cpp:51) is
+    // not stable, so duplicates leave it in an order of its own.  The file
+    // order and the comparator (src/util.h:35-38) fix that order for a given
+    // libstdc++; when duplicates exist, the whole list is re-sorted exactly as
+    // the reference does (one thread), so their summation order matches too.
+    bool dups = false;
+#pragma omp parallel for schedule(static) reduction(|| : dups)
+    for (long long r = 0; r < M; ++r)
+        for (int64_t j = rp[(size_t)r] + 1; j < rp[(size_t)r + 1]; ++j) dups = dups || ci[j] == ci[j - 1];
+    if (dups) {
+        struct Element {  // the reference's triplet and operator< (src/util.h:30-39)
+            int row, col;
+            double val;
+            bool operator<(const Element &e) const {
+                if (row == e.row) return col < e.col;
+                return row < e.row;
+            }
+        };
+        std::vector<Element> el((size_t)L);
+        for (long long i = 0; i < L; ++i) el[(size_t)i] = Element{tr[(size_t)i], tc[(size_t)i], tv[(size_t)i]};
+        std::sort(el.begin(), el.end());
+        for (long long i = 0; i < L; ++i) {
+            ri[i] = el[(size_t)i].row;
+            ci[i] = el[(size_t)i].col;
+            vv[i] = el[(size_t)i].val;
+        }
+    }
     *m = (int32_t)M;
     *n = (int32_t)N;
     *nnz = (int32_t)L;
