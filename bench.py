@@ -60,7 +60,10 @@ CONFIGS = {
     "c4": (dict(kind="banded", band_lo=-32, band_hi=31), "banded 20M rows, 64 diagonals", 20_000_000),
 }
 # the configs the N = 1 line carries beside the headline: (config, formats)
-EXTRA_CONFIGS = (("c3", ["auto", "hyb", "csr", "ss"]), ("c4", ["auto", "csr", "ell"]))
+EXTRA_CONFIGS = (("c3", ["auto", "hyb", "csr", "ss"]), ("c4", ["auto", "csr", "ell", "ss", "jds"]))
+# plans built so far in this process: a late plan can land in slower memory
+# (include/spmv_hip.h, placement), so every format result records its ordinal
+PLAN_ORDINAL = [0]
 KFD_TOPOLOGY = "/sys/class/kfd/kfd/topology/nodes"
 
 
@@ -355,6 +358,7 @@ def time_formats(ctx, args, M, fmts, trials_head: int, y_check=None, setup_mark=
                 plan.destroy()
             continue
         t_plan = time.time() - tp
+        PLAN_ORDINAL[0] += 1
         info = plan.info()
         progress(f"{M['config']}: {fmt} plan ({info['kernel']}) built in {t_plan:.1f} s")
         stream = torch.cuda.Stream(device=ctx.dev)
@@ -396,6 +400,10 @@ def time_formats(ctx, args, M, fmts, trials_head: int, y_check=None, setup_mark=
             "algo_bytes": algo, "format_bytes": info["algo_bytes"], "stored_slots": info["stored_slots"],
             "device_bytes": info["device_bytes"], "plan_build_s": round(t_plan, 3),
             "n_kernels": info["n_kernels"], "placement": info["placement"],
+            "plan_ordinal": PLAN_ORDINAL[0],
+            "placement_info": {"mode": info["placement"], "candidates": info["placement_candidates"],
+                               "best_ms": round(info["placement_best_ms"], 5),
+                               "worst_ms": round(info["placement_worst_ms"], 5)},
         }
         for k in RELEVANT.get(info["format"], ()):
             r[k] = info[k]
@@ -416,6 +424,38 @@ def time_formats(ctx, args, M, fmts, trials_head: int, y_check=None, setup_mark=
             plan.destroy()
         torch.cuda.synchronize()
     return results, headline, y_head
+
+
+def device_build_record(ctx, M, host_plan, y_host, host_build_s) -> dict:
+    """The same AUTO plan built on the GPU from the CSR already in HBM
+    (spmv_plan_create_csr_device): its build time (the CSR
+    upload excluded), whether its layout is byte-identical to the host
+    build's (spmv_plan_digest) and its y to the host plan's."""
+    import singlespmv_amd as sp
+    torch = ctx.torch
+    drp = torch.from_numpy(M["rp"]).to(ctx.dev)
+    dcol = torch.from_numpy(M["col"]).to(ctx.dev)
+    dval = torch.from_numpy(M["val"]).to(ctx.dev)
+    torch.cuda.synchronize()
+    tp = time.time()
+    pd = sp.Plan.from_device_csr(M["rows"], M["n"], drp, dcol, dval, "auto", device=ctx.local)
+    t_dev = time.time() - tp
+    PLAN_ORDINAL[0] += 1
+    info = pd.info()
+    rec = {"format": info["format"], "kernel": info["kernel"], "plan_build_s": round(t_dev, 4),
+           "host_plan_build_s": host_build_s, "plan_ordinal": PLAN_ORDINAL[0]}
+    try:
+        rec["layout_identical_to_host_build"] = pd.digest() == host_plan.digest()
+    except sp.SpmvError as e:
+        rec["layout_identical_to_host_build"] = str(e)
+    y = torch.empty(M["rows"], dtype=torch.float64, device=ctx.dev)
+    pd.execute(M["x"], y)
+    rec["y_identical_to_host_plan"] = bool(torch.equal(y, y_host))
+    pd.destroy()
+    del drp, dcol, dval, y
+    torch.cuda.empty_cache()
+    progress(f"{M['config']}: device-built {info['format']} plan in {t_dev:.3f} s")
+    return rec
 
 
 def roofline_of(config: str, M, r) -> dict:
@@ -457,6 +497,9 @@ def extra_config(ctx, args, config: str, fmts, stream_gbs: float) -> dict:
     if head is None:
         return {"error": "no plan could be built", "details": results}
     plan, info, r = head
+    device_build = None
+    if config == "c4":
+        device_build = device_build_record(ctx, M, plan, y_head, results[fmts[0]].get("plan_build_s"))
     plan.destroy()
     max_rel = r["max_rel_err_vs_cpu"]
     for fr in results.values():
@@ -472,6 +515,8 @@ def extra_config(ctx, args, config: str, fmts, stream_gbs: float) -> dict:
            "cpu_check": {"kind": "port", "ms_one_call": t_cpu * 1e3,
                          "note": "oracle opt_crs restatement (src/opt_crs.cpp:44-70), all host threads, one call"},
            "gen_s": round(M["gen_s"], 2), "formats": results}
+    if device_build is not None:
+        out["device_build"] = device_build
     if "csr" in results and "event_ms_per_launch" in results["csr"] and r["format"] != "csr":
         out[f"{r['format']}_vs_csr"] = results["csr"]["event_ms_per_launch"] / r["event_ms_per_launch"]
     del M, y_head

@@ -121,11 +121,9 @@ static bool env_flag(const char *name) {
 }
 
 void SpMV(const SpMatOpt &A, const VecOpt &x, Vec &y) {
-    static int resident = -1, y_resident = -1;
-    if (resident < 0) {
-        resident = env_flag("SPMV_HIP_X_RESIDENT") ? 1 : 0;
-        y_resident = env_flag("SPMV_HIP_Y_RESIDENT") ? 1 : 0;
-    }
+    // read per call (a getenv is ~0.1 us against a >= 2 us launch), so a
+    // process may switch modes between plans
+    const bool resident = env_flag("SPMV_HIP_X_RESIDENT"), y_resident = env_flag("SPMV_HIP_Y_RESIDENT");
     SpMatOpt &a = const_cast<SpMatOpt &>(A);  // the reference passes const& too
     const bool staged_x = resident && a.x_uploaded;
     int st;

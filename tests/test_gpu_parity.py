@@ -697,6 +697,7 @@ def test_device_conversion_matches_host_build():
     ELL, HYB, JDS, DIA, COO, and AUTO resolved from device data) gives the
     host builder's layout byte for byte (spmv_plan_digest, array by array)
     and so the same y; a format the host refuses is refused on the device."""
+    import torch
     for name, m, n, rp, col, val in _device_build_cases():
         x = sp.generate_vector(n, seed=9)
         yo = oracle_y(rp, col, val, x)
