@@ -661,15 +661,38 @@ int build_hyb(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
 }
 
 // ---------------------------------------------------------------- SS
+// x window of each tile for ss_stream_kernel: the column range of its 64 x
+// SIGMA positions (padding positions read column 0, as they do in the kernel)
+// when it spans <= kSsWinCols columns, else none
+void ss_tile_windows(const int32_t *col, int64_t nnz, int64_t n_tiles, int sigma, std::vector<int32_t> &win) {
+    const int64_t T = 64 * (int64_t)sigma;
+    win.assign((size_t)(2 * std::max<int64_t>(n_tiles, 1)), 0);
+#pragma omp parallel for schedule(static)
+    for (int64_t t = 0; t < n_tiles; ++t) {
+        int32_t lo = std::numeric_limits<int32_t>::max(), hi = -1;
+        for (int64_t i = t * T; i < (t + 1) * T; ++i) {
+            const int32_t c = i < nnz ? col[i] : 0;
+            lo = std::min(lo, c);
+            hi = std::max(hi, c);
+        }
+        if (hi - lo < kSsWinCols) {
+            win[(size_t)(2 * t)] = lo;
+            win[(size_t)(2 * t + 1)] = hi - lo + 1;
+        }
+    }
+}
+
 int build_ss(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
     SsDev &s = p->ss;
     const double mean = A.m ? (double)A.nnz / (double)A.m : 0.0;
     s.sigma = o.ss_sigma > 0 ? o.ss_sigma : auto_ss_sigma(mean);
-    if (s.sigma % 4 || s.sigma < 4 || s.sigma > 32 || s.sigma == 28) {
-        set_error("ss_sigma must be one of 4,8,12,16,20,24,32");
+    if (!ss_sigma_ok(s.sigma)) {
+        set_error("ss_sigma must be one of 4,8,12,16,20,24,32,48,64");
         return SPMV_ERROR_INVALID_VALUE;
     }
+    ss_probe_options(s);
     const int64_t T = 64 * (int64_t)s.sigma;
+    const int W = ss_flag_words(s.sigma);
     s.n_tiles = (A.nnz + T - 1) / T;
     // ordinals of non-empty rows
     std::vector<int64_t> nzord((size_t)A.m + 1, 0);
@@ -688,12 +711,12 @@ int build_ss(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
         SPMV_RETURN_IF(upload(p, &s.empty_rows, empty.data(), s.n_empty));
     }
     const int64_t total = s.n_tiles * T;
-    std::vector<uint32_t> flags((size_t)s.n_tiles * 64, 0u);
+    std::vector<uint32_t> flags((size_t)s.n_tiles * 64 * W, 0u);
     std::vector<int32_t> tord((size_t)s.n_tiles);
     auto set_flag = [&](int64_t pos) {
-        const int64_t t = pos / T, li = pos % T;
-        uint32_t *w = &flags[(size_t)(t * 64 + li / s.sigma)];
-        __atomic_fetch_or(w, 1u << (li % s.sigma), __ATOMIC_RELAXED);
+        const int64_t t = pos / T, li = pos % T, k = li % s.sigma;
+        uint32_t *w = &flags[(size_t)((t * W + k / 32) * 64 + li / s.sigma)];
+        __atomic_fetch_or(w, 1u << (k % 32), __ATOMIC_RELAXED);
     };
 #pragma omp parallel for schedule(static)
     for (int64_t r = 0; r < A.m; ++r)
@@ -717,19 +740,34 @@ int build_ss(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
             val[vpos] = i < A.nnz ? A.val[i] : 0.0;
         }
     }
+    std::vector<int32_t> win;
+    ss_tile_windows(A.col, A.nnz, s.n_tiles, s.sigma, win);
     SPMV_RETURN_IF(upload(p, &s.col, col.data(), total));
     SPMV_RETURN_IF(upload(p, &s.val, val.data(), total));
-    SPMV_RETURN_IF(upload(p, &s.flags, flags.data(), s.n_tiles * 64));
+    SPMV_RETURN_IF(upload(p, &s.flags, flags.data(), s.n_tiles * 64 * W));
     SPMV_RETURN_IF(upload(p, &s.tile_ord, tord.data(), s.n_tiles));
+    SPMV_RETURN_IF(upload(p, &s.win, win.data(), 2 * s.n_tiles));
     SPMV_RETURN_IF(dev_alloc(p, &s.head, s.n_tiles));
     SPMV_RETURN_IF(dev_alloc(p, &s.tail, s.n_tiles));
     SPMV_RETURN_IF(dev_alloc(p, &s.tail_ord, s.n_tiles));
-    p->stored_slots = total;
-    p->empty_rows = s.n_empty;
-    p->algo_bytes = 12 * A.nnz + 8 * A.n + 8 * A.m;
-    p->n_kernels = 2;
-    p->kernel_name = "ss_tile_kernel<" + std::to_string(s.sigma) + ">+ss_fixup_kernel";
+    ss_finish_info(p);
     return SPMV_SUCCESS;
+}
+
+void ss_finish_info(spmv_plan_s *p) {
+    const SsDev &s = p->ss;
+    p->stored_slots = s.n_tiles * 64 * s.sigma;
+    p->empty_rows = s.n_empty;
+    p->algo_bytes = 12 * p->nnz + 8 * p->n + 8 * p->m;
+    p->n_kernels = 2;
+    p->kernel_name = std::string(s.kernel == 0 && s.sigma <= 32 ? "ss_tile_kernel<" : "ss_stream_kernel<") +
+                     std::to_string(s.sigma) + ">+ss_fixup_kernel";
+}
+
+// probe build: SPMV_SS_KERNEL (0 = ss_tile_kernel), SPMV_SS_PF at plan build
+void ss_probe_options(SsDev &s) {
+    if (const char *e = probe_env("SPMV_SS_KERNEL")) s.kernel = std::atoi(e);
+    if (const char *e = probe_env("SPMV_SS_PF")) s.pf = std::atoi(e);
 }
 
 // ---------------------------------------------------------------- DIA

@@ -198,12 +198,21 @@ struct HybDev {
 // tile_ord[t]: ordinal (among non-empty rows) of the first row that starts
 // inside tile t.  Rows that cross tiles are finished by a fixup kernel from
 // per-tile head/tail partials (deterministic, no atomics, β = 0).
+constexpr int kSsWinCols = 512;  // widest per-tile x window (doubles of LDS per wave)
+// flag words per lane of a tile: bit k of word k/32 (SIGMA <= 64)
+__host__ __device__ inline int ss_flag_words(int sigma) { return sigma > 32 ? 2 : 1; }
+inline bool ss_sigma_ok(int sigma) {
+    return sigma >= 4 && sigma % 4 == 0 && (sigma <= 24 || sigma == 32 || sigma == 48 || sigma == 64);
+}
 struct SsDev {
     int sigma = 16;
     int64_t n_tiles = 0;
     int32_t *col = nullptr;
     double *val = nullptr;
-    uint32_t *flags = nullptr;
+    uint32_t *flags = nullptr;   // [n_tiles][words][64]
+    int32_t *win = nullptr;      // [n_tiles][2]: x window (first column, length; 0 = none)
+    int kernel = 1;              // 1 = ss_stream_kernel, 0 = ss_tile_kernel (SIGMA <= 32)
+    int pf = 2;                  // ss_stream_kernel: quads loaded ahead
     int32_t *tile_ord = nullptr;
     double *head = nullptr;      // scratch [n_tiles]
     double *tail = nullptr;      // scratch [n_tiles]
@@ -497,6 +506,9 @@ int csr_plan_lanes(spmv_plan_s *p, const int64_t *row_ptr, int64_t m, const spmv
 int csr_windows_finish(spmv_plan_s *p, const std::vector<int32_t> &lo, const std::vector<int32_t> &hi);
 void csr_finish_info(spmv_plan_s *p);
 int auto_ss_sigma(double mean_row);
+void ss_tile_windows(const int32_t *col, int64_t nnz, int64_t n_tiles, int sigma, std::vector<int32_t> &win);
+void ss_finish_info(spmv_plan_s *p);
+void ss_probe_options(SsDev &s);
 
 // end of one phase of a multi-kernel launch (no-op unless profiling)
 inline void phase_mark(const spmv_plan_s *p) {

@@ -98,6 +98,7 @@ __global__ void compact_rows(const int64_t *__restrict__ rp, const int64_t *__re
 __global__ void start_flags(const int64_t *__restrict__ rp, int64_t m, int64_t nnz, int sigma,
                             uint32_t *__restrict__ flags) {
     const int64_t T = 64 * (int64_t)sigma;
+    const int W = ss_flag_words(sigma);
     for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r <= m; r += (int64_t)gridDim.x * blockDim.x) {
         int64_t pos;
         if (r < m) {
@@ -107,8 +108,8 @@ __global__ void start_flags(const int64_t *__restrict__ rp, int64_t m, int64_t n
             if (nnz % T == 0) continue;
             pos = nnz;
         }
-        const int64_t t = pos / T, li = pos % T;
-        atomicOr(&flags[t * 64 + li / sigma], 1u << (li % sigma));
+        const int64_t t = pos / T, li = pos % T, k = li % sigma;
+        atomicOr(&flags[(t * W + k / 32) * 64 + li / sigma], 1u << (k % 32));
     }
 }
 
@@ -143,6 +144,31 @@ __global__ void tile_transpose(const int32_t *__restrict__ col, const double *__
         const int64_t r = w & 255, vlane = (r & 127) >> 1, vk = q * 4 + (r >> 7) * 2 + (r & 1);
         const int64_t vi = t * T + vlane * sigma + vk;
         tval[pos] = vi < nnz ? val[vi] : 0.0;
+    }
+}
+
+// x window of every tile (ss_tile_windows, formats.cpp): one wave per tile
+// reduces the column range of its 64 x sigma positions (padding: column 0)
+__global__ __launch_bounds__(256) void tile_windows(const int32_t *__restrict__ col, int64_t nnz, int sigma,
+                                                    int64_t n_tiles, int32_t *__restrict__ win) {
+    const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (t >= n_tiles) return;
+    const int64_t T = 64 * (int64_t)sigma;
+    int lo = INT32_MAX, hi = -1;
+    for (int64_t i = t * T + lane; i < (t + 1) * T; i += 64) {
+        const int c = i < nnz ? col[i] : 0;
+        lo = c < lo ? c : lo;
+        hi = c > hi ? c : hi;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        lo = min(lo, __shfl_xor(lo, o, 64));
+        hi = max(hi, __shfl_xor(hi, o, 64));
+    }
+    if (lane == 0) {
+        const bool fits = hi - lo < kSsWinCols;
+        win[2 * t] = fits ? lo : 0;
+        win[2 * t + 1] = fits ? hi - lo + 1 : 0;
     }
 }
 
@@ -322,10 +348,12 @@ int build_ss_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, c
     SsDev &s = p->ss;
     const hipStream_t st = p->stream;
     s.sigma = o.ss_sigma > 0 ? o.ss_sigma : auto_ss_sigma(mean_row);
-    if (s.sigma % 4 || s.sigma < 4 || s.sigma > 32 || s.sigma == 28) {
-        set_error("ss_sigma must be one of 4,8,12,16,20,24,32");
+    if (!ss_sigma_ok(s.sigma)) {
+        set_error("ss_sigma must be one of 4,8,12,16,20,24,32,48,64");
         return SPMV_ERROR_INVALID_VALUE;
     }
+    ss_probe_options(s);
+    const int W = ss_flag_words(s.sigma);
     const int64_t m = p->m, nnz = p->nnz, T = 64 * (int64_t)s.sigma;
     s.n_tiles = (nnz + T - 1) / T;
     // scratch freed on every exit path (after the stream drains)
@@ -359,9 +387,9 @@ int build_ss_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, c
         hipLaunchKernelGGL(compact_rows, dim3(grid_for(m)), dim3(256), 0, st, d_rp, nzord, m, s.nzrow, s.empty_rows);
     }
     const int64_t total = s.n_tiles * T;
-    SPMV_RETURN_IF(p->arena.alloc(&q, 4 * (size_t)std::max<int64_t>(s.n_tiles * 64, 1)));
+    SPMV_RETURN_IF(p->arena.alloc(&q, 4 * (size_t)std::max<int64_t>(s.n_tiles * 64 * W, 1)));
     s.flags = (uint32_t *)q;
-    SPMV_HIP_TRY(hipMemsetAsync(s.flags, 0, 4 * (size_t)std::max<int64_t>(s.n_tiles * 64, 1), st));
+    SPMV_HIP_TRY(hipMemsetAsync(s.flags, 0, 4 * (size_t)std::max<int64_t>(s.n_tiles * 64 * W, 1), st));
     hipLaunchKernelGGL(start_flags, dim3(grid_for(m + 1)), dim3(256), 0, st, d_rp, m, nnz, s.sigma, s.flags);
     SPMV_RETURN_IF(p->arena.alloc(&q, 4 * (size_t)std::max<int64_t>(s.n_tiles, 1)));
     s.tile_ord = (int32_t *)q;
@@ -374,6 +402,11 @@ int build_ss_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, c
     hipLaunchKernelGGL(tile_transpose, dim3(grid_for(total)), dim3(256), 0, st, d_col, d_val, nnz, s.sigma, total,
                        s.col, s.val);
     SPMV_RETURN_IF(p->arena.alloc(&q, 8 * (size_t)std::max<int64_t>(s.n_tiles, 1)));
+    s.win = (int32_t *)q;
+    if (s.n_tiles > 0)
+        hipLaunchKernelGGL(tile_windows, dim3((unsigned)((s.n_tiles + 3) / 4)), dim3(256), 0, st, d_col, nnz, s.sigma,
+                           s.n_tiles, s.win);
+    SPMV_RETURN_IF(p->arena.alloc(&q, 8 * (size_t)std::max<int64_t>(s.n_tiles, 1)));
     s.head = (double *)q;
     SPMV_RETURN_IF(p->arena.alloc(&q, 8 * (size_t)std::max<int64_t>(s.n_tiles, 1)));
     s.tail = (double *)q;
@@ -385,11 +418,7 @@ int build_ss_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, c
         set_error(std::string("device SS conversion: ") + hipGetErrorString(e));
         return SPMV_ERROR_HIP;
     }
-    p->stored_slots = total;
-    p->empty_rows = s.n_empty;
-    p->algo_bytes = 12 * nnz + 8 * p->n + 8 * m;
-    p->n_kernels = 2;
-    p->kernel_name = "ss_tile_kernel<" + std::to_string(s.sigma) + ">+ss_fixup_kernel";
+    ss_finish_info(p);
     return SPMV_SUCCESS;
 }
 

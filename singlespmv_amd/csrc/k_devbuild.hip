@@ -474,7 +474,8 @@ int plan_arrays(const spmv_plan_s *p, std::vector<ArrayRef> &a) {
             const int64_t total = s.n_tiles * 64 * s.sigma;
             add("col", s.col, 4 * total);
             add("val", s.val, 8 * total);
-            add("flags", s.flags, 4 * 64 * s.n_tiles);
+            add("flags", s.flags, 4 * 64 * ss_flag_words(s.sigma) * s.n_tiles);
+            add("win", s.win, 8 * s.n_tiles);
             add("tile_ord", s.tile_ord, 4 * s.n_tiles);
             add("nzrow", s.nzrow, 4 * s.n_nonempty);
             add("empty_rows", s.empty_rows, 4 * s.n_empty);

@@ -153,6 +153,115 @@ __global__ __launch_bounds__(256) void ss_tile_kernel(
     }
 }
 
+// ss_stream_kernel<SIGMA, WIN, PF>: the same tile, sums and hand-off as
+// ss_tile_kernel (bit-identical y), streamed: the quads of a lane are loaded
+// PF ahead of the quad being summed (sched_barrier-fenced stages), so a lane
+// holds PF + 1 quads instead of all SIGMA entries -- SIGMA up to 64 (two flag
+// words per lane) at the register cost of SIGMA 12.  The x window of a tile is
+// a plan-time descriptor (SsDev::win: first column, length), so the wave
+// stages it while its first quads are still in flight instead of after its
+// columns arrive.
+template <int SIGMA, bool WIN, int PF>
+__global__ __launch_bounds__(256) void ss_stream_kernel(
+    int64_t n_tiles, const int32_t *__restrict__ col, const double *__restrict__ val,
+    const uint32_t *__restrict__ flags, const int32_t *__restrict__ tile_ord, const int32_t *__restrict__ win,
+    const int32_t *__restrict__ nzrow, int64_t n_nonempty, const double *__restrict__ x,
+    double *__restrict__ y, double *__restrict__ head, double *__restrict__ tail,
+    int32_t *__restrict__ tail_ord) {
+    static_assert(SIGMA % 4 == 0 && SIGMA <= 64, "sigma");
+    constexpr int Q = SIGMA / 4, W = SIGMA > 32 ? 2 : 1;
+    const int64_t tile = (int64_t)blockIdx.x * (blockDim.x / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (tile >= n_tiles) return;  // wave-uniform
+    const int64_t base = tile * 64 * SIGMA;
+    const int32_t *cp = col + base + lane * 4;
+    const double *vp = val + base + lane * 2;
+    i32x4 c[Q];
+    f64x2 a[Q], b[Q];
+    auto load = [&](int q) {
+        c[q] = ld_stream4(cp + q * 256);
+        a[q] = ld_stream2(vp + q * 256);
+        b[q] = ld_stream2(vp + q * 256 + 128);
+    };
+#pragma unroll
+    for (int q = 0; q < (PF < Q ? PF : Q); ++q) load(q);
+    uint32_t f[W];
+#pragma unroll
+    for (int w = 0; w < W; ++w) f[w] = flags[(tile * W + w) * 64 + lane];
+    __shared__ double xs[4][kSsWin];
+    const int wv = threadIdx.x >> 6;
+    int32_t lo = 0, len = 0;
+    if constexpr (WIN) {
+        lo = win[2 * tile];
+        len = win[2 * tile + 1];
+        if (len > 0) {  // wave-uniform
+            for (int i = lane; i < len; i += 64) xs[wv][i] = ld_x(x, lo + i);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+    }
+    int pc = 0;
+#pragma unroll
+    for (int w = 0; w < W; ++w) pc += __builtin_popcount(f[w]);
+    const int incl = wave_inclusive_sum(pc, lane);
+    const int64_t ord0 = (int64_t)tile_ord[tile] + (incl - pc);  // this lane's first start
+
+    double run = 0.0, head_l = 0.0;
+    int seen = 0;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+        if (q + PF < Q) load(q + PF);
+        __builtin_amdgcn_sched_barrier(0);
+        double g[4];
+        if (WIN && len > 0) {
+            g[0] = xs[wv][c[q].x - lo];
+            g[1] = xs[wv][c[q].y - lo];
+            g[2] = xs[wv][c[q].z - lo];
+            g[3] = xs[wv][c[q].w - lo];
+        } else {
+            g[0] = ld_x(x, c[q].x);
+            g[1] = ld_x(x, c[q].y);
+            g[2] = ld_x(x, c[q].z);
+            g[3] = ld_x(x, c[q].w);
+        }
+        const double v[4] = {a[q].x, a[q].y, b[q].x, b[q].y};
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+            const int k = 4 * q + kk;
+            if ((f[k >> 5] >> (k & 31)) & 1u) {
+                if (seen == 0) head_l = run;
+                else ss_store(y, nzrow, n_nonempty, ord0 + seen - 1, run);
+                run = 0.0;
+                ++seen;
+            }
+            run = madd(v[kk], g[kk], run);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+
+    const bool has = pc != 0;
+    const double S = wave_seg_scan(run, has, lane);  // open-segment sum at lane end
+    double C = __shfl_up(S, 1, 64);
+    if (lane == 0) C = 0.0;
+    const uint64_t ball = __ballot(has);
+    const bool started_before = (ball & ((1ull << lane) - 1ull)) != 0ull;
+    if (has) {
+        const double tot = __dadd_rn(C, head_l);
+        if (started_before) ss_store(y, nzrow, n_nonempty, ord0 - 1, tot);
+        else head[tile] = tot;  // exactly one lane: the first lane with a start
+    }
+    if (lane == 63) {
+        if (ball == 0ull) {
+            head[tile] = S;  // the whole tile continues an earlier row
+            tail_ord[tile] = -1;
+        } else {
+            tail[tile] = S;
+            tail_ord[tile] = tile_ord[tile] + incl - 1;
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void ss_fixup_kernel(int64_t n_tiles, const double *__restrict__ head,
                                                        const double *__restrict__ tail,
                                                        const int32_t *__restrict__ tail_ord,
@@ -179,16 +288,38 @@ template <int SIGMA>
 static void launch_ss_t(const spmv_plan_s *p, const double *x, double *y) {
     const SsDev &s = p->ss;
     const int64_t blocks = (s.n_tiles + 3) / 4;
-    bool win = true;  // probe build: SPMV_LAUNCH_SS_WIN=0 gathers x from memory always
+    // probe build: SPMV_LAUNCH_SS = 0 -> ss_tile_kernel (all SIGMA entries
+    // loaded up front, window from the loaded columns, round 4), else the
+    // streamed kernel with SPMV_LAUNCH_SS_PF quads ahead; SPMV_LAUNCH_SS_WIN=0
+    // gathers x from memory always
+    int kind = SIGMA > 32 ? 1 : s.kernel, pf = s.pf;
+    bool win = true;
+    if (const char *v = probe_env("SPMV_LAUNCH_SS")) kind = SIGMA > 32 ? 1 : std::atoi(v);
+    if (const char *v = probe_env("SPMV_LAUNCH_SS_PF")) pf = std::atoi(v);
     if (const char *v = probe_env("SPMV_LAUNCH_SS_WIN")) win = std::atoi(v) != 0;
-    if (win)
-        hipLaunchKernelGGL((ss_tile_kernel<SIGMA, true>), dim3((unsigned)blocks), dim3(256), 0, p->stream,
-                           s.n_tiles, s.col, s.val, s.flags, s.tile_ord, s.nzrow, s.n_nonempty, x, y,
-                           s.head, s.tail, s.tail_ord);
-    else
-        hipLaunchKernelGGL((ss_tile_kernel<SIGMA, false>), dim3((unsigned)blocks), dim3(256), 0, p->stream,
-                           s.n_tiles, s.col, s.val, s.flags, s.tile_ord, s.nzrow, s.n_nonempty, x, y,
-                           s.head, s.tail, s.tail_ord);
+    auto go = [&](auto kern, bool stream) {
+        if (stream)
+            hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), 0, p->stream, s.n_tiles, s.col, s.val, s.flags,
+                               s.tile_ord, s.win, s.nzrow, s.n_nonempty, x, y, s.head, s.tail, s.tail_ord);
+    };
+    if (kind == 0 && SIGMA <= 32) {
+        constexpr int S0 = SIGMA <= 32 ? SIGMA : 32;
+        if (win)
+            hipLaunchKernelGGL((ss_tile_kernel<S0, true>), dim3((unsigned)blocks), dim3(256), 0, p->stream,
+                               s.n_tiles, s.col, s.val, s.flags, s.tile_ord, s.nzrow, s.n_nonempty, x, y,
+                               s.head, s.tail, s.tail_ord);
+        else
+            hipLaunchKernelGGL((ss_tile_kernel<S0, false>), dim3((unsigned)blocks), dim3(256), 0, p->stream,
+                               s.n_tiles, s.col, s.val, s.flags, s.tile_ord, s.nzrow, s.n_nonempty, x, y,
+                               s.head, s.tail, s.tail_ord);
+        return;
+    }
+    win = win && s.win;
+    switch (pf) {
+        case 1: win ? go(ss_stream_kernel<SIGMA, true, 1>, true) : go(ss_stream_kernel<SIGMA, false, 1>, true); break;
+        case 4: win ? go(ss_stream_kernel<SIGMA, true, 4>, true) : go(ss_stream_kernel<SIGMA, false, 4>, true); break;
+        default: win ? go(ss_stream_kernel<SIGMA, true, 2>, true) : go(ss_stream_kernel<SIGMA, false, 2>, true);
+    }
 }
 
 int launch_ss(const spmv_plan_s *p, const double *x, double *y) {
@@ -202,7 +333,9 @@ int launch_ss(const spmv_plan_s *p, const double *x, double *y) {
             case 20: launch_ss_t<20>(p, x, y); break;
             case 24: launch_ss_t<24>(p, x, y); break;
             case 32: launch_ss_t<32>(p, x, y); break;
-            default: set_error("ss sigma must be one of 4,8,12,16,20,24,32"); return SPMV_ERROR_INVALID_VALUE;
+            case 48: launch_ss_t<48>(p, x, y); break;
+            case 64: launch_ss_t<64>(p, x, y); break;
+            default: set_error("ss sigma must be one of 4,8,12,16,20,24,32,48,64"); return SPMV_ERROR_INVALID_VALUE;
         }
         SPMV_HIP_TRY(hipGetLastError());
     }

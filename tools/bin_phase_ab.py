@@ -51,9 +51,12 @@ def main():
     plans = []
     for part in filter(None, a.variants.split(";")):
         name, _, envs = part.partition(":")
-        saved, opts = {}, {}
+        saved, opts, fmt = {}, {}, a.fmt
         for kv in filter(None, envs.split(",")):
             k, v = kv.split("=")
+            if k == "fmt":  # this variant's format (the others: --fmt)
+                fmt = v
+                continue
             if k.islower():
                 opts[k] = int(v)
                 continue
@@ -61,7 +64,7 @@ def main():
             os.environ[k] = v
         kw = dict(placement=a.placement)
         kw.update(opts)
-        p = sp.Plan.from_csr(m, n, rp, col, val, a.fmt, **kw)
+        p = sp.Plan.from_csr(m, n, rp, col, val, fmt, **kw)
         for k, v in saved.items():
             if v is None:
                 os.environ.pop(k, None)
