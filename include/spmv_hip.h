@@ -137,22 +137,26 @@ typedef struct spmv_options {
  * plain hipMalloc on most plans than with the same buffer built from 2-MB
  * physical handles (profiles/round1/README.md §4a "Placement, round 3").
  *
- * Known limitation: placement is not fully under the library's control.  In
- * a long-lived process that builds several large plans, about one plan in
- * three lands in memory where the BIN Mul runs 15-23 % slower (and DIA at
- * config 4 varies 1.48-1.54 ms), VMM or not; the first plan of a process has
- * been fast on three boxes of four.  A caller who needs the best time should
- * build its hot plan first (or rebuild a slow one); no API exposes the
- * placement the hardware picked (profiles/round3/probe/
- * mulorder_plans_arena_vmm_n8.jsonl). */
+ * Known limitation: placement is not fully under the library's control.
+ * Measured residual spread of AUTO over 8 same-size plans kept alive in one
+ * process (profiles/round5/placement/): config-4 DIA 1.472-1.562 ms (6.1 %,
+ * every later plan within 1 % of the first or faster), config-2 BIN
+ * 0.797-0.897 ms (12.6 %, worst 7.6 % above the first).  SEARCH narrowed
+ * that to 1.2 % (DIA 1.478-1.495) and 4.2 % (BIN 0.801-0.835) at 0.6-7.3 s
+ * of build per plan and transient candidate buffers over the free HBM, so it
+ * stays an explicit opt-in; a caller who needs the best time builds its hot
+ * plan first or with SEARCH (spmv_plan_info reports the mode, the candidates
+ * and their best / worst launch). */
 #define SPMV_PLACEMENT_AUTO 0   /* BIN products >= 32 MB, DIA values >= 256 MB and
                                    the streamed arrays (col / val / slots) of the
                                    other formats >= 256 MB: VMM; the rest PLAIN  */
 #define SPMV_PLACEMENT_PLAIN 1  /* one hipMalloc                                     */
-#define SPMV_PLACEMENT_SEARCH 2 /* experiment (probe build only; the product library
-                                   returns SPMV_ERROR_NOT_SUPPORTED): up to 8
-                                   candidates spread over all free HBM, each timed
-                                   with one launch, the fastest kept              */
+#define SPMV_PLACEMENT_SEARCH 2 /* BIN product buffer (>= 32 MB) / DIA values
+                                   (>= 256 MB): up to 8 plain candidates spread
+                                   over all free HBM, each timed with one launch
+                                   over a zero x, the fastest kept (build-time
+                                   cost and transient memory: see above); other
+                                   formats: as AUTO                               */
 #define SPMV_PLACEMENT_VMM 3    /* hipMemCreate handles of 2 MB mapped back to back
                                    into one VA range aligned to 1 GB (no transient
                                    device memory)                                 */

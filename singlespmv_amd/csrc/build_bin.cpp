@@ -636,7 +636,6 @@ static int alloc_prod_plain(spmv_plan_s *p, size_t prod_bytes) {
     return SPMV_SUCCESS;
 }
 
-#ifdef SPMV_PROBES
 // SPMV_PLACEMENT_SEARCH: keep the fastest of up to K candidates, each timed
 // with a Mul pass over a zero x at build time (results never depend on it).
 // Up to 8 candidates: best-of-4 still left 5 of 9 config-2 plans in the slow
@@ -726,7 +725,6 @@ static int bin_place_search(spmv_plan_s *p, int64_t n, size_t prod_bytes) {
     B.placement_ms.assign(t.begin(), t.end());
     return SPMV_SUCCESS;
 }
-#endif  // SPMV_PROBES
 
 static int bin_place_prod(spmv_plan_s *p, int64_t n, size_t prod_bytes, const spmv_options_t &o) {
     BinDev &B = p->bin;
@@ -747,9 +745,7 @@ static int bin_place_prod(spmv_plan_s *p, int64_t n, size_t prod_bytes, const sp
     // by placement as much as config 2's does: search from 32 MB
     if (mode == SPMV_PLACEMENT_SEARCH && prod_bytes < ((size_t)32 << 20)) mode = SPMV_PLACEMENT_PLAIN;
     B.placement = mode;
-#ifdef SPMV_PROBES
     if (mode == SPMV_PLACEMENT_SEARCH) return bin_place_search(p, n, prod_bytes);
-#endif
     if (mode == SPMV_PLACEMENT_VMM) {
         size_t chunk = kVmmChunk, align = kVmmAlign;
         if (const char *e = probe_env("SPMV_VMM_CHUNK_MB")) chunk = (size_t)std::max(1, std::atoi(e)) << 20;

@@ -768,6 +768,7 @@ void ss_finish_info(spmv_plan_s *p) {
 void ss_probe_options(SsDev &s) {
     if (const char *e = probe_env("SPMV_SS_KERNEL")) s.kernel = std::atoi(e);
     if (const char *e = probe_env("SPMV_SS_PF")) s.pf = std::atoi(e);
+    if (const char *e = probe_env("SPMV_SS_STAGE")) s.stage = std::atoi(e) != 0;
 }
 
 // ---------------------------------------------------------------- DIA
@@ -800,7 +801,7 @@ int dia_placement(spmv_plan_s *p, int64_t m, int64_t n, size_t bytes, const spmv
     int mode = o.placement;
     SPMV_RETURN_IF(placement_mode_check(mode));
     if (const char *e = probe_env("SPMV_PLACEMENT_MODE")) mode = std::atoi(e);
-    if (mode == SPMV_PLACEMENT_AUTO) mode = SPMV_PLACEMENT_PLAIN;  // the search: probe build only, as BIN's
+    if (mode == SPMV_PLACEMENT_AUTO) mode = SPMV_PLACEMENT_PLAIN;
     if (mode == SPMV_PLACEMENT_SEARCH && bytes < ((size_t)256 << 20)) mode = SPMV_PLACEMENT_PLAIN;
     d.placement = mode;
     if (mode == SPMV_PLACEMENT_PLAIN) return SPMV_SUCCESS;
@@ -815,11 +816,6 @@ int dia_placement(spmv_plan_s *p, int64_t m, int64_t n, size_t bytes, const spmv
         d.val = (double *)q;
         return SPMV_SUCCESS;
     }
-#ifndef SPMV_PROBES
-    (void)m;
-    (void)n;
-    return SPMV_SUCCESS;
-#else
     int K = 8;
     if (const char *e = probe_env("SPMV_DIA_PLACEMENT")) K = std::max(1, std::min(8, std::atoi(e)));
     if (K <= 1) return SPMV_SUCCESS;
@@ -894,7 +890,6 @@ int dia_placement(spmv_plan_s *p, int64_t m, int64_t n, size_t bytes, const spmv
         std::fprintf(stderr, " -> %zu\n", best);
     }
     return st;
-#endif  // SPMV_PROBES
 }
 
 int build_dia(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {

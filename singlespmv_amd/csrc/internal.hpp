@@ -66,19 +66,12 @@ inline int launch_dbg(int plan_dbg) {
     return plan_dbg;
 }
 
-// The placement search (SPMV_PLACEMENT_SEARCH) exists only in
-// the probe build: the product library holds no transient device memory at
-// create and times nothing.  SPMV_PLACEMENT_VMM (2-MB physical handles mapped
-// into one 1-GB-aligned VA range) is what AUTO uses for large BIN product
-// buffers.
+// Placement modes.  AUTO (the default) holds no transient
+// device memory at create and times nothing; SPMV_PLACEMENT_SEARCH is the
+// caller's explicit opt-in to a build-time search (transient candidate
+// buffers spread over free HBM, one timed launch each).
 inline int placement_mode_check(int mode) {
     SPMV_CHECK_ARG(mode >= SPMV_PLACEMENT_AUTO && mode <= SPMV_PLACEMENT_VMM, "unknown placement mode");
-#ifndef SPMV_PROBES
-    if (mode == SPMV_PLACEMENT_SEARCH) {
-        set_error("the placement search is an experiment of the probe build (make probes)");
-        return SPMV_ERROR_NOT_SUPPORTED;
-    }
-#endif
     return SPMV_SUCCESS;
 }
 constexpr size_t kVmmChunk = (size_t)2 << 20;          // physical handle size
@@ -213,6 +206,7 @@ struct SsDev {
     int32_t *win = nullptr;      // [n_tiles][2]: x window (first column, length; 0 = none)
     int kernel = 1;              // 1 = ss_stream_kernel, 0 = ss_tile_kernel (SIGMA <= 32)
     int pf = 2;                  // ss_stream_kernel: quads loaded ahead
+    bool stage = true;           // ss_stream_kernel: finished rows staged in LDS, stored after the stream
     int32_t *tile_ord = nullptr;
     double *head = nullptr;      // scratch [n_tiles]
     double *tail = nullptr;      // scratch [n_tiles]

@@ -29,6 +29,8 @@
 // csr5_spmv_cuda.h:313-382), and zeroes empty rows.  Every y entry is written
 // exactly once per execute (β = 0), fixing the CSR5 non-idempotence noted in
 // SURVEY §3.5.
+#include <type_traits>
+
 #include "device.hpp"
 #include "internal.hpp"
 
@@ -161,7 +163,9 @@ __global__ __launch_bounds__(256) void ss_tile_kernel(
 // a plan-time descriptor (SsDev::win: first column, length), so the wave
 // stages it while its first quads are still in flight instead of after its
 // columns arrive.
-template <int SIGMA, bool WIN, int PF>
+constexpr int kSsStageRows = 256;  // rows a wave stages in LDS before writing them out
+
+template <int SIGMA, bool WIN, int PF, bool STAGE>
 __global__ __launch_bounds__(256) void ss_stream_kernel(
     int64_t n_tiles, const int32_t *__restrict__ col, const double *__restrict__ val,
     const uint32_t *__restrict__ flags, const int32_t *__restrict__ tile_ord, const int32_t *__restrict__ win,
@@ -205,7 +209,19 @@ __global__ __launch_bounds__(256) void ss_stream_kernel(
 #pragma unroll
     for (int w = 0; w < W; ++w) pc += __builtin_popcount(f[w]);
     const int incl = wave_inclusive_sum(pc, lane);
-    const int64_t ord0 = (int64_t)tile_ord[tile] + (incl - pc);  // this lane's first start
+    const int64_t ord_base = tile_ord[tile];  // rel ordinal r below = row ord_base + r
+    // STAGE: the rows finished inside the tile (ordinals ord_base + [0,
+    // total - 1)) go to an LDS slice and leave as coalesced stores after the
+    // stream, so no y store sits between the tile's loads in the in-order
+    // vmcnt queue; tiles finishing more rows than the slice store directly
+    __shared__ double ys[STAGE ? 4 : 1][STAGE ? kSsStageRows : 1];
+    const int total = __shfl(incl, 63, 64);
+    const bool stage = STAGE && total <= kSsStageRows;  // wave-uniform
+    auto finish = [&](int rel, double v) {
+        if (STAGE && stage) ys[STAGE ? wv : 0][rel] = v;
+        else ss_store(y, nzrow, n_nonempty, ord_base + rel, v);
+    };
+    const int rel0 = incl - pc;  // this lane's first start
 
     double run = 0.0, head_l = 0.0;
     int seen = 0;
@@ -231,7 +247,7 @@ __global__ __launch_bounds__(256) void ss_stream_kernel(
             const int k = 4 * q + kk;
             if ((f[k >> 5] >> (k & 31)) & 1u) {
                 if (seen == 0) head_l = run;
-                else ss_store(y, nzrow, n_nonempty, ord0 + seen - 1, run);
+                else finish(rel0 + seen - 1, run);
                 run = 0.0;
                 ++seen;
             }
@@ -248,8 +264,16 @@ __global__ __launch_bounds__(256) void ss_stream_kernel(
     const bool started_before = (ball & ((1ull << lane) - 1ull)) != 0ull;
     if (has) {
         const double tot = __dadd_rn(C, head_l);
-        if (started_before) ss_store(y, nzrow, n_nonempty, ord0 - 1, tot);
+        if (started_before) finish(rel0 - 1, tot);
         else head[tile] = tot;  // exactly one lane: the first lane with a start
+    }
+    if constexpr (STAGE) {
+        if (stage) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            for (int i = lane; i < total - 1; i += 64) ss_store(y, nzrow, n_nonempty, ord_base + i, ys[wv][i]);
+        }
     }
     if (lane == 63) {
         if (ball == 0ull) {
@@ -257,7 +281,7 @@ __global__ __launch_bounds__(256) void ss_stream_kernel(
             tail_ord[tile] = -1;
         } else {
             tail[tile] = S;
-            tail_ord[tile] = tile_ord[tile] + incl - 1;
+            tail_ord[tile] = (int32_t)(ord_base + incl - 1);
         }
     }
 }
@@ -293,32 +317,40 @@ static void launch_ss_t(const spmv_plan_s *p, const double *x, double *y) {
     // streamed kernel with SPMV_LAUNCH_SS_PF quads ahead; SPMV_LAUNCH_SS_WIN=0
     // gathers x from memory always
     int kind = SIGMA > 32 ? 1 : s.kernel, pf = s.pf;
-    bool win = true;
+    size_t lds = 0;  // dynamic LDS per workgroup: caps workgroups per CU (probe: SPMV_LAUNCH_SS_LDS_KB)
+    bool win = true, stage = s.stage;
+    if (const char *v = probe_env("SPMV_LAUNCH_SS_STAGE")) stage = std::atoi(v) != 0;
+    if (const char *v = probe_env("SPMV_LAUNCH_SS_LDS_KB")) lds = (size_t)std::atoi(v) * 1024;
     if (const char *v = probe_env("SPMV_LAUNCH_SS")) kind = SIGMA > 32 ? 1 : std::atoi(v);
     if (const char *v = probe_env("SPMV_LAUNCH_SS_PF")) pf = std::atoi(v);
     if (const char *v = probe_env("SPMV_LAUNCH_SS_WIN")) win = std::atoi(v) != 0;
     auto go = [&](auto kern, bool stream) {
         if (stream)
-            hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), 0, p->stream, s.n_tiles, s.col, s.val, s.flags,
+            hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), lds, p->stream, s.n_tiles, s.col, s.val, s.flags,
                                s.tile_ord, s.win, s.nzrow, s.n_nonempty, x, y, s.head, s.tail, s.tail_ord);
     };
     if (kind == 0 && SIGMA <= 32) {
         constexpr int S0 = SIGMA <= 32 ? SIGMA : 32;
         if (win)
-            hipLaunchKernelGGL((ss_tile_kernel<S0, true>), dim3((unsigned)blocks), dim3(256), 0, p->stream,
+            hipLaunchKernelGGL((ss_tile_kernel<S0, true>), dim3((unsigned)blocks), dim3(256), lds, p->stream,
                                s.n_tiles, s.col, s.val, s.flags, s.tile_ord, s.nzrow, s.n_nonempty, x, y,
                                s.head, s.tail, s.tail_ord);
         else
-            hipLaunchKernelGGL((ss_tile_kernel<S0, false>), dim3((unsigned)blocks), dim3(256), 0, p->stream,
+            hipLaunchKernelGGL((ss_tile_kernel<S0, false>), dim3((unsigned)blocks), dim3(256), lds, p->stream,
                                s.n_tiles, s.col, s.val, s.flags, s.tile_ord, s.nzrow, s.n_nonempty, x, y,
                                s.head, s.tail, s.tail_ord);
         return;
     }
     win = win && s.win;
+    auto pick = [&](auto pfc) {
+        constexpr int P = decltype(pfc)::value;
+        if (stage) win ? go(ss_stream_kernel<SIGMA, true, P, true>, true) : go(ss_stream_kernel<SIGMA, false, P, true>, true);
+        else win ? go(ss_stream_kernel<SIGMA, true, P, false>, true) : go(ss_stream_kernel<SIGMA, false, P, false>, true);
+    };
     switch (pf) {
-        case 1: win ? go(ss_stream_kernel<SIGMA, true, 1>, true) : go(ss_stream_kernel<SIGMA, false, 1>, true); break;
-        case 4: win ? go(ss_stream_kernel<SIGMA, true, 4>, true) : go(ss_stream_kernel<SIGMA, false, 4>, true); break;
-        default: win ? go(ss_stream_kernel<SIGMA, true, 2>, true) : go(ss_stream_kernel<SIGMA, false, 2>, true);
+        case 1: pick(std::integral_constant<int, 1>{}); break;
+        case 4: pick(std::integral_constant<int, 4>{}); break;
+        default: pick(std::integral_constant<int, 2>{});
     }
 }
 

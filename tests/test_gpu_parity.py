@@ -201,8 +201,8 @@ def test_csr_window_kernel_small_shapes(m, n, lanes):
         check_close(y, yo, what=f"{m}x{n}")
 
 
-@pytest.mark.parametrize("sigma", [4, 8, 12, 16, 20, 24, 32])
-@pytest.mark.parametrize("kind", ["powerlaw", "uniform", "empty_rows"])
+@pytest.mark.parametrize("sigma", [4, 8, 12, 16, 20, 24, 32, 48, 64])
+@pytest.mark.parametrize("kind", ["powerlaw", "uniform", "empty_rows", "banded"])
 def test_ss_sigma(sigma, kind):
     m = 30011
     if kind == "empty_rows":
@@ -216,8 +216,8 @@ def test_ss_sigma(sigma, kind):
         keep = np.repeat(~zero, lens)
         col, val = np.ascontiguousarray(col[keep]), np.ascontiguousarray(val[keep])
         rp = np.concatenate([[0], np.cumsum(np.where(zero, 0, lens))]).astype(np.int64)
-    else:
-        spec = sp.gen_spec(kind, m, per_row=13, max_len=4000, seed=17)
+    else:  # banded: every tile's x window fits (ss_stream_kernel reads x from LDS)
+        spec = sp.gen_spec(kind, m, per_row=13, max_len=4000, band_lo=-40, band_hi=23, seed=17)
         rp, col, val = sp.generate_csr(spec)
     x = sp.generate_vector(m, seed=19)
     plan = sp.Plan.from_csr(m, m, rp, col, val, "ss", ss_sigma=sigma)
@@ -658,7 +658,7 @@ def _device_csr(rp, col, val):
 
 
 DEVICE_FORMATS = [("csr", {}), ("csr", {"csr_lanes": 1}), ("ss", {"ss_sigma": 4}), ("ss", {"ss_sigma": 16}),
-                  ("ss", {"ss_sigma": 32}), ("ss", {}), ("ell", {}), ("hyb", {}), ("hyb", {"ell_width": 4}),
+                  ("ss", {"ss_sigma": 32}), ("ss", {"ss_sigma": 64}), ("ss", {}), ("ell", {}), ("hyb", {}), ("hyb", {"ell_width": 4}),
                   ("jds", {}), ("jds", {"ell_width": 8}), ("dia", {}), ("coo", {}), ("auto", {})]
 
 
@@ -1000,8 +1000,8 @@ def test_plan_create_holds_only_the_plan(fmt, kind):
     """AUTO placement: while a large BIN / DIA plan is created, free device
     memory never drops by more than the plan's own bytes (+128 MB of runtime
     slack); ten plans built in a row behave the same.  The placement search
-    is refused by the product library: it exists only in the probe build
-    (DESIGN §3.6)."""
+    (an explicit opt-in) times its candidates and gives the same y bit for
+    bit."""
     m = 4_000_000
     spec = sp.gen_spec(kind, m, per_row=16, band_lo=-20, band_hi=20, seed=21)
     rp, col, val = sp.generate_csr(spec)
@@ -1012,9 +1012,15 @@ def test_plan_create_holds_only_the_plan(fmt, kind):
         # from 2-MB VMM handles
         assert info["format"] == fmt and info["placement"] == "vmm"
         assert drop <= info["device_bytes"] + (128 << 20), (i, drop, info["device_bytes"])
+        if i == 0:
+            x = sp.generate_vector(m, seed=22)
+            y_auto = run_plan(plan, x, m)
         plan.destroy()
-    with pytest.raises(sp.SpmvError, match="probe build"):
-        sp.Plan.from_csr(m, m, rp, col, val, fmt, placement="search")
+    plan = sp.Plan.from_csr(m, m, rp, col, val, fmt, placement="search")
+    info = plan.info()
+    assert info["placement"] == "search" and info["placement_candidates"] >= 1
+    assert 0 < info["placement_best_ms"] <= info["placement_worst_ms"]
+    assert np.array_equal(run_plan(plan, x, m), y_auto)
 
 
 def test_experiment_switches_do_not_reach_the_product_library(monkeypatch):
