@@ -207,6 +207,7 @@ struct SsDev {
     int kernel = 1;              // 1 = ss_stream_kernel, 0 = ss_tile_kernel (SIGMA <= 32)
     int pf = 2;                  // ss_stream_kernel: quads loaded ahead
     bool stage = true;           // ss_stream_kernel: finished rows staged in LDS, stored after the stream
+    int tpw = 4;                 // ss_run_kernel: tiles per wave
     int32_t *tile_ord = nullptr;
     double *head = nullptr;      // scratch [n_tiles]
     double *tail = nullptr;      // scratch [n_tiles]

@@ -286,6 +286,174 @@ __global__ __launch_bounds__(256) void ss_stream_kernel(
     }
 }
 
+// ss_run_kernel<SIGMA, PF, STAGE>: the tiles [t0, t0 + tpw) of one wave as ONE
+// stream.  Quad g of the wave (tile t0 + g / Q, quad g % Q) sits at
+// (t0 * Q + g) * 256 in the column array and likewise in the value halves, so
+// the wave's loads are a contiguous 1-KiB-per-instruction stream across its
+// tiles, kept PF quads deep (a quad is loaded right after the one PF earlier
+// is summed, into the register slot it frees: slot g % Q, statically indexed
+// because the tile loop is unrolled over Q).  Each tile's flags and first
+// ordinal are loaded one tile ahead; the per-tile scan, hand-off and y writes
+// are those of ss_tile_kernel (bit-identical y, same head / tail for
+// ss_fixup_kernel).  x: the wave's tiles' plan-time windows (SsDev::win) are
+// merged at the wave start; when all have one and their union spans fewer than
+// kSsWin columns, that union is staged once into the wave's LDS slice and
+// every tile reads x there, else x is gathered.
+template <int SIGMA, int PF, bool STAGE>
+__global__ __launch_bounds__(256) void ss_run_kernel(
+    int64_t n_tiles, int tpw, const int32_t *__restrict__ col, const double *__restrict__ val,
+    const uint32_t *__restrict__ flags, const int32_t *__restrict__ tile_ord, const int32_t *__restrict__ win,
+    const int32_t *__restrict__ nzrow, int64_t n_nonempty, const double *__restrict__ x, double *__restrict__ y,
+    double *__restrict__ head, double *__restrict__ tail, int32_t *__restrict__ tail_ord) {
+    static_assert(SIGMA % 4 == 0 && SIGMA <= 64, "sigma");
+    constexpr int Q = SIGMA / 4, W = SIGMA > 32 ? 2 : 1;
+    static_assert(PF >= 1 && PF <= Q, "prefetch depth");
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int64_t t0 = ((int64_t)blockIdx.x * 4 + wv) * tpw;
+    if (t0 >= n_tiles) return;  // wave-uniform
+    const int nt = (int)(n_tiles - t0 < tpw ? n_tiles - t0 : (int64_t)tpw);
+    // the wave's window candidates first: they are waited on before the stream
+    int32_t wlo = INT32_MAX, whi = -1, wok = 1;
+    if (lane < nt) {
+        const int32_t lo = win[2 * (t0 + lane)], len = win[2 * (t0 + lane) + 1];
+        wok = len > 0;
+        wlo = lo;
+        whi = lo + len - 1;
+    }
+    uint32_t f[W];
+#pragma unroll
+    for (int w = 0; w < W; ++w) f[w] = flags[(t0 * W + w) * 64 + lane];
+    int32_t ordb = tile_ord[t0];
+    const int32_t *cp = col + t0 * 64 * SIGMA + lane * 4;
+    const double *vp = val + t0 * 64 * SIGMA + lane * 2;
+    i32x4 c[Q];
+    f64x2 a[Q], b[Q];
+    auto load = [&](int slot, int64_t g) {
+        c[slot] = ld_stream4(cp + g * 256);
+        a[slot] = ld_stream2(vp + g * 256);
+        b[slot] = ld_stream2(vp + g * 256 + 128);
+    };
+#pragma unroll
+    for (int q = 0; q < PF; ++q) load(q, q);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        wlo = min(wlo, __shfl_xor(wlo, o, 64));
+        whi = max(whi, __shfl_xor(whi, o, 64));
+        wok = min(wok, __shfl_xor(wok, o, 64));
+    }
+    wlo = __builtin_amdgcn_readfirstlane(wlo);
+    whi = __builtin_amdgcn_readfirstlane(whi);
+    const bool xwin = __builtin_amdgcn_readfirstlane(wok) && whi - wlo < kSsWin;  // wave-uniform
+    __shared__ double xs[4][kSsWin];
+    if (xwin) {
+        for (int i = lane; i <= whi - wlo; i += 64) xs[wv][i] = ld_x(x, wlo + i);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    __shared__ double ys[STAGE ? 4 : 1][STAGE ? kSsStageRows : 1];
+
+    for (int it = 0; it < nt; ++it) {
+        const int64_t t = t0 + it;
+        const bool more = it + 1 < nt;  // wave-uniform
+        uint32_t fn[W];
+        int32_t ordn = 0;
+        if (more) {
+#pragma unroll
+            for (int w = 0; w < W; ++w) fn[w] = flags[((t + 1) * W + w) * 64 + lane];
+            ordn = tile_ord[t + 1];
+        }
+        int pc = 0;
+#pragma unroll
+        for (int w = 0; w < W; ++w) pc += __builtin_popcount(f[w]);
+        const int incl = wave_inclusive_sum(pc, lane);
+        const int total = __shfl(incl, 63, 64);
+        const bool stage = STAGE && total <= kSsStageRows;  // wave-uniform
+        const int64_t ord_base = ordb;
+        auto finish = [&](int rel, double v) {
+            if (STAGE && stage) ys[STAGE ? wv : 0][rel] = v;
+            else ss_store(y, nzrow, n_nonempty, ord_base + rel, v);
+        };
+        const int rel0 = incl - pc;
+        double run = 0.0, head_l = 0.0;
+        int seen = 0;
+        const int64_t gq = (int64_t)it * Q;  // the tile's first quad in the wave stream
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            __builtin_amdgcn_sched_barrier(0);
+            double g[4];
+            if (xwin) {
+                g[0] = xs[wv][c[q].x - wlo];
+                g[1] = xs[wv][c[q].y - wlo];
+                g[2] = xs[wv][c[q].z - wlo];
+                g[3] = xs[wv][c[q].w - wlo];
+            } else {
+                g[0] = ld_x(x, c[q].x);
+                g[1] = ld_x(x, c[q].y);
+                g[2] = ld_x(x, c[q].z);
+                g[3] = ld_x(x, c[q].w);
+            }
+            const double v[4] = {a[q].x, a[q].y, b[q].x, b[q].y};
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) {
+                const int k = 4 * q + kk;
+                if ((f[k >> 5] >> (k & 31)) & 1u) {
+                    if (seen == 0) head_l = run;
+                    else finish(rel0 + seen - 1, run);
+                    run = 0.0;
+                    ++seen;
+                }
+                run = madd(v[kk], g[kk], run);
+            }
+            // the slot just summed takes the quad PF ahead (this tile's or
+            // the next tile's)
+            if (q + PF < Q) load(q + PF, gq + q + PF);
+            else if (more) load(q + PF - Q, gq + q + PF);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+
+        const bool has = pc != 0;
+        const double S = wave_seg_scan(run, has, lane);
+        double C = __shfl_up(S, 1, 64);
+        if (lane == 0) C = 0.0;
+        const uint64_t ball = __ballot(has);
+        const bool started_before = (ball & ((1ull << lane) - 1ull)) != 0ull;
+        if (has) {
+            const double tot = __dadd_rn(C, head_l);
+            if (started_before) finish(rel0 - 1, tot);
+            else head[t] = tot;
+        }
+        if constexpr (STAGE) {
+            if (stage) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                for (int i = lane; i < total - 1; i += 64) ss_store(y, nzrow, n_nonempty, ord_base + i, ys[wv][i]);
+                // the slice is rewritten by the next tile: every lane's reads first
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
+        }
+        if (lane == 63) {
+            if (ball == 0ull) {
+                head[t] = S;
+                tail_ord[t] = -1;
+            } else {
+                tail[t] = S;
+                tail_ord[t] = (int32_t)(ord_base + incl - 1);
+            }
+        }
+        if (more) {
+#pragma unroll
+            for (int w = 0; w < W; ++w) f[w] = fn[w];
+            ordb = ordn;
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void ss_fixup_kernel(int64_t n_tiles, const double *__restrict__ head,
                                                        const double *__restrict__ tail,
                                                        const int32_t *__restrict__ tail_ord,
@@ -316,12 +484,12 @@ static void launch_ss_t(const spmv_plan_s *p, const double *x, double *y) {
     // loaded up front, window from the loaded columns, round 4), else the
     // streamed kernel with SPMV_LAUNCH_SS_PF quads ahead; SPMV_LAUNCH_SS_WIN=0
     // gathers x from memory always
-    int kind = SIGMA > 32 ? 1 : s.kernel, pf = s.pf;
+    int kind = SIGMA > 32 && s.kernel == 0 ? 1 : s.kernel, pf = s.pf;
     size_t lds = 0;  // dynamic LDS per workgroup: caps workgroups per CU (probe: SPMV_LAUNCH_SS_LDS_KB)
     bool win = true, stage = s.stage;
     if (const char *v = probe_env("SPMV_LAUNCH_SS_STAGE")) stage = std::atoi(v) != 0;
     if (const char *v = probe_env("SPMV_LAUNCH_SS_LDS_KB")) lds = (size_t)std::atoi(v) * 1024;
-    if (const char *v = probe_env("SPMV_LAUNCH_SS")) kind = SIGMA > 32 ? 1 : std::atoi(v);
+    if (const char *v = probe_env("SPMV_LAUNCH_SS")) kind = SIGMA > 32 && std::atoi(v) == 0 ? 1 : std::atoi(v);
     if (const char *v = probe_env("SPMV_LAUNCH_SS_PF")) pf = std::atoi(v);
     if (const char *v = probe_env("SPMV_LAUNCH_SS_WIN")) win = std::atoi(v) != 0;
     auto go = [&](auto kern, bool stream) {
@@ -342,6 +510,21 @@ static void launch_ss_t(const spmv_plan_s *p, const double *x, double *y) {
         return;
     }
     win = win && s.win;
+    if (kind == 2) {  // ss_run_kernel: tpw tiles per wave as one stream
+        int tpw = s.tpw;
+        if (const char *v = probe_env("SPMV_LAUNCH_SS_TPW")) tpw = std::atoi(v);
+        tpw = tpw < 1 ? 1 : (tpw > 64 ? 64 : tpw);
+        const int64_t waves = (s.n_tiles + tpw - 1) / tpw;
+        const unsigned rblocks = (unsigned)((waves + 3) / 4);
+        auto run = [&](auto kern) {
+            hipLaunchKernelGGL(kern, dim3(rblocks), dim3(256), lds, p->stream, s.n_tiles, tpw, s.col, s.val, s.flags,
+                               s.tile_ord, s.win, s.nzrow, s.n_nonempty, x, y, s.head, s.tail, s.tail_ord);
+        };
+        constexpr int P2 = SIGMA / 4 < 2 ? SIGMA / 4 : 2, P4 = SIGMA / 4 < 4 ? SIGMA / 4 : 4;
+        if (pf >= 4) stage ? run(ss_run_kernel<SIGMA, P4, true>) : run(ss_run_kernel<SIGMA, P4, false>);
+        else stage ? run(ss_run_kernel<SIGMA, P2, true>) : run(ss_run_kernel<SIGMA, P2, false>);
+        return;
+    }
     auto pick = [&](auto pfc) {
         constexpr int P = decltype(pfc)::value;
         if (stage) win ? go(ss_stream_kernel<SIGMA, true, P, true>, true) : go(ss_stream_kernel<SIGMA, false, P, true>, true);
