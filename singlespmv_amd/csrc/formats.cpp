@@ -747,9 +747,9 @@ int build_ss(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
     SPMV_RETURN_IF(upload(p, &s.flags, flags.data(), s.n_tiles * 64 * W));
     SPMV_RETURN_IF(upload(p, &s.tile_ord, tord.data(), s.n_tiles));
     SPMV_RETURN_IF(upload(p, &s.win, win.data(), 2 * s.n_tiles));
-    SPMV_RETURN_IF(dev_alloc(p, &s.head, s.n_tiles));
-    SPMV_RETURN_IF(dev_alloc(p, &s.tail, s.n_tiles));
+    SPMV_RETURN_IF(dev_alloc(p, &s.ht, 2 * s.n_tiles));
     SPMV_RETURN_IF(dev_alloc(p, &s.tail_ord, s.n_tiles));
+    SPMV_RETURN_IF(ss_plan_tail_ord(p));
     ss_finish_info(p);
     return SPMV_SUCCESS;
 }

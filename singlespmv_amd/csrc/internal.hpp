@@ -207,11 +207,9 @@ struct SsDev {
     int kernel = 1;              // 1 = ss_stream_kernel, 0 = ss_tile_kernel (SIGMA <= 32)
     int pf = 2;                  // ss_stream_kernel: quads loaded ahead
     bool stage = true;           // ss_stream_kernel: finished rows staged in LDS, stored after the stream
-    int tpw = 4;                 // ss_run_kernel: tiles per wave
     int32_t *tile_ord = nullptr;
-    double *head = nullptr;      // scratch [n_tiles]
-    double *tail = nullptr;      // scratch [n_tiles]
-    int32_t *tail_ord = nullptr; // scratch [n_tiles], -1 = no row starts in tile
+    double *ht = nullptr;        // scratch [n_tiles][2]: head partial, tail partial (one store per tile)
+    int32_t *tail_ord = nullptr; // [n_tiles] plan-time: ordinal of the tile's last row start, -1 = none
     int32_t *nzrow = nullptr;    // ordinal -> row (null when no empty rows)
     int64_t n_nonempty = 0;
     int32_t *empty_rows = nullptr;
@@ -504,6 +502,7 @@ int auto_ss_sigma(double mean_row);
 void ss_tile_windows(const int32_t *col, int64_t nnz, int64_t n_tiles, int sigma, std::vector<int32_t> &win);
 void ss_finish_info(spmv_plan_s *p);
 void ss_probe_options(SsDev &s);
+int ss_plan_tail_ord(spmv_plan_s *p);
 
 // end of one phase of a multi-kernel launch (no-op unless profiling)
 inline void phase_mark(const spmv_plan_s *p) {

@@ -406,12 +406,11 @@ int build_ss_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, c
     if (s.n_tiles > 0)
         hipLaunchKernelGGL(tile_windows, dim3((unsigned)((s.n_tiles + 3) / 4)), dim3(256), 0, st, d_col, nnz, s.sigma,
                            s.n_tiles, s.win);
-    SPMV_RETURN_IF(p->arena.alloc(&q, 8 * (size_t)std::max<int64_t>(s.n_tiles, 1)));
-    s.head = (double *)q;
-    SPMV_RETURN_IF(p->arena.alloc(&q, 8 * (size_t)std::max<int64_t>(s.n_tiles, 1)));
-    s.tail = (double *)q;
+    SPMV_RETURN_IF(p->arena.alloc(&q, 16 * (size_t)std::max<int64_t>(s.n_tiles, 1)));
+    s.ht = (double *)q;
     SPMV_RETURN_IF(p->arena.alloc(&q, 4 * (size_t)std::max<int64_t>(s.n_tiles, 1)));
     s.tail_ord = (int32_t *)q;
+    SPMV_RETURN_IF(ss_plan_tail_ord(p));
     hipError_t e = hipGetLastError();
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     if (e != hipSuccess) {

@@ -43,13 +43,78 @@ __device__ __forceinline__ void ss_store(double *y, const int32_t *nzrow, int64_
 
 constexpr int kSsWin = 512;  // x window per wave (doubles) of the WIN instance
 
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)b, l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+// The end of a tile, after the wave's segmented scan.  S: the lane's open
+// segment sum at its end; tot: a starting lane's finished first row (C + its
+// head run); ball: the lanes with a row start.  Lanes with a start after the
+// tile's first finished rows (tot) already; the rest leave here:
+//   head = tot of the first lane with a start (or the whole-tile S of lane 63
+//          when no row starts: the tile continues an earlier row),
+//   tail = S of lane 63 (the row still open at the tile end),
+//   and, when `nrows` finished rows wait in the wave's LDS slice `ys`, those.
+// All of them go out as ONE store instruction (lanes 0..nrows-1 the rows,
+// lane 62 the head, lane 63 the tail) when nrows <= 62: per-tile stores are
+// what backs up the TA data path under the load stream (config 4 PMC:
+// TA_DATA_STALLED_BY_TC 419 M cycles for 4 stores per tile, ELL 4.8 M,
+// profiles/round5/c4_ss_stalls).  The tail's ordinal is a plan constant
+// (SsDev::tail_ord), not stored here.
+__device__ __forceinline__ void ss_tile_end(int lane, int64_t tile, uint64_t ball, double tot, double S, int nrows,
+                                            const double *ys, int64_t ord_base, const int32_t *nzrow,
+                                            int64_t n_nonempty, double *y, double *ht, int mode = 0) {
+    const bool split = mode & 1;
+    const double s63 = readlane_f64(S, 63);
+    const double headv = ball ? readlane_f64(tot, (int)__builtin_ctzll(ball)) : s63;
+    if (split) {  // probe build (SPMV_LAUNCH_SS_SPLIT): round 4's separate store instructions
+        for (int i = lane; i < nrows; i += 64) ss_store(y, nzrow, n_nonempty, ord_base + i, ys[i]);
+        if (ball && lane == (int)__builtin_ctzll(ball)) ht[2 * tile] = tot;
+        if (lane == 63) {
+            if (!ball) ht[2 * tile] = S;
+            else ht[2 * tile + 1] = S;
+        }
+        if (lane == 63 && ball) __builtin_nontemporal_store(S, ht + 2 * tile + 1);  // stands for the tail_ord store
+        return;
+    }
+    int rem = nrows;
+    if (nrows > 62) {  // wide tile: the rows first, in whole waves
+        for (int i = lane; i < nrows; i += 64) ss_store(y, nzrow, n_nonempty, ord_base + i, ys[i]);
+        rem = 0;
+    }
+    if (mode & 128) rem = 0;  // probe: ablate the row stores (wrong y)
+    double *a = nullptr;
+    double v = 0.0;
+    if (lane < rem) {
+        const int64_t ord = ord_base + lane;
+        if (ord < n_nonempty) a = y + (nzrow ? (int64_t)nzrow[ord] : ord);
+        if (mode & 1024) a = ht + 2 * tile + 2 + lane;  // probe: the row bytes to scratch instead of y (wrong y)
+        v = ys[lane];
+    } else if ((mode & 256) && ball && lane == rem && rem < 62) {  // probe: provisional tail row in y
+        const int64_t ord = ord_base + rem;
+        if (ord < n_nonempty) a = y + (nzrow ? (int64_t)nzrow[ord] : ord);
+        v = s63;
+    } else if (lane == 62) {
+        a = ht + 2 * tile;
+        v = headv;
+    } else if (lane == 63 && ball) {
+        a = ht + 2 * tile + 1;
+        v = s63;
+    }
+    if (a) {
+        if (mode & 64) __builtin_nontemporal_store(v, a);  // probe: streamed-out stores
+        else *a = v;
+    }
+}
+
 template <int SIGMA, bool WIN>
 __global__ __launch_bounds__(256) void ss_tile_kernel(
     int64_t n_tiles, const int32_t *__restrict__ col, const double *__restrict__ val,
     const uint32_t *__restrict__ flags, const int32_t *__restrict__ tile_ord,
     const int32_t *__restrict__ nzrow, int64_t n_nonempty, const double *__restrict__ x,
-    double *__restrict__ y, double *__restrict__ head, double *__restrict__ tail,
-    int32_t *__restrict__ tail_ord) {
+    double *__restrict__ y, double *__restrict__ ht) {
     static_assert(SIGMA % 4 == 0 && SIGMA <= 32, "sigma");
     constexpr int Q = SIGMA / 4;
     const int64_t tile = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
@@ -139,20 +204,9 @@ __global__ __launch_bounds__(256) void ss_tile_kernel(
     if (lane == 0) C = 0.0;
     const uint64_t ball = __ballot(has);
     const bool started_before = (ball & ((1ull << lane) - 1ull)) != 0ull;
-    if (has) {
-        const double tot = __dadd_rn(C, head_l);
-        if (started_before) ss_store(y, nzrow, n_nonempty, ord0 - 1, tot);
-        else head[tile] = tot;  // exactly one lane: the first lane with a start
-    }
-    if (lane == 63) {
-        if (ball == 0ull) {
-            head[tile] = S;  // the whole tile continues an earlier row
-            tail_ord[tile] = -1;
-        } else {
-            tail[tile] = S;
-            tail_ord[tile] = tile_ord[tile] + incl - 1;
-        }
-    }
+    const double tot = __dadd_rn(C, head_l);
+    if (has && started_before) ss_store(y, nzrow, n_nonempty, ord0 - 1, tot);
+    ss_tile_end(lane, tile, ball, tot, S, 0, nullptr, 0, nzrow, n_nonempty, y, ht);
 }
 
 // ss_stream_kernel<SIGMA, WIN, PF>: the same tile, sums and hand-off as
@@ -170,11 +224,17 @@ __global__ __launch_bounds__(256) void ss_stream_kernel(
     int64_t n_tiles, const int32_t *__restrict__ col, const double *__restrict__ val,
     const uint32_t *__restrict__ flags, const int32_t *__restrict__ tile_ord, const int32_t *__restrict__ win,
     const int32_t *__restrict__ nzrow, int64_t n_nonempty, const double *__restrict__ x,
-    double *__restrict__ y, double *__restrict__ head, double *__restrict__ tail,
-    int32_t *__restrict__ tail_ord) {
+    double *__restrict__ y, double *__restrict__ ht, int dbg) {
     static_assert(SIGMA % 4 == 0 && SIGMA <= 64, "sigma");
     constexpr int Q = SIGMA / 4, W = SIGMA > 32 ? 2 : 1;
-    const int64_t tile = (int64_t)blockIdx.x * (blockDim.x / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    int64_t blk = blockIdx.x;
+#ifdef SPMV_PROBES
+    if (dbg & 32) {  // XCD-contiguous: workgroup b (XCD b % 8) takes block (b % 8) * (grid / 8) + b / 8
+        const unsigned per = gridDim.x / 8;
+        blk = (int64_t)(blockIdx.x % 8) * per + blockIdx.x / 8;
+    }
+#endif
+    const int64_t tile = blk * (blockDim.x / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (tile >= n_tiles) return;  // wave-uniform
     const int64_t base = tile * 64 * SIGMA;
@@ -192,6 +252,10 @@ __global__ __launch_bounds__(256) void ss_stream_kernel(
     uint32_t f[W];
 #pragma unroll
     for (int w = 0; w < W; ++w) f[w] = flags[(tile * W + w) * 64 + lane];
+#ifdef SPMV_PROBES
+    if (dbg & 8)  // ablate the row starts: no in-lane finishes
+        for (int w = 0; w < W; ++w) f[w] = 0u;
+#endif
     __shared__ double xs[4][kSsWin];
     const int wv = threadIdx.x >> 6;
     int32_t lo = 0, len = 0;
@@ -208,187 +272,45 @@ __global__ __launch_bounds__(256) void ss_stream_kernel(
     int pc = 0;
 #pragma unroll
     for (int w = 0; w < W; ++w) pc += __builtin_popcount(f[w]);
+#ifdef SPMV_PROBES
+    const int incl = (dbg & 4) ? pc * (lane + 1) : wave_inclusive_sum(pc, lane);  // 4: ablate the count scan
+#else
     const int incl = wave_inclusive_sum(pc, lane);
+#endif
     const int64_t ord_base = tile_ord[tile];  // rel ordinal r below = row ord_base + r
     // STAGE: the rows finished inside the tile (ordinals ord_base + [0,
-    // total - 1)) go to an LDS slice and leave as coalesced stores after the
-    // stream, so no y store sits between the tile's loads in the in-order
-    // vmcnt queue; tiles finishing more rows than the slice store directly
-    __shared__ double ys[STAGE ? 4 : 1][STAGE ? kSsStageRows : 1];
+    // total - 1)) go to the wave's LDS slice and leave in the tile's one store
+    // instruction (ss_tile_end); tiles finishing more rows than the slice
+    // holds store them directly.  Slice layout: [0] = rel -1 (a lane's head
+    // segment parks at rel0 - 1 until the scan), [1, kSsStageRows] = rel 0..,
+    // then one dump slot per lane.
+    __shared__ double ys[STAGE ? 4 : 1][STAGE ? kSsStageRows + 1 + 64 : 1];
     const int total = __shfl(incl, 63, 64);
     const bool stage = STAGE && total <= kSsStageRows;  // wave-uniform
-    auto finish = [&](int rel, double v) {
-        if (STAGE && stage) ys[STAGE ? wv : 0][rel] = v;
-        else ss_store(y, nzrow, n_nonempty, ord_base + rel, v);
-    };
+    double *yl = &ys[STAGE ? wv : 0][STAGE ? 1 : 0];
+    double *dump = &ys[STAGE ? wv : 0][STAGE ? kSsStageRows + 1 + lane : 0];
     const int rel0 = incl - pc;  // this lane's first start
 
     double run = 0.0, head_l = 0.0;
-    int seen = 0;
-#pragma unroll
-    for (int q = 0; q < Q; ++q) {
-        if (q + PF < Q) load(q + PF);
-        __builtin_amdgcn_sched_barrier(0);
-        double g[4];
-        if (WIN && len > 0) {
-            g[0] = xs[wv][c[q].x - lo];
-            g[1] = xs[wv][c[q].y - lo];
-            g[2] = xs[wv][c[q].z - lo];
-            g[3] = xs[wv][c[q].w - lo];
-        } else {
-            g[0] = ld_x(x, c[q].x);
-            g[1] = ld_x(x, c[q].y);
-            g[2] = ld_x(x, c[q].z);
-            g[3] = ld_x(x, c[q].w);
-        }
-        const double v[4] = {a[q].x, a[q].y, b[q].x, b[q].y};
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) {
-            const int k = 4 * q + kk;
-            if ((f[k >> 5] >> (k & 31)) & 1u) {
-                if (seen == 0) head_l = run;
-                else finish(rel0 + seen - 1, run);
-                run = 0.0;
-                ++seen;
-            }
-            run = madd(v[kk], g[kk], run);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-    }
-
-    const bool has = pc != 0;
-    const double S = wave_seg_scan(run, has, lane);  // open-segment sum at lane end
-    double C = __shfl_up(S, 1, 64);
-    if (lane == 0) C = 0.0;
-    const uint64_t ball = __ballot(has);
-    const bool started_before = (ball & ((1ull << lane) - 1ull)) != 0ull;
-    if (has) {
-        const double tot = __dadd_rn(C, head_l);
-        if (started_before) finish(rel0 - 1, tot);
-        else head[tile] = tot;  // exactly one lane: the first lane with a start
-    }
-    if constexpr (STAGE) {
-        if (stage) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            for (int i = lane; i < total - 1; i += 64) ss_store(y, nzrow, n_nonempty, ord_base + i, ys[wv][i]);
-        }
-    }
-    if (lane == 63) {
-        if (ball == 0ull) {
-            head[tile] = S;  // the whole tile continues an earlier row
-            tail_ord[tile] = -1;
-        } else {
-            tail[tile] = S;
-            tail_ord[tile] = (int32_t)(ord_base + incl - 1);
-        }
-    }
-}
-
-// ss_run_kernel<SIGMA, PF, STAGE>: the tiles [t0, t0 + tpw) of one wave as ONE
-// stream.  Quad g of the wave (tile t0 + g / Q, quad g % Q) sits at
-// (t0 * Q + g) * 256 in the column array and likewise in the value halves, so
-// the wave's loads are a contiguous 1-KiB-per-instruction stream across its
-// tiles, kept PF quads deep (a quad is loaded right after the one PF earlier
-// is summed, into the register slot it frees: slot g % Q, statically indexed
-// because the tile loop is unrolled over Q).  Each tile's flags and first
-// ordinal are loaded one tile ahead; the per-tile scan, hand-off and y writes
-// are those of ss_tile_kernel (bit-identical y, same head / tail for
-// ss_fixup_kernel).  x: the wave's tiles' plan-time windows (SsDev::win) are
-// merged at the wave start; when all have one and their union spans fewer than
-// kSsWin columns, that union is staged once into the wave's LDS slice and
-// every tile reads x there, else x is gathered.
-template <int SIGMA, int PF, bool STAGE>
-__global__ __launch_bounds__(256) void ss_run_kernel(
-    int64_t n_tiles, int tpw, const int32_t *__restrict__ col, const double *__restrict__ val,
-    const uint32_t *__restrict__ flags, const int32_t *__restrict__ tile_ord, const int32_t *__restrict__ win,
-    const int32_t *__restrict__ nzrow, int64_t n_nonempty, const double *__restrict__ x, double *__restrict__ y,
-    double *__restrict__ head, double *__restrict__ tail, int32_t *__restrict__ tail_ord) {
-    static_assert(SIGMA % 4 == 0 && SIGMA <= 64, "sigma");
-    constexpr int Q = SIGMA / 4, W = SIGMA > 32 ? 2 : 1;
-    static_assert(PF >= 1 && PF <= Q, "prefetch depth");
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    const int64_t t0 = ((int64_t)blockIdx.x * 4 + wv) * tpw;
-    if (t0 >= n_tiles) return;  // wave-uniform
-    const int nt = (int)(n_tiles - t0 < tpw ? n_tiles - t0 : (int64_t)tpw);
-    // the wave's window candidates first: they are waited on before the stream
-    int32_t wlo = INT32_MAX, whi = -1, wok = 1;
-    if (lane < nt) {
-        const int32_t lo = win[2 * (t0 + lane)], len = win[2 * (t0 + lane) + 1];
-        wok = len > 0;
-        wlo = lo;
-        whi = lo + len - 1;
-    }
-    uint32_t f[W];
-#pragma unroll
-    for (int w = 0; w < W; ++w) f[w] = flags[(t0 * W + w) * 64 + lane];
-    int32_t ordb = tile_ord[t0];
-    const int32_t *cp = col + t0 * 64 * SIGMA + lane * 4;
-    const double *vp = val + t0 * 64 * SIGMA + lane * 2;
-    i32x4 c[Q];
-    f64x2 a[Q], b[Q];
-    auto load = [&](int slot, int64_t g) {
-        c[slot] = ld_stream4(cp + g * 256);
-        a[slot] = ld_stream2(vp + g * 256);
-        b[slot] = ld_stream2(vp + g * 256 + 128);
-    };
-#pragma unroll
-    for (int q = 0; q < PF; ++q) load(q, q);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        wlo = min(wlo, __shfl_xor(wlo, o, 64));
-        whi = max(whi, __shfl_xor(whi, o, 64));
-        wok = min(wok, __shfl_xor(wok, o, 64));
-    }
-    wlo = __builtin_amdgcn_readfirstlane(wlo);
-    whi = __builtin_amdgcn_readfirstlane(whi);
-    const bool xwin = __builtin_amdgcn_readfirstlane(wok) && whi - wlo < kSsWin;  // wave-uniform
-    __shared__ double xs[4][kSsWin];
-    if (xwin) {
-        for (int i = lane; i <= whi - wlo; i += 64) xs[wv][i] = ld_x(x, wlo + i);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
-    __shared__ double ys[STAGE ? 4 : 1][STAGE ? kSsStageRows : 1];
-
-    for (int it = 0; it < nt; ++it) {
-        const int64_t t = t0 + it;
-        const bool more = it + 1 < nt;  // wave-uniform
-        uint32_t fn[W];
-        int32_t ordn = 0;
-        if (more) {
-#pragma unroll
-            for (int w = 0; w < W; ++w) fn[w] = flags[((t + 1) * W + w) * 64 + lane];
-            ordn = tile_ord[t + 1];
-        }
-        int pc = 0;
-#pragma unroll
-        for (int w = 0; w < W; ++w) pc += __builtin_popcount(f[w]);
-        const int incl = wave_inclusive_sum(pc, lane);
-        const int total = __shfl(incl, 63, 64);
-        const bool stage = STAGE && total <= kSsStageRows;  // wave-uniform
-        const int64_t ord_base = ordb;
-        auto finish = [&](int rel, double v) {
-            if (STAGE && stage) ys[STAGE ? wv : 0][rel] = v;
-            else ss_store(y, nzrow, n_nonempty, ord_base + rel, v);
-        };
-        const int rel0 = incl - pc;
-        double run = 0.0, head_l = 0.0;
-        int seen = 0;
-        const int64_t gq = (int64_t)it * Q;  // the tile's first quad in the wave stream
+    auto sum_tile = [&](auto fastc) {
+        // FAST (staged tiles): branch-free -- at every entry the run so far
+        // is written to LDS, to the slot of the segment it closes when the
+        // entry starts a row (its head segment to rel0 - 1, then rel0, ...)
+        // and to the lane's dump slot otherwise, then reset by a select.
+        // Same additions in the same order as the branchy form below (which
+        // the direct-store tiles keep): bit-identical.
+        constexpr bool FAST = decltype(fastc)::value;
+        int seen = 0, sl = rel0 - 1;
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
+            if (q + PF < Q) load(q + PF);
             __builtin_amdgcn_sched_barrier(0);
             double g[4];
-            if (xwin) {
-                g[0] = xs[wv][c[q].x - wlo];
-                g[1] = xs[wv][c[q].y - wlo];
-                g[2] = xs[wv][c[q].z - wlo];
-                g[3] = xs[wv][c[q].w - wlo];
+            if (WIN && len > 0) {
+                g[0] = xs[wv][c[q].x - lo];
+                g[1] = xs[wv][c[q].y - lo];
+                g[2] = xs[wv][c[q].z - lo];
+                g[3] = xs[wv][c[q].w - lo];
             } else {
                 g[0] = ld_x(x, c[q].x);
                 g[1] = ld_x(x, c[q].y);
@@ -399,63 +321,57 @@ __global__ __launch_bounds__(256) void ss_run_kernel(
 #pragma unroll
             for (int kk = 0; kk < 4; ++kk) {
                 const int k = 4 * q + kk;
-                if ((f[k >> 5] >> (k & 31)) & 1u) {
+                const bool st = (f[k >> 5] >> (k & 31)) & 1u;
+                if constexpr (FAST) {
+                    *(st ? yl + sl : dump) = run;
+                    run = st ? 0.0 : run;
+                    sl += st ? 1 : 0;
+                } else if (st) {
                     if (seen == 0) head_l = run;
-                    else finish(rel0 + seen - 1, run);
+                    else ss_store(y, nzrow, n_nonempty, ord_base + rel0 + seen - 1, run);
                     run = 0.0;
                     ++seen;
                 }
                 run = madd(v[kk], g[kk], run);
             }
-            // the slot just summed takes the quad PF ahead (this tile's or
-            // the next tile's)
-            if (q + PF < Q) load(q + PF, gq + q + PF);
-            else if (more) load(q + PF - Q, gq + q + PF);
             __builtin_amdgcn_sched_barrier(0);
         }
+        if constexpr (FAST) head_l = pc ? yl[rel0 - 1] : 0.0;
+    };
+    if (stage) sum_tile(std::true_type{});
+    else sum_tile(std::false_type{});
 
-        const bool has = pc != 0;
-        const double S = wave_seg_scan(run, has, lane);
-        double C = __shfl_up(S, 1, 64);
-        if (lane == 0) C = 0.0;
-        const uint64_t ball = __ballot(has);
-        const bool started_before = (ball & ((1ull << lane) - 1ull)) != 0ull;
-        if (has) {
-            const double tot = __dadd_rn(C, head_l);
-            if (started_before) finish(rel0 - 1, tot);
-            else head[t] = tot;
-        }
-        if constexpr (STAGE) {
-            if (stage) {
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                for (int i = lane; i < total - 1; i += 64) ss_store(y, nzrow, n_nonempty, ord_base + i, ys[wv][i]);
-                // the slice is rewritten by the next tile: every lane's reads first
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            }
-        }
-        if (lane == 63) {
-            if (ball == 0ull) {
-                head[t] = S;
-                tail_ord[t] = -1;
-            } else {
-                tail[t] = S;
-                tail_ord[t] = (int32_t)(ord_base + incl - 1);
-            }
-        }
-        if (more) {
-#pragma unroll
-            for (int w = 0; w < W; ++w) f[w] = fn[w];
-            ordb = ordn;
+    const bool has = pc != 0;
+#ifdef SPMV_PROBES
+    const double S = (dbg & 2) ? run : wave_seg_scan(run, has, lane);  // 2: ablate the value scan
+#else
+    const double S = wave_seg_scan(run, has, lane);  // open-segment sum at lane end
+#endif
+    double C = __shfl_up(S, 1, 64);
+    if (lane == 0) C = 0.0;
+    const uint64_t ball = __ballot(has);
+    const bool started_before = (ball & ((1ull << lane) - 1ull)) != 0ull;
+    const double tot = __dadd_rn(C, head_l);
+    if (has && started_before) {
+        if (stage) yl[rel0 - 1] = tot;
+        else ss_store(y, nzrow, n_nonempty, ord_base + rel0 - 1, tot);
+    }
+    if constexpr (STAGE) {
+        if (stage) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
     }
+#ifdef SPMV_PROBES
+    const int split = dbg;
+#else
+    constexpr int split = 0;
+#endif
+    ss_tile_end(lane, tile, ball, tot, S, stage ? total - 1 : 0, yl, ord_base, nzrow, n_nonempty, y, ht, split);
 }
 
-__global__ __launch_bounds__(256) void ss_fixup_kernel(int64_t n_tiles, const double *__restrict__ head,
-                                                       const double *__restrict__ tail,
+__global__ __launch_bounds__(256) void ss_fixup_kernel(int64_t n_tiles, const double *__restrict__ ht,
                                                        const int32_t *__restrict__ tail_ord,
                                                        const int32_t *__restrict__ nzrow,
                                                        int64_t n_nonempty,
@@ -465,9 +381,9 @@ __global__ __launch_bounds__(256) void ss_fixup_kernel(int64_t n_tiles, const do
     if (t < n_tiles) {
         const int32_t ord = tail_ord[t];
         if (ord >= 0 && ord < n_nonempty) {
-            double s = tail[t];
+            double s = ht[2 * t + 1];
             for (int64_t u = t + 1; u < n_tiles; ++u) {
-                s = __dadd_rn(s, head[u]);
+                s = __dadd_rn(s, ht[2 * u]);
                 if (tail_ord[u] >= 0) break;
             }
             y[nzrow ? (int64_t)nzrow[ord] : (int64_t)ord] = s;
@@ -476,10 +392,38 @@ __global__ __launch_bounds__(256) void ss_fixup_kernel(int64_t n_tiles, const do
     if (t < n_empty) y[empty_rows[t]] = 0.0;
 }
 
+// plan time: tail_ord[t] = ordinal of tile t's last row start (its first
+// start's ordinal tile_ord[t] + the tile's flag count - 1; the dummy start
+// over the padding counts, as the tile kernels count it), -1 when no row
+// starts in the tile.  One wave per tile.
+__global__ __launch_bounds__(256) void ss_tail_ord_kernel(int64_t n_tiles, int words,
+                                                          const uint32_t *__restrict__ flags,
+                                                          const int32_t *__restrict__ tile_ord,
+                                                          int32_t *__restrict__ tail_ord) {
+    const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (t >= n_tiles) return;
+    int pc = 0;
+    for (int w = 0; w < words; ++w) pc += __builtin_popcount(flags[(t * words + w) * 64 + lane]);
+    for (int o = 32; o > 0; o >>= 1) pc += __shfl_xor(pc, o, 64);
+    if (lane == 0) tail_ord[t] = pc ? tile_ord[t] + pc - 1 : -1;
+}
+
+int ss_plan_tail_ord(spmv_plan_s *p) {
+    const SsDev &s = p->ss;
+    if (s.n_tiles > 0) {
+        hipLaunchKernelGGL(ss_tail_ord_kernel, dim3((unsigned)((s.n_tiles + 3) / 4)), dim3(256), 0, p->stream,
+                           s.n_tiles, ss_flag_words(s.sigma), s.flags, s.tile_ord, s.tail_ord);
+        SPMV_HIP_TRY(hipGetLastError());
+        SPMV_HIP_TRY(hipStreamSynchronize(p->stream));  // executes may run on another stream
+    }
+    return SPMV_SUCCESS;
+}
+
 template <int SIGMA>
 static void launch_ss_t(const spmv_plan_s *p, const double *x, double *y) {
     const SsDev &s = p->ss;
-    const int64_t blocks = (s.n_tiles + 3) / 4;
+    int64_t blocks = (s.n_tiles + 3) / 4;
     // probe build: SPMV_LAUNCH_SS = 0 -> ss_tile_kernel (all SIGMA entries
     // loaded up front, window from the loaded columns, round 4), else the
     // streamed kernel with SPMV_LAUNCH_SS_PF quads ahead; SPMV_LAUNCH_SS_WIN=0
@@ -492,39 +436,25 @@ static void launch_ss_t(const spmv_plan_s *p, const double *x, double *y) {
     if (const char *v = probe_env("SPMV_LAUNCH_SS")) kind = SIGMA > 32 && std::atoi(v) == 0 ? 1 : std::atoi(v);
     if (const char *v = probe_env("SPMV_LAUNCH_SS_PF")) pf = std::atoi(v);
     if (const char *v = probe_env("SPMV_LAUNCH_SS_WIN")) win = std::atoi(v) != 0;
+    int dbg = 0;  // probe build: SPMV_LAUNCH_SS_SPLIT=1 -> separate per-tile store instructions (round 4)
+    if (const char *v = probe_env("SPMV_LAUNCH_SS_SPLIT")) dbg = std::atoi(v);  // bits 2, 4, 8: ablations (wrong y)
+    if (dbg & 32) blocks = (blocks + 7) / 8 * 8;  // XCD-contiguous mapping: a whole number of blocks per XCD
     auto go = [&](auto kern, bool stream) {
         if (stream)
             hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), lds, p->stream, s.n_tiles, s.col, s.val, s.flags,
-                               s.tile_ord, s.win, s.nzrow, s.n_nonempty, x, y, s.head, s.tail, s.tail_ord);
+                               s.tile_ord, s.win, s.nzrow, s.n_nonempty, x, y, s.ht, dbg);
     };
     if (kind == 0 && SIGMA <= 32) {
         constexpr int S0 = SIGMA <= 32 ? SIGMA : 32;
         if (win)
             hipLaunchKernelGGL((ss_tile_kernel<S0, true>), dim3((unsigned)blocks), dim3(256), lds, p->stream,
-                               s.n_tiles, s.col, s.val, s.flags, s.tile_ord, s.nzrow, s.n_nonempty, x, y,
-                               s.head, s.tail, s.tail_ord);
+                               s.n_tiles, s.col, s.val, s.flags, s.tile_ord, s.nzrow, s.n_nonempty, x, y, s.ht);
         else
             hipLaunchKernelGGL((ss_tile_kernel<S0, false>), dim3((unsigned)blocks), dim3(256), lds, p->stream,
-                               s.n_tiles, s.col, s.val, s.flags, s.tile_ord, s.nzrow, s.n_nonempty, x, y,
-                               s.head, s.tail, s.tail_ord);
+                               s.n_tiles, s.col, s.val, s.flags, s.tile_ord, s.nzrow, s.n_nonempty, x, y, s.ht);
         return;
     }
     win = win && s.win;
-    if (kind == 2) {  // ss_run_kernel: tpw tiles per wave as one stream
-        int tpw = s.tpw;
-        if (const char *v = probe_env("SPMV_LAUNCH_SS_TPW")) tpw = std::atoi(v);
-        tpw = tpw < 1 ? 1 : (tpw > 64 ? 64 : tpw);
-        const int64_t waves = (s.n_tiles + tpw - 1) / tpw;
-        const unsigned rblocks = (unsigned)((waves + 3) / 4);
-        auto run = [&](auto kern) {
-            hipLaunchKernelGGL(kern, dim3(rblocks), dim3(256), lds, p->stream, s.n_tiles, tpw, s.col, s.val, s.flags,
-                               s.tile_ord, s.win, s.nzrow, s.n_nonempty, x, y, s.head, s.tail, s.tail_ord);
-        };
-        constexpr int P2 = SIGMA / 4 < 2 ? SIGMA / 4 : 2, P4 = SIGMA / 4 < 4 ? SIGMA / 4 : 4;
-        if (pf >= 4) stage ? run(ss_run_kernel<SIGMA, P4, true>) : run(ss_run_kernel<SIGMA, P4, false>);
-        else stage ? run(ss_run_kernel<SIGMA, P2, true>) : run(ss_run_kernel<SIGMA, P2, false>);
-        return;
-    }
     auto pick = [&](auto pfc) {
         constexpr int P = decltype(pfc)::value;
         if (stage) win ? go(ss_stream_kernel<SIGMA, true, P, true>, true) : go(ss_stream_kernel<SIGMA, false, P, true>, true);
@@ -558,7 +488,7 @@ int launch_ss(const spmv_plan_s *p, const double *x, double *y) {
     const int64_t work = s.n_tiles > s.n_empty ? s.n_tiles : s.n_empty;
     if (work > 0) {
         hipLaunchKernelGGL(ss_fixup_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0,
-                           p->stream, s.n_tiles, s.head, s.tail, s.tail_ord, s.nzrow, s.n_nonempty,
+                           p->stream, s.n_tiles, s.ht, s.tail_ord, s.nzrow, s.n_nonempty,
                            s.empty_rows, s.n_empty, y);
         SPMV_HIP_TRY(hipGetLastError());
     }
