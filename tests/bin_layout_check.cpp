@@ -24,6 +24,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <cstdlib>
 #include <random>
 
 using namespace spmv;
@@ -192,10 +193,11 @@ static int emulate(const BinDev &B, const HostCsr &A, const BinLayout &L, const 
     return 0;
 }
 
-int main() {
+int main(int argc, char **argv) {
     std::mt19937_64 rng(7);
     int cases = 0;
-    for (int trial = 0; trial < 60; ++trial) {
+    const int trials = argc > 1 ? std::atoi(argv[1]) : 60;  // the ASan run takes fewer (tests/test_guards.py)
+    for (int trial = 0; trial < trials; ++trial) {
         const int64_t m = 1 + (int64_t)(rng() % 60000), n = 1 + (int64_t)(rng() % 300000);
         const int kind = trial % 3;  // uniform short rows / long rows / many empty rows
         std::vector<int64_t> rp(m + 1, 0);

@@ -213,7 +213,9 @@ def test_host_code_under_asan_ubsan():
     host/oracle test files clean."""
     subprocess.check_call(["make", "-s", "-j8", "asan"], cwd=ROOT)
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:verify_asan_link_order=0", UBSAN_OPTIONS="halt_on_error=1")
-    out = subprocess.run([os.path.join(ROOT, "build", "asan", "bin_layout_check")], env=env, capture_output=True,
+    # 12 of the plain run's 60 random matrices (4 of each kind): the plain
+    # build checks all 60 (tests/test_bin_layout.py)
+    out = subprocess.run([os.path.join(ROOT, "build", "asan", "bin_layout_check"), "12"], env=env, capture_output=True,
                          text=True, timeout=600)
     assert out.returncode == 0 and out.stdout.startswith("ok"), out.stderr[-3000:]
     rt = subprocess.check_output(["/opt/rocm/bin/hipcc", "-print-file-name=libclang_rt.asan-x86_64.so"], text=True).strip()
