@@ -202,10 +202,19 @@ def test_csr_window_kernel_small_shapes(m, n, lanes):
 
 
 @pytest.mark.parametrize("sigma", [4, 8, 12, 16, 20, 24, 32, 48, 64])
-@pytest.mark.parametrize("kind", ["powerlaw", "uniform", "empty_rows", "banded"])
+@pytest.mark.parametrize("kind", ["powerlaw", "uniform", "empty_rows", "banded", "short"])
 def test_ss_sigma(sigma, kind):
     m = 30011
-    if kind == "empty_rows":
+    if kind == "short":
+        # rows of 0-3 entries: a tile finishes 64-4096 rows, so every tile-end
+        # path runs -- rows in the one store instruction (<= 62), in whole
+        # waves (63-256, staged) and stored directly (> 256)
+        rng = np.random.default_rng(100 + sigma)
+        lens = rng.integers(0, 4, m)
+        rp = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+        col = np.concatenate([np.sort(rng.choice(m, int(k), replace=False)) for k in lens]).astype(np.int32)
+        val = rng.standard_normal(int(rp[-1]))
+    elif kind == "empty_rows":
         spec = sp.gen_spec("powerlaw", m, max_len=500, seed=13)
         rp, col, val = sp.generate_csr(spec)
         rng = np.random.default_rng(sigma)
