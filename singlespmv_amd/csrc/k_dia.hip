@@ -96,7 +96,10 @@ __global__ __launch_bounds__(256) void dia_kernel(int64_t m, int64_t mp, int64_t
     }
     // y is written once and not re-read: the row pair as one 16-byte
     // nontemporal store where y is 16-byte aligned (r is even)
-    if constexpr (YMODE == 2) return;  // probe: y store ablated (wrong y)
+    if constexpr (YMODE == 2) {  // probe: y store ablated (wrong y); the sums stay live
+        if (acc0 + acc1 == -0x1.23456789p+1000) y[r] = acc0;
+        return;
+    }
     if (r + 1 < m && (reinterpret_cast<uintptr_t>(y) & 15) == 0) {
         f64x2 yv;
         yv.x = acc0;
