@@ -55,9 +55,10 @@ extern "C" {
  * fields, round 2) and spmv_plan_info_t: a caller built against a version-1
  * header passes structs of the wrong size and must be rebuilt.  Version 3
  * (round 3) took bin_product_order from spmv_options_t's reserved words (same
- * size) and appended bin_sum_entries to spmv_plan_info_t.  crs_exact (round
- * 5) took one more reserved word: same size, and 0 (spmv_options_default)
- * keeps the version-3 behaviour.  Callers may
+ * size) and appended bin_sum_entries to spmv_plan_info_t.  crs_exact and build
+ * (round 5) took the last reserved words: same size, and 0
+ * (spmv_options_default) keeps the version-3 results (build = AUTO moves only
+ * where the layout is made, not what it is).  Callers may
  * check spmv_api_version() == SPMV_HIP_API_VERSION once at startup; the
  * structs are only ever filled by spmv_options_default / spmv_plan_info of a
  * library with the same version. */
@@ -129,8 +130,24 @@ typedef struct spmv_options {
                                 one lane per row; spmv_plan_info reports the
                                 layout.  0 = the CSR kernels as configured
                                 (row groups of L lanes: butterfly sums)       */
-    int32_t reserved[1];
+    int32_t build;           /* plan builders (SPMV_BUILD_*): AUTO = a host CSR of
+                                >= 2^24 entries is staged into HBM and built by
+                                the device builders (every format but CSS;
+                                byte-identical layouts, spmv_plan_digest), when
+                                the staging copy fits in device memory;
+                                smaller ones, CSS, and AUTO / BIN / crs_exact
+                                requests with a row whose columns decrease take
+                                the host builders */
 } spmv_options_t;
+
+/* Where spmv_plan_create_csr / _csr32 / _coo build the layout. */
+typedef enum spmv_build {
+    SPMV_BUILD_AUTO = 0,
+    SPMV_BUILD_HOST = 1,    /* host builders (formats.cpp, build_bin.cpp)       */
+    SPMV_BUILD_DEVICE = 2   /* stage the CSR into HBM and build there whatever
+                               the size (CSS and unsorted BIN requests still
+                               take the host builders)                         */
+} spmv_build_t;
 
 /* Placement of the large buffers of a plan (the BIN product buffer, the DIA
  * values, the streamed col / val arrays of CSR, ELL, HYB, JDS, SS, COO, CSS).  The BIN Mul ran ~15 % slower with one
@@ -372,6 +389,11 @@ int spmv_plan_info(spmv_plan_t plan, spmv_plan_info_t *info);
  * return SPMV_ERROR_NOT_SUPPORTED. */
 int spmv_plan_digest(spmv_plan_t plan, uint64_t *digests, int32_t cap, int32_t *n_arrays);
 const char *spmv_plan_digest_name(spmv_plan_t plan, int32_t k);
+
+/* *on_device = 1 when the plan's layout was built in HBM (by
+ * spmv_plan_create_csr_device, or from a host CSR under
+ * spmv_options_t::build), 0 when by the host builders. */
+int spmv_plan_built_on_device(spmv_plan_t plan, int32_t *on_device);
 
 const char *spmv_status_string(int status);
 /* Detail of the last failure on the calling thread ("" if none). */

@@ -59,10 +59,11 @@ class Options(C.Structure):
                 ("css_pace", C.c_int32), ("bin_strip_cols", C.c_int32), ("bin_groups", C.c_int32),
                 ("bin_sum_waves", C.c_int32), ("bin_pad", C.c_int32), ("csr_row_ptr64", C.c_int32),
                 ("placement", C.c_int32), ("bin_long_len", C.c_int32), ("bin_product_order", C.c_int32),
-                ("crs_exact", C.c_int32), ("reserved", C.c_int32 * 1)]
+                ("crs_exact", C.c_int32), ("build", C.c_int32)]
 
 
 PLACEMENTS = {"auto": 0, "plain": 1, "search": 2, "vmm": 3}
+BUILDS = {"auto": 0, "host": 1, "device": 2}
 
 
 class PlanInfo(C.Structure):
@@ -107,7 +108,7 @@ EXPORTS = [
     "spmv_dist_execute", "spmv_dist_time", "spmv_dist_info", "spmv_dist_destroy", "spmv_stream_write_probe",
     "spmv_mixed_probe", "spmv_graph_create", "spmv_graph_launch", "spmv_graph_time", "spmv_graph_destroy",
     "spmv_plan_digest", "spmv_plan_digest_name", "spmv_dist_shard", "spmv_dist_assemble",
-    "spmv_fetch_y", "spmv_dist_fetch_y",
+    "spmv_fetch_y", "spmv_dist_fetch_y", "spmv_plan_built_on_device",
 ]
 
 _lib = None
@@ -168,6 +169,7 @@ def lib():
     L.spmv_phase_name.restype = C.c_char_p
     L.spmv_plan_info.argtypes = [vp, C.POINTER(PlanInfo)]
     L.spmv_plan_digest.argtypes = [vp, C.POINTER(C.c_uint64), i32, C.POINTER(i32)]
+    L.spmv_plan_built_on_device.argtypes = [vp, C.POINTER(i32)]
     L.spmv_plan_digest_name.argtypes = [vp, i32]
     L.spmv_plan_digest_name.restype = C.c_char_p
     L.spmv_status_string.argtypes = [C.c_int]
@@ -375,7 +377,8 @@ def make_options(fmt="auto", device: int = -1, csr_lanes: int = 0, ell_width: in
                  css_slab_shift: int = 0, css_lag: int = 0, css_pace: int = 0,
                  bin_strip_cols: int = 0, bin_groups: int = 0, bin_sum_waves: int = 0,
                  bin_pad: int = 0, csr_row_ptr64: bool = False, placement="auto",
-                 bin_long_len: int = 0, bin_product_order: int = 0, crs_exact: bool = False) -> Options:
+                 bin_long_len: int = 0, bin_product_order: int = 0, crs_exact: bool = False,
+                 build="auto") -> Options:
     o = Options()
     lib().spmv_options_default(C.byref(o))
     o.format = FORMATS[fmt] if isinstance(fmt, str) else int(fmt)
@@ -388,6 +391,7 @@ def make_options(fmt="auto", device: int = -1, csr_lanes: int = 0, ell_width: in
     o.bin_long_len = bin_long_len
     o.bin_product_order = bin_product_order
     o.crs_exact = 1 if crs_exact else 0
+    o.build = BUILDS[build] if isinstance(build, str) else int(build)
     return o
 
 
@@ -574,6 +578,12 @@ class Plan:
         i = PlanInfo()
         _check(lib().spmv_plan_info(self._h, C.byref(i)), "spmv_plan_info")
         return i.as_dict()
+
+    def built_on_device(self) -> bool:
+        """True when the layout was built in HBM (spmv_plan_built_on_device)."""
+        v = C.c_int32()
+        _check(lib().spmv_plan_built_on_device(self._h, C.byref(v)), "spmv_plan_built_on_device")
+        return bool(v.value)
 
     def digest(self) -> dict:
         """{array name: 64-bit layout digest} (spmv_plan_digest): equal dicts

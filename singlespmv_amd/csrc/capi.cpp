@@ -71,126 +71,23 @@ static int validate_csr(const HostCsr &A) {
     return SPMV_SUCCESS;
 }
 
-static int create_from_csr(const HostCsr &A, const spmv_options_t *opt_in, spmv_plan_t *out) {
-    SPMV_CHECK_ARG(out != nullptr, "plan out-pointer is NULL");
-    *out = nullptr;
-    spmv_options_t o;
-    if (opt_in) o = *opt_in;
-    else spmv_options_default(&o);
-    SPMV_RETURN_IF(validate_csr(A));
-    int count = 0;
-    if (hipGetDeviceCount(&count) != hipSuccess || count == 0) {
-        (void)hipGetLastError();
-        set_error("no HIP device visible (libspmv_hip needs an MI355X / gfx950)");
-        return SPMV_ERROR_NO_DEVICE;
-    }
-    int dev = o.device;
-    if (dev < 0) SPMV_HIP_TRY(hipGetDevice(&dev));
-    SPMV_RETURN_IF(check_device(dev));
-    SPMV_HIP_TRY(hipSetDevice(dev));
-    spmv_plan_s *p = new (std::nothrow) spmv_plan_s;
-    if (!p) {
-        set_error("host allocation of the plan failed");
-        return SPMV_ERROR_OUT_OF_MEMORY;
-    }
-    p->device = dev;
-    p->arena.device = dev;
-    if (const char *e = probe_env("SPMV_ARENA_VMM_MB")) p->arena.vmm_min = (size_t)std::max(0, std::atoi(e)) << 20;
-    p->m = A.m;
-    p->n = A.n;
-    p->nnz = A.nnz;
-    int fmt = o.format == SPMV_FORMAT_AUTO ? choose_format(A, o) : o.format;
-    if (fmt == SPMV_FORMAT_CSR && o.crs_exact) fmt = choose_crs_exact(A, o);
-    stream_placement(p, fmt, o);
-    int st;
-    switch (fmt) {
-        case SPMV_FORMAT_CSR: st = build_csr(p, A, o); break;
-        case SPMV_FORMAT_ELL: st = build_ell(p, A, o, INT32_MAX); break;
-        case SPMV_FORMAT_HYB: st = build_hyb(p, A, o); break;
-        case SPMV_FORMAT_SS: st = build_ss(p, A, o); break;
-        case SPMV_FORMAT_DIA: st = build_dia(p, A, o); break;
-        case SPMV_FORMAT_CSS: st = build_css(p, A, o); break;
-        case SPMV_FORMAT_COO: st = build_coo(p, A, o); break;
-        case SPMV_FORMAT_JDS: st = build_jds(p, A, o); break;
-        case SPMV_FORMAT_BIN: st = build_bin(p, A, o); break;
-        default:
-            set_error("unknown format");
-            st = SPMV_ERROR_INVALID_VALUE;
-    }
-    if (st != SPMV_SUCCESS) {
-        p->arena.release();
-        delete p;
-        return st;
-    }
-    p->format = fmt;
-    *out = p;
-    return SPMV_SUCCESS;
-}
+// spmv_options_t::build AUTO: host CSRs from this many entries up are built
+// by the device builders (config 4's DIA plan: 10.3 s through the host
+// builders; below this size a host build takes well under a second)
+constexpr int64_t kDeviceBuildMinNnz = (int64_t)1 << 24;
 
-static int dispatch(const spmv_plan_s *p, const double *x, double *y) {
-    switch (p->format) {
-        case SPMV_FORMAT_CSR: return launch_csr(p, x, y);
-        case SPMV_FORMAT_ELL: return launch_ell(p, x, y);
-        case SPMV_FORMAT_HYB:
-            SPMV_RETURN_IF(launch_ell(p, x, y));
-            phase_mark(p);  // ell | overflow
-            return launch_hyb_overflow(p, x, y);
-        case SPMV_FORMAT_SS: return launch_ss(p, x, y);
-        case SPMV_FORMAT_DIA: return launch_dia(p, x, y);
-        case SPMV_FORMAT_CSS: return launch_css(p, x, y);
-        case SPMV_FORMAT_COO: return launch_coo(p, x, y);
-        case SPMV_FORMAT_JDS:
-            SPMV_RETURN_IF(launch_ell(p, x, y));
-            phase_mark(p);  // ell | overflow
-            return launch_hyb_overflow(p, x, y);
-        case SPMV_FORMAT_BIN: return launch_bin(p, x, y);
-    }
-    set_error("plan has an unknown format");
-    return SPMV_ERROR_INVALID_VALUE;
-}
+static int create_from_csr(const HostCsr &A, const spmv_options_t *opt_in, spmv_plan_t *out);
 
-static int bind_device(const spmv_plan_s *p) {
-    int cur = -1;
-    SPMV_HIP_TRY(hipGetDevice(&cur));
-    if (cur != p->device) SPMV_HIP_TRY(hipSetDevice(p->device));
-    return SPMV_SUCCESS;
-}
-
-}  // namespace spmv
-
-using namespace spmv;
-
-extern "C" {
-
-int spmv_api_version(void) { return SPMV_HIP_API_VERSION; }
-
-void spmv_options_default(spmv_options_t *o) {
-    if (!o) return;
-    std::memset(o, 0, sizeof(*o));
-    o->format = SPMV_FORMAT_AUTO;
-    o->device = -1;
-}
-
-int spmv_plan_create_csr(int64_t m, int64_t n, int64_t nnz, const int64_t *row_ptr,
-                         const int32_t *col_idx, const double *val, const spmv_options_t *opt,
-                         spmv_plan_t *plan) {
-    HostCsr A{m, n, nnz, row_ptr, col_idx, val};
-    return create_from_csr(A, opt, plan);
-}
-
-int spmv_plan_create_csr32(int32_t m, int32_t n, int32_t nnz, const int32_t *row_ptr,
-                           const int32_t *col_idx, const double *val, const spmv_options_t *opt,
-                           spmv_plan_t *plan) {
-    SPMV_CHECK_ARG(m >= 0 && row_ptr != nullptr, "bad m or NULL row_ptr");
-    std::vector<int64_t> rp((size_t)m + 1);
-    for (int32_t i = 0; i <= m; ++i) rp[i] = row_ptr[i];
-    HostCsr A{m, n, nnz, rp.data(), col_idx, val};
-    return create_from_csr(A, opt, plan);
-}
-
-int spmv_plan_create_csr_device(int64_t m, int64_t n, int64_t nnz, const int64_t *d_row_ptr,
-                                const int32_t *d_col_idx, const double *d_val, const spmv_options_t *opt_in,
-                                spmv_plan_t *out) {
+// spmv_plan_create_csr_device's body.  A plan whose format the device
+// builders do not make (CSS; BIN rows out of column order or with the long-row
+// run path) is built by the host builders: from a D2H copy of the CSR, or --
+// when need_host_fmt is given (create_via_device, whose caller still holds the
+// host CSR) -- by returning kNeedHostBuild with the resolved options there
+// (format chosen, crs_exact's rewrites applied, build = HOST).
+constexpr int kNeedHostBuild = -2000;
+static int create_device_impl(int64_t m, int64_t n, int64_t nnz, const int64_t *d_row_ptr,
+                              const int32_t *d_col_idx, const double *d_val, const spmv_options_t *opt_in,
+                              spmv_plan_t *out, spmv_options_t *need_host) {
     SPMV_CHECK_ARG(out != nullptr, "plan out-pointer is NULL");
     *out = nullptr;
     spmv_options_t o;
@@ -301,12 +198,20 @@ int spmv_plan_create_csr_device(int64_t m, int64_t n, int64_t nnz, const int64_t
     }
     if (st == SPMV_SUCCESS && !host_build) {
         p->format = fmt;
+        p->built_on_device = 1;
         *out = p;
         return SPMV_SUCCESS;
     }
     p->arena.release();
     delete p;
     if (!host_build) return st;
+    if (need_host) {
+        *need_host = o;
+        need_host->device = dev;
+        need_host->format = fmt;  // AUTO resolved above
+        need_host->build = SPMV_BUILD_HOST;
+        return kNeedHostBuild;
+    }
     {
         // host builders: stage the CSR through host memory
         std::vector<int64_t> rp((size_t)m + 1);
@@ -319,9 +224,185 @@ int spmv_plan_create_csr_device(int64_t m, int64_t n, int64_t nnz, const int64_t
         }
         o.device = dev;
         o.format = fmt;  // AUTO resolved above
+        o.build = SPMV_BUILD_HOST;
         HostCsr H{m, n, nnz, rp.data(), col.data(), val.data()};
         return create_from_csr(H, &o, out);
     }
+}
+
+// Stage a (validated) host CSR into HBM and build the plan there
+// (create_device_impl: the same layouts byte for byte, AUTO resolved by the
+// same chooser).  A format the device builders do not make comes back as
+// kNeedHostBuild with the resolved options in *host_opts;
+// SPMV_ERROR_OUT_OF_MEMORY when the staging copy does not fit.  Either way
+// the caller then takes the host builders.
+static int create_via_device(const HostCsr &A, spmv_options_t o, int dev, spmv_plan_t *out,
+                             spmv_options_t *host_opts) {
+    void *d[3] = {nullptr, nullptr, nullptr};
+    const size_t bytes[3] = {8 * (size_t)(A.m + 1), 4 * (size_t)std::max<int64_t>(A.nnz, 1),
+                             8 * (size_t)std::max<int64_t>(A.nnz, 1)};
+    auto release = [&]() {
+        (void)hipDeviceSynchronize();  // the builders' kernels have read the staging copy
+        for (void *q : d)
+            if (q) (void)hipFree(q);
+    };
+    for (int k = 0; k < 3; ++k)
+        if (hipMalloc(&d[k], bytes[k]) != hipSuccess) {
+            (void)hipGetLastError();
+            release();
+            set_error("device staging of the CSR: out of device memory");
+            return SPMV_ERROR_OUT_OF_MEMORY;
+        }
+    hipError_t e = hipMemcpy(d[0], A.row_ptr, bytes[0], hipMemcpyHostToDevice);
+    if (e == hipSuccess && A.nnz) e = hipMemcpy(d[1], A.col, 4 * (size_t)A.nnz, hipMemcpyHostToDevice);
+    if (e == hipSuccess && A.nnz) e = hipMemcpy(d[2], A.val, 8 * (size_t)A.nnz, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        release();
+        set_error(std::string("device staging of the CSR: ") + hipGetErrorString(e));
+        return SPMV_ERROR_HIP;
+    }
+    o.device = dev;
+    const int st = create_device_impl(A.m, A.n, A.nnz, (const int64_t *)d[0], (const int32_t *)d[1],
+                                      (const double *)d[2], &o, out, host_opts);
+    release();
+    return st;
+}
+
+static int create_from_csr(const HostCsr &A, const spmv_options_t *opt_in, spmv_plan_t *out) {
+    SPMV_CHECK_ARG(out != nullptr, "plan out-pointer is NULL");
+    *out = nullptr;
+    spmv_options_t o;
+    if (opt_in) o = *opt_in;
+    else spmv_options_default(&o);
+    SPMV_CHECK_ARG(o.build >= SPMV_BUILD_AUTO && o.build <= SPMV_BUILD_DEVICE, "build must be SPMV_BUILD_*");
+    SPMV_RETURN_IF(validate_csr(A));
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count == 0) {
+        (void)hipGetLastError();
+        set_error("no HIP device visible (libspmv_hip needs an MI355X / gfx950)");
+        return SPMV_ERROR_NO_DEVICE;
+    }
+    int dev = o.device;
+    if (dev < 0) SPMV_HIP_TRY(hipGetDevice(&dev));
+    SPMV_RETURN_IF(check_device(dev));
+    SPMV_HIP_TRY(hipSetDevice(dev));
+    // the device builders make every format but CSS (and BIN only for rows
+    // in column order without the long-row run path): those, and a staging
+    // copy that does not fit, take the host builders below -- with the format
+    // AUTO resolved on the device
+    if (o.format != SPMV_FORMAT_CSS &&
+        (o.build == SPMV_BUILD_DEVICE || (o.build == SPMV_BUILD_AUTO && A.nnz >= kDeviceBuildMinNnz))) {
+        spmv_options_t ho = o;
+        const int st = create_via_device(A, o, dev, out, &ho);
+        if (st != SPMV_ERROR_OUT_OF_MEMORY && st != kNeedHostBuild) return st;
+        if (st == kNeedHostBuild) o = ho;
+        SPMV_HIP_TRY(hipSetDevice(dev));
+    }
+    spmv_plan_s *p = new (std::nothrow) spmv_plan_s;
+    if (!p) {
+        set_error("host allocation of the plan failed");
+        return SPMV_ERROR_OUT_OF_MEMORY;
+    }
+    p->device = dev;
+    p->arena.device = dev;
+    if (const char *e = probe_env("SPMV_ARENA_VMM_MB")) p->arena.vmm_min = (size_t)std::max(0, std::atoi(e)) << 20;
+    p->m = A.m;
+    p->n = A.n;
+    p->nnz = A.nnz;
+    int fmt = o.format == SPMV_FORMAT_AUTO ? choose_format(A, o) : o.format;
+    if (fmt == SPMV_FORMAT_CSR && o.crs_exact) fmt = choose_crs_exact(A, o);
+    stream_placement(p, fmt, o);
+    int st;
+    switch (fmt) {
+        case SPMV_FORMAT_CSR: st = build_csr(p, A, o); break;
+        case SPMV_FORMAT_ELL: st = build_ell(p, A, o, INT32_MAX); break;
+        case SPMV_FORMAT_HYB: st = build_hyb(p, A, o); break;
+        case SPMV_FORMAT_SS: st = build_ss(p, A, o); break;
+        case SPMV_FORMAT_DIA: st = build_dia(p, A, o); break;
+        case SPMV_FORMAT_CSS: st = build_css(p, A, o); break;
+        case SPMV_FORMAT_COO: st = build_coo(p, A, o); break;
+        case SPMV_FORMAT_JDS: st = build_jds(p, A, o); break;
+        case SPMV_FORMAT_BIN: st = build_bin(p, A, o); break;
+        default:
+            set_error("unknown format");
+            st = SPMV_ERROR_INVALID_VALUE;
+    }
+    if (st != SPMV_SUCCESS) {
+        p->arena.release();
+        delete p;
+        return st;
+    }
+    p->format = fmt;
+    *out = p;
+    return SPMV_SUCCESS;
+}
+
+static int dispatch(const spmv_plan_s *p, const double *x, double *y) {
+    switch (p->format) {
+        case SPMV_FORMAT_CSR: return launch_csr(p, x, y);
+        case SPMV_FORMAT_ELL: return launch_ell(p, x, y);
+        case SPMV_FORMAT_HYB:
+            SPMV_RETURN_IF(launch_ell(p, x, y));
+            phase_mark(p);  // ell | overflow
+            return launch_hyb_overflow(p, x, y);
+        case SPMV_FORMAT_SS: return launch_ss(p, x, y);
+        case SPMV_FORMAT_DIA: return launch_dia(p, x, y);
+        case SPMV_FORMAT_CSS: return launch_css(p, x, y);
+        case SPMV_FORMAT_COO: return launch_coo(p, x, y);
+        case SPMV_FORMAT_JDS:
+            SPMV_RETURN_IF(launch_ell(p, x, y));
+            phase_mark(p);  // ell | overflow
+            return launch_hyb_overflow(p, x, y);
+        case SPMV_FORMAT_BIN: return launch_bin(p, x, y);
+    }
+    set_error("plan has an unknown format");
+    return SPMV_ERROR_INVALID_VALUE;
+}
+
+static int bind_device(const spmv_plan_s *p) {
+    int cur = -1;
+    SPMV_HIP_TRY(hipGetDevice(&cur));
+    if (cur != p->device) SPMV_HIP_TRY(hipSetDevice(p->device));
+    return SPMV_SUCCESS;
+}
+
+}  // namespace spmv
+
+using namespace spmv;
+
+extern "C" {
+
+int spmv_api_version(void) { return SPMV_HIP_API_VERSION; }
+
+void spmv_options_default(spmv_options_t *o) {
+    if (!o) return;
+    std::memset(o, 0, sizeof(*o));
+    o->format = SPMV_FORMAT_AUTO;
+    o->device = -1;
+}
+
+int spmv_plan_create_csr(int64_t m, int64_t n, int64_t nnz, const int64_t *row_ptr,
+                         const int32_t *col_idx, const double *val, const spmv_options_t *opt,
+                         spmv_plan_t *plan) {
+    HostCsr A{m, n, nnz, row_ptr, col_idx, val};
+    return create_from_csr(A, opt, plan);
+}
+
+int spmv_plan_create_csr32(int32_t m, int32_t n, int32_t nnz, const int32_t *row_ptr,
+                           const int32_t *col_idx, const double *val, const spmv_options_t *opt,
+                           spmv_plan_t *plan) {
+    SPMV_CHECK_ARG(m >= 0 && row_ptr != nullptr, "bad m or NULL row_ptr");
+    std::vector<int64_t> rp((size_t)m + 1);
+    for (int32_t i = 0; i <= m; ++i) rp[i] = row_ptr[i];
+    HostCsr A{m, n, nnz, rp.data(), col_idx, val};
+    return create_from_csr(A, opt, plan);
+}
+
+int spmv_plan_create_csr_device(int64_t m, int64_t n, int64_t nnz, const int64_t *d_row_ptr,
+                                const int32_t *d_col_idx, const double *d_val, const spmv_options_t *opt_in,
+                                spmv_plan_t *out) {
+    return create_device_impl(m, n, nnz, d_row_ptr, d_col_idx, d_val, opt_in, out, nullptr);
 }
 
 int spmv_plan_create_csr32_device(int32_t m, int32_t n, int32_t nnz, const int32_t *d_row_ptr,
@@ -688,6 +769,12 @@ int spmv_bin_prod(spmv_plan_t p, void **buf, int64_t *bytes) {
     *buf = p->bin.prod;
     *bytes = 8 * std::max<int64_t>(p->bin.prod_cap, 1);
     return 0;
+}
+
+int spmv_plan_built_on_device(spmv_plan_t p, int32_t *on_device) {
+    SPMV_CHECK_ARG(p != nullptr && on_device != nullptr, "NULL plan or out-pointer");
+    *on_device = p->built_on_device;
+    return SPMV_SUCCESS;
 }
 
 int spmv_plan_info(spmv_plan_t p, spmv_plan_info_t *info) {

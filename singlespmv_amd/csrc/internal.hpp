@@ -386,6 +386,7 @@ struct BinDev {
 struct spmv_plan_s {
     int format = SPMV_FORMAT_CSR;
     int device = 0;
+    int built_on_device = 0;  // 1: the layout was built in HBM (spmv_plan_create_csr_device or build AUTO/DEVICE)
     int64_t m = 0, n = 0, nnz = 0;
     hipStream_t stream = nullptr;
     spmv::DevArena arena;

@@ -701,6 +701,74 @@ def _device_build_cases():
     return cases
 
 
+def test_host_csr_build_routing():
+    """spmv_options_t::build: a host CSR of >= 2^24 entries (AUTO) or any
+    size (DEVICE) is staged into HBM and built by the device builders -- the
+    host builder's layout byte for byte and the same y; CSS, and BIN on rows
+    out of column order or with the long-row run path, take the host
+    builders with the format resolved on the device; small CSRs under AUTO
+    stay on the host builders."""
+    import torch
+    # large: 1 M rows x 17 entries = 17 M entries, AUTO -> BIN (x too wide
+    # for a window) built on the device
+    m = 1_000_000
+    spec = sp.gen_spec("uniform", m, per_row=17, seed=5)
+    rp, col, val = sp.generate_csr(spec)
+    assert int(rp[-1]) >= 1 << 24
+    x = sp.generate_vector(m, seed=6)
+    yo = oracle_y(rp, col, val, x)
+    for fmt in ("auto", "ell", "csr"):
+        pa = sp.Plan.from_csr(m, m, rp, col, val, fmt)
+        assert pa.built_on_device(), fmt
+        ph = sp.Plan.from_csr(m, m, rp, col, val, fmt, build="host")
+        assert not ph.built_on_device()
+        assert pa.info()["format"] == ph.info()["format"] and pa.info()["kernel"] == ph.info()["kernel"], fmt
+        if pa.info()["format"] not in ("bin", "css"):
+            assert pa.digest() == ph.digest(), fmt
+        ya, yh = run_plan(pa, x, m), run_plan(ph, x, m)
+        assert np.array_equal(ya, yh), fmt
+        check_close(ya, yo, what=f"routed {fmt}")
+        pa.destroy()
+        ph.destroy()
+    # small: AUTO keeps the host builders, DEVICE forces the device ones
+    cases = _device_build_cases()
+    for name, mm, n, rp2, col2, val2 in cases[:4] + cases[-1:]:
+        x2 = sp.generate_vector(n, seed=9)
+        for fmt in ("auto", "dia", "hyb", "ss", "jds", "coo", "css", "bin"):
+            try:
+                ph = sp.Plan.from_csr(mm, n, rp2, col2, val2, fmt, build="host")
+            except sp.SpmvError as e:
+                assert "not supported" in str(e), (name, fmt, e)
+                continue
+            assert not sp.Plan.from_csr(mm, n, rp2, col2, val2, fmt).built_on_device()
+            pd = sp.Plan.from_csr(mm, n, rp2, col2, val2, fmt, build="device")
+            dec = np.diff(col2.astype(np.int64) // 20480) < 0  # entry j+1 in an earlier x strip ...
+            inner = rp2[1:-1]
+            dec[inner[(inner > 0) & (inner < len(col2))] - 1] = False  # ... inside one row
+            sorted_rows = not dec.any()  # BIN's device fill wants each row's strips in order
+            # BIN's long-row run path is laid out on the host (build_bin.cpp
+            # bin_long_threshold with the default options)
+            lens2 = np.diff(rp2)
+            S = max(1, -(-n // 20480))
+            lnnz = int(lens2[lens2 >= max(128, S)].sum())
+            nnz2 = int(rp2[-1])
+            long_rows = lnnz > 0 and lnnz * 20 >= nnz2 and nnz2 + nnz2 // 2 + (S << 6) < (1 << 31)
+            got = ph.info()["format"]  # AUTO resolves alike on the host and the device
+            expect_dev = got != "css" and (got != "bin" or (sorted_rows and not long_rows))
+            assert pd.built_on_device() == expect_dev, (name, fmt)
+            if ph.info()["format"] not in ("bin", "css"):
+                assert pd.digest() == ph.digest(), (name, fmt)
+            yd2, yh2 = run_plan(pd, x2, mm), run_plan(ph, x2, mm)
+            if ph.info()["format"] == "coo":  # f64 atomics: unordered adds
+                check_close(yd2, yh2, what=f"routed coo {name}")
+            else:
+                assert np.array_equal(yd2, yh2), (name, fmt)
+            pd.destroy()
+            ph.destroy()
+    with pytest.raises(KeyError):
+        sp.make_options("auto", build="sideways")
+
+
 def test_device_conversion_matches_host_build():
     """spmv_plan_create_csr_device: every format built on the GPU (CSR, SS,
     ELL, HYB, JDS, DIA, COO, and AUTO resolved from device data) gives the
@@ -713,7 +781,7 @@ def test_device_conversion_matches_host_build():
         drp, dcol, dval = _device_csr(rp, col, val)
         for fmt, kw in DEVICE_FORMATS:
             try:
-                ph = sp.Plan.from_csr(m, n, rp, col, val, fmt, **kw)
+                ph = sp.Plan.from_csr(m, n, rp, col, val, fmt, build="host", **kw)
             except sp.SpmvError as e:
                 assert "not supported" in str(e), (name, fmt, e)
                 with pytest.raises(sp.SpmvError, match="not supported"):
@@ -1271,8 +1339,8 @@ def test_full_size_c4_banded():
     yo = oracle_y(rp, col, val, x)
     xd = torch.from_numpy(x).cuda()
     y = torch.empty(m, dtype=torch.float64, device="cuda")
-    plan = sp.Plan.from_csr(m, m, rp, col, val, "dia")
-    assert plan.info()["n_diags"] == 64
+    plan = sp.Plan.from_csr(m, m, rp, col, val, "dia", build="host")
+    assert plan.info()["n_diags"] == 64 and not plan.built_on_device()
     plan.execute(xd, y)
     assert np.array_equal(y.cpu().numpy(), yo)
     # the same DIA plan built on the device from the CSR in HBM (f2): byte-
