@@ -1082,8 +1082,10 @@ def test_plan_create_holds_only_the_plan(fmt, kind):
     m = 4_000_000
     spec = sp.gen_spec(kind, m, per_row=16, band_lo=-20, band_hi=20, seed=21)
     rp, col, val = sp.generate_csr(spec)
+    csr_bytes = 8 * (m + 1) + 12 * int(rp[-1])
     for i in range(10 if fmt == "bin" else 2):
-        plan, drop = _create_peak_drop(lambda: sp.Plan.from_csr(m, m, rp, col, val, fmt))
+        # the host builders (the device builders stage the CSR in HBM: below)
+        plan, drop = _create_peak_drop(lambda: sp.Plan.from_csr(m, m, rp, col, val, fmt, build="host"))
         info = plan.info()
         # AUTO: BIN's product buffer (>= 32 MB) and DIA's values (>= 256 MB)
         # from 2-MB VMM handles
@@ -1093,6 +1095,13 @@ def test_plan_create_holds_only_the_plan(fmt, kind):
             x = sp.generate_vector(m, seed=22)
             y_auto = run_plan(plan, x, m)
         plan.destroy()
+    # built on the device: the staged CSR (and the builders' scratch) on top
+    plan, drop = _create_peak_drop(lambda: sp.Plan.from_csr(m, m, rp, col, val, fmt, build="device"))
+    info = plan.info()
+    assert plan.built_on_device() and info["placement"] == "vmm"
+    assert drop <= info["device_bytes"] + 2 * csr_bytes + (128 << 20), (drop, info["device_bytes"], csr_bytes)
+    assert np.array_equal(run_plan(plan, x, m), y_auto)
+    plan.destroy()
     plan = sp.Plan.from_csr(m, m, rp, col, val, fmt, placement="search")
     info = plan.info()
     assert info["placement"] == "search" and info["placement_candidates"] >= 1
@@ -1108,11 +1117,13 @@ def test_experiment_switches_do_not_reach_the_product_library(monkeypatch):
            "SPMV_BIN_REUSE": "1", "SPMV_BIN_SB": "2", "SPMV_BIN_CUS": "3", "SPMV_BIN_PLACEMENT": "3",
            "SPMV_BIN_HOST_BUILD": "1", "SPMV_CSS_DEBUG": "3", "SPMV_CSS_LAYOUT": "0", "SPMV_CSS_PIECE_DIV": "7",
            "SPMV_CSS_WGS": "5", "SPMV_DIA_DEBUG": "1", "SPMV_DIA_PLACEMENT": "2", "SPMV_ELL_UNROLL": "3",
-           "SPMV_CSR_FORCE_RP64": "1", "SPMV_PLACEMENT_MODE": "9", "SPMV_VMM_CHUNK_MB": "1", "SPMV_BIN_ORDER": "1"}
+           "SPMV_CSR_FORCE_RP64": "1", "SPMV_PLACEMENT_MODE": "9", "SPMV_VMM_CHUNK_MB": "1", "SPMV_BIN_ORDER": "1",
+           "SPMV_LAUNCH_DEBUG": "16", "SPMV_LAUNCH_SS": "0", "SPMV_LAUNCH_SS_SPLIT": "136", "SPMV_LAUNCH_ELL_DBG": "1",
+           "SPMV_LAUNCH_SS_WIN": "0", "SPMV_SS_KERNEL": "0"}
     for k, v in bad.items():
         monkeypatch.setenv(k, v)
     m = 60_000
-    for kind, fmts in (("powerlaw", ["bin", "css", "csr", "ell"]), ("banded", ["dia", "bin"])):
+    for kind, fmts in (("powerlaw", ["bin", "css", "csr", "ell", "ss"]), ("banded", ["dia", "bin", "ss"])):
         spec = sp.gen_spec(kind, m, max_len=900, band_lo=-5, band_hi=9, seed=12)
         rp, col, val = sp.generate_csr(spec)
         x = sp.generate_vector(m, seed=13)
