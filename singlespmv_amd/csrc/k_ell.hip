@@ -35,7 +35,7 @@ __global__ __launch_bounds__(256) void ell_slice_kernel(int64_t m, int64_t n_sli
                                                         const int32_t *__restrict__ col,
                                                         const double *__restrict__ val,
                                                         const double *__restrict__ x,
-                                                        double *__restrict__ y, int dbg) {
+                                                        double *__restrict__ y) {
     const int64_t slice = (int64_t)blockIdx.x * (blockDim.x / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (slice >= n_slices) return;
@@ -92,9 +92,6 @@ __global__ __launch_bounds__(256) void ell_slice_kernel(int64_t m, int64_t n_sli
         acc = madd(b.x, g2, acc);
         acc = madd(b.y, g3, acc);
     }
-#ifdef SPMV_PROBES
-    if (dbg & 1) return;  // probe: ablate the y store (wrong y)
-#endif
     if (srow < m) {
         if (ADD) y[row] = __dadd_rn(y[row], acc);
         else __builtin_nontemporal_store(acc, y + row);  // not re-read: streamed out
@@ -104,15 +101,13 @@ __global__ __launch_bounds__(256) void ell_slice_kernel(int64_t m, int64_t n_sli
 template <int U, bool O32>
 static void launch_ell_uo(const spmv_plan_s *p, const double *x, double *y, size_t lds) {
     const EllDev &e = p->ell;
-    int dbg = 0;  // probe build: SPMV_LAUNCH_ELL_DBG
-    if (const char *v = probe_env("SPMV_LAUNCH_ELL_DBG")) dbg = std::atoi(v);
     const int64_t blocks = (e.n_slices + 3) / 4;
     if (e.perm)
         hipLaunchKernelGGL((ell_slice_kernel<U, false, true, O32>), dim3((unsigned)blocks), dim3(256), lds,
-                           p->stream, p->m, e.n_slices, e.perm, e.slice_off, e.col, e.val, x, y, dbg);
+                           p->stream, p->m, e.n_slices, e.perm, e.slice_off, e.col, e.val, x, y);
     else
         hipLaunchKernelGGL((ell_slice_kernel<U, false, false, O32>), dim3((unsigned)blocks), dim3(256), lds,
-                           p->stream, p->m, e.n_slices, e.perm, e.slice_off, e.col, e.val, x, y, dbg);
+                           p->stream, p->m, e.n_slices, e.perm, e.slice_off, e.col, e.val, x, y);
 }
 
 template <int U>

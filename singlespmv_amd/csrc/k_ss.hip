@@ -58,44 +58,27 @@ __device__ __forceinline__ double readlane_f64(double v, int l) {
 //   tail = S of lane 63 (the row still open at the tile end),
 //   and, when `nrows` finished rows wait in the wave's LDS slice `ys`, those.
 // All of them go out as ONE store instruction (lanes 0..nrows-1 the rows,
-// lane 62 the head, lane 63 the tail) when nrows <= 62: per-tile stores are
-// what backs up the TA data path under the load stream (config 4 PMC:
-// TA_DATA_STALLED_BY_TC 419 M cycles for 4 stores per tile, ELL 4.8 M,
-// profiles/round5/c4_ss_stalls).  The tail's ordinal is a plan constant
+// lane 62 the head, lane 63 the tail) when nrows <= 62, instead of round 4's
+// four (rows, head, tail, tail ordinal) -- neutral at config 4, where the
+// time the y writes cost is spent at the memory, not in the store count
+// (profiles/round5/README.md).  The tail's ordinal is a plan constant
 // (SsDev::tail_ord), not stored here.
 __device__ __forceinline__ void ss_tile_end(int lane, int64_t tile, uint64_t ball, double tot, double S, int nrows,
                                             const double *ys, int64_t ord_base, const int32_t *nzrow,
-                                            int64_t n_nonempty, double *y, double *ht, int mode = 0) {
-    const bool split = mode & 1;
+                                            int64_t n_nonempty, double *y, double *ht) {
     const double s63 = readlane_f64(S, 63);
     const double headv = ball ? readlane_f64(tot, (int)__builtin_ctzll(ball)) : s63;
-    if (split) {  // probe build (SPMV_LAUNCH_SS_SPLIT): round 4's separate store instructions
-        for (int i = lane; i < nrows; i += 64) ss_store(y, nzrow, n_nonempty, ord_base + i, ys[i]);
-        if (ball && lane == (int)__builtin_ctzll(ball)) ht[2 * tile] = tot;
-        if (lane == 63) {
-            if (!ball) ht[2 * tile] = S;
-            else ht[2 * tile + 1] = S;
-        }
-        if (lane == 63 && ball) __builtin_nontemporal_store(S, ht + 2 * tile + 1);  // stands for the tail_ord store
-        return;
-    }
     int rem = nrows;
     if (nrows > 62) {  // wide tile: the rows first, in whole waves
         for (int i = lane; i < nrows; i += 64) ss_store(y, nzrow, n_nonempty, ord_base + i, ys[i]);
         rem = 0;
     }
-    if (mode & 128) rem = 0;  // probe: ablate the row stores (wrong y)
     double *a = nullptr;
     double v = 0.0;
     if (lane < rem) {
         const int64_t ord = ord_base + lane;
         if (ord < n_nonempty) a = y + (nzrow ? (int64_t)nzrow[ord] : ord);
-        if (mode & 1024) a = ht + 2 * tile + 2 + lane;  // probe: the row bytes to scratch instead of y (wrong y)
         v = ys[lane];
-    } else if ((mode & 256) && ball && lane == rem && rem < 62) {  // probe: provisional tail row in y
-        const int64_t ord = ord_base + rem;
-        if (ord < n_nonempty) a = y + (nzrow ? (int64_t)nzrow[ord] : ord);
-        v = s63;
     } else if (lane == 62) {
         a = ht + 2 * tile;
         v = headv;
@@ -103,10 +86,7 @@ __device__ __forceinline__ void ss_tile_end(int lane, int64_t tile, uint64_t bal
         a = ht + 2 * tile + 1;
         v = s63;
     }
-    if (a) {
-        if (mode & 64) __builtin_nontemporal_store(v, a);  // probe: streamed-out stores
-        else *a = v;
-    }
+    if (a) *a = v;
 }
 
 template <int SIGMA, bool WIN>
@@ -224,17 +204,10 @@ __global__ __launch_bounds__(256) void ss_stream_kernel(
     int64_t n_tiles, const int32_t *__restrict__ col, const double *__restrict__ val,
     const uint32_t *__restrict__ flags, const int32_t *__restrict__ tile_ord, const int32_t *__restrict__ win,
     const int32_t *__restrict__ nzrow, int64_t n_nonempty, const double *__restrict__ x,
-    double *__restrict__ y, double *__restrict__ ht, int dbg) {
+    double *__restrict__ y, double *__restrict__ ht) {
     static_assert(SIGMA % 4 == 0 && SIGMA <= 64, "sigma");
     constexpr int Q = SIGMA / 4, W = SIGMA > 32 ? 2 : 1;
-    int64_t blk = blockIdx.x;
-#ifdef SPMV_PROBES
-    if (dbg & 32) {  // XCD-contiguous: workgroup b (XCD b % 8) takes block (b % 8) * (grid / 8) + b / 8
-        const unsigned per = gridDim.x / 8;
-        blk = (int64_t)(blockIdx.x % 8) * per + blockIdx.x / 8;
-    }
-#endif
-    const int64_t tile = blk * (blockDim.x / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t tile = (int64_t)blockIdx.x * (blockDim.x / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (tile >= n_tiles) return;  // wave-uniform
     const int64_t base = tile * 64 * SIGMA;
@@ -252,10 +225,6 @@ __global__ __launch_bounds__(256) void ss_stream_kernel(
     uint32_t f[W];
 #pragma unroll
     for (int w = 0; w < W; ++w) f[w] = flags[(tile * W + w) * 64 + lane];
-#ifdef SPMV_PROBES
-    if (dbg & 8)  // ablate the row starts: no in-lane finishes
-        for (int w = 0; w < W; ++w) f[w] = 0u;
-#endif
     __shared__ double xs[4][kSsWin];
     const int wv = threadIdx.x >> 6;
     int32_t lo = 0, len = 0;
@@ -272,11 +241,7 @@ __global__ __launch_bounds__(256) void ss_stream_kernel(
     int pc = 0;
 #pragma unroll
     for (int w = 0; w < W; ++w) pc += __builtin_popcount(f[w]);
-#ifdef SPMV_PROBES
-    const int incl = (dbg & 4) ? pc * (lane + 1) : wave_inclusive_sum(pc, lane);  // 4: ablate the count scan
-#else
     const int incl = wave_inclusive_sum(pc, lane);
-#endif
     const int64_t ord_base = tile_ord[tile];  // rel ordinal r below = row ord_base + r
     // STAGE: the rows finished inside the tile (ordinals ord_base + [0,
     // total - 1)) go to the wave's LDS slice and leave in the tile's one store
@@ -342,11 +307,7 @@ __global__ __launch_bounds__(256) void ss_stream_kernel(
     else sum_tile(std::false_type{});
 
     const bool has = pc != 0;
-#ifdef SPMV_PROBES
-    const double S = (dbg & 2) ? run : wave_seg_scan(run, has, lane);  // 2: ablate the value scan
-#else
     const double S = wave_seg_scan(run, has, lane);  // open-segment sum at lane end
-#endif
     double C = __shfl_up(S, 1, 64);
     if (lane == 0) C = 0.0;
     const uint64_t ball = __ballot(has);
@@ -363,12 +324,7 @@ __global__ __launch_bounds__(256) void ss_stream_kernel(
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
     }
-#ifdef SPMV_PROBES
-    const int split = dbg;
-#else
-    constexpr int split = 0;
-#endif
-    ss_tile_end(lane, tile, ball, tot, S, stage ? total - 1 : 0, yl, ord_base, nzrow, n_nonempty, y, ht, split);
+    ss_tile_end(lane, tile, ball, tot, S, stage ? total - 1 : 0, yl, ord_base, nzrow, n_nonempty, y, ht);
 }
 
 __global__ __launch_bounds__(256) void ss_fixup_kernel(int64_t n_tiles, const double *__restrict__ ht,
@@ -423,7 +379,7 @@ int ss_plan_tail_ord(spmv_plan_s *p) {
 template <int SIGMA>
 static void launch_ss_t(const spmv_plan_s *p, const double *x, double *y) {
     const SsDev &s = p->ss;
-    int64_t blocks = (s.n_tiles + 3) / 4;
+    const int64_t blocks = (s.n_tiles + 3) / 4;
     // probe build: SPMV_LAUNCH_SS = 0 -> ss_tile_kernel (all SIGMA entries
     // loaded up front, window from the loaded columns, round 4), else the
     // streamed kernel with SPMV_LAUNCH_SS_PF quads ahead; SPMV_LAUNCH_SS_WIN=0
@@ -436,13 +392,10 @@ static void launch_ss_t(const spmv_plan_s *p, const double *x, double *y) {
     if (const char *v = probe_env("SPMV_LAUNCH_SS")) kind = SIGMA > 32 && std::atoi(v) == 0 ? 1 : std::atoi(v);
     if (const char *v = probe_env("SPMV_LAUNCH_SS_PF")) pf = std::atoi(v);
     if (const char *v = probe_env("SPMV_LAUNCH_SS_WIN")) win = std::atoi(v) != 0;
-    int dbg = 0;  // probe build: SPMV_LAUNCH_SS_SPLIT=1 -> separate per-tile store instructions (round 4)
-    if (const char *v = probe_env("SPMV_LAUNCH_SS_SPLIT")) dbg = std::atoi(v);  // bits 2, 4, 8: ablations (wrong y)
-    if (dbg & 32) blocks = (blocks + 7) / 8 * 8;  // XCD-contiguous mapping: a whole number of blocks per XCD
     auto go = [&](auto kern, bool stream) {
         if (stream)
             hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), lds, p->stream, s.n_tiles, s.col, s.val, s.flags,
-                               s.tile_ord, s.win, s.nzrow, s.n_nonempty, x, y, s.ht, dbg);
+                               s.tile_ord, s.win, s.nzrow, s.n_nonempty, x, y, s.ht);
     };
     if (kind == 0 && SIGMA <= 32) {
         constexpr int S0 = SIGMA <= 32 ? SIGMA : 32;
