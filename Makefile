@@ -26,7 +26,7 @@ OPTLIB    = singlespmv_amd/libopt_hip.so
 OBJDIR    = build/obj
 HOST_SRC  = $(CSRC)/capi.cpp $(CSRC)/formats.cpp $(CSRC)/build_bin.cpp $(CSRC)/hostutil.cpp $(CSRC)/mmio.cpp \
             $(CSRC)/dist.cpp
-KERN_SRC  = $(CSRC)/k_csr.hip $(CSRC)/k_ell.hip $(CSRC)/k_ss.hip $(CSRC)/k_dia.hip $(CSRC)/k_css.hip $(CSRC)/k_coo.hip $(CSRC)/k_convert.hip $(CSRC)/k_probe.hip $(CSRC)/k_bin.hip $(CSRC)/k_bin_build.hip $(CSRC)/k_devbuild.hip
+KERN_SRC  = $(CSRC)/k_csr.hip $(CSRC)/k_ell.hip $(CSRC)/k_ss.hip $(CSRC)/k_dia.hip $(CSRC)/k_css.hip $(CSRC)/k_coo.hip $(CSRC)/k_convert.hip $(CSRC)/k_probe.hip $(CSRC)/k_bin.hip $(CSRC)/k_bin_build.hip $(CSRC)/k_devbuild.hip $(CSRC)/k_css_build.hip
 HOST_OBJ  = $(patsubst $(CSRC)/%.cpp,$(OBJDIR)/%.o,$(HOST_SRC))
 KERN_OBJ  = $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(KERN_SRC))
 HDRS      = include/spmv_hip.h include/opt_hip.h include/spmv_util.h \

@@ -132,12 +132,13 @@ typedef struct spmv_options {
                                 (row groups of L lanes: butterfly sums)       */
     int32_t build;           /* plan builders (SPMV_BUILD_*): AUTO = a host CSR of
                                 >= 2^24 entries is staged into HBM and built by
-                                the device builders (every format but CSS;
+                                the device builders (every format;
                                 byte-identical layouts, spmv_plan_digest), when
-                                the staging copy fits in device memory;
-                                smaller ones, CSS, and AUTO / BIN / crs_exact
-                                requests with a row whose columns decrease take
-                                the host builders */
+                                the staging copy fits in device memory
+                                (BIN rows out of column-strip order or with the
+                                long-row run path, and CSS from 2^31 entries,
+                                take the host builders with the format resolved
+                                there); smaller ones take the host builders */
 } spmv_options_t;
 
 /* Where spmv_plan_create_csr / _csr32 / _coo build the layout. */
@@ -145,8 +146,7 @@ typedef enum spmv_build {
     SPMV_BUILD_AUTO = 0,
     SPMV_BUILD_HOST = 1,    /* host builders (formats.cpp, build_bin.cpp)       */
     SPMV_BUILD_DEVICE = 2   /* stage the CSR into HBM and build there whatever
-                               the size (CSS and unsorted BIN requests still
-                               take the host builders)                         */
+                               the size (same exceptions as AUTO)              */
 } spmv_build_t;
 
 /* Placement of the large buffers of a plan (the BIN product buffer, the DIA
@@ -218,15 +218,16 @@ int spmv_plan_create_csr32(int32_t m, int32_t n, int32_t nnz, const int32_t *row
                            const spmv_options_t *opt, spmv_plan_t *plan);
 
 /* Plan from a CSR that already lives in device memory (64-bit row pointers;
- * all three arrays on the plan's device, only read).  Every format but CSS
- * is built on the device (the CSR5 conversion pipeline's role,
+ * all three arrays on the plan's device, only read).  Every format is built
+ * on the device (the CSR5 conversion pipeline's role,
  * CSR5_cuda/detail/cuda/format_cuda.h:21-718): only the row pointers (and,
  * for BIN, the (bin, strip) counts) visit the host, for the layout decisions
  * that depend on row lengths alone; AUTO is resolved there too, its diagonal
- * census run on the device.  The layouts are byte-identical to the host
- * builders' (spmv_plan_digest).  CSS, and BIN when some row's columns are not
- * ascending by 20480-column strip, copy the CSR to the host and take the
- * host builder.  The input is validated on the device like
+ * census run on the device; CSS's per-wave column sorts are one segmented
+ * sort.  The layouts are byte-identical to the host builders'
+ * (spmv_plan_digest).  BIN when some row's columns are not ascending by
+ * 20480-column strip or when it takes the long-row run path, and CSS from
+ * 2^31 entries, copy the CSR to the host and take the host builder.  The input is validated on the device like
  * spmv_plan_create_csr's host check. */
 int spmv_plan_create_csr_device(int64_t m, int64_t n, int64_t nnz, const int64_t *d_row_ptr,
                                 const int32_t *d_col_idx, const double *d_val,
@@ -385,8 +386,8 @@ int spmv_plan_info(spmv_plan_t plan, spmv_plan_info_t *info);
  * of one matrix -- e.g. a host build and a device build -- can be compared
  * array by array without copying them out.  *n_arrays = the plan's array
  * count (digests beyond `cap` are not written); spmv_plan_digest_name(plan,
- * k) names array k.  CSR, ELL, HYB, JDS, SS, DIA and COO plans; BIN and CSS
- * return SPMV_ERROR_NOT_SUPPORTED. */
+ * k) names array k.  CSR, ELL, HYB, JDS, SS, DIA, COO and CSS plans; BIN
+ * returns SPMV_ERROR_NOT_SUPPORTED. */
 int spmv_plan_digest(spmv_plan_t plan, uint64_t *digests, int32_t cap, int32_t *n_arrays);
 const char *spmv_plan_digest_name(spmv_plan_t plan, int32_t k);
 

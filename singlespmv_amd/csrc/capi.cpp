@@ -79,8 +79,8 @@ constexpr int64_t kDeviceBuildMinNnz = (int64_t)1 << 24;
 static int create_from_csr(const HostCsr &A, const spmv_options_t *opt_in, spmv_plan_t *out);
 
 // spmv_plan_create_csr_device's body.  A plan whose format the device
-// builders do not make (CSS; BIN rows out of column order or with the long-row
-// run path) is built by the host builders: from a D2H copy of the CSR, or --
+// builders do not make (BIN rows out of column order or with the long-row run
+// path; CSS from 2^31 entries) is built by the host builders: from a D2H copy of the CSR, or --
 // when need_host_fmt is given (create_via_device, whose caller still holds the
 // host CSR) -- by returning kNeedHostBuild with the resolved options there
 // (format chosen, crs_exact's rewrites applied, build = HOST).
@@ -132,7 +132,8 @@ static int create_device_impl(int64_t m, int64_t n, int64_t nnz, const int64_t *
     // lengths drive AUTO and every slice / bin / overflow decision
     std::vector<int64_t> hrp;
     const bool need_rp = o.format == SPMV_FORMAT_AUTO || o.format == SPMV_FORMAT_ELL || o.format == SPMV_FORMAT_HYB ||
-                         o.format == SPMV_FORMAT_JDS || (o.format == SPMV_FORMAT_CSR && o.crs_exact);
+                         o.format == SPMV_FORMAT_JDS || o.format == SPMV_FORMAT_CSS ||
+                         (o.format == SPMV_FORMAT_CSR && o.crs_exact);
     if (need_rp) {
         hrp.resize((size_t)m + 1);
         const hipError_t e = hipMemcpy(hrp.data(), d_row_ptr, 8 * (size_t)(m + 1), hipMemcpyDeviceToHost);
@@ -190,7 +191,10 @@ static int create_device_impl(int64_t m, int64_t n, int64_t nnz, const int64_t *
                 // non-decreasing; other CSRs take the host builder below
                 if (st == kBinNeedHostBuild) host_build = true;
                 break;
-            case SPMV_FORMAT_CSS: host_build = true; break;  // CSS: host builder only
+            case SPMV_FORMAT_CSS:
+                if (nnz >= ((int64_t)1 << 31) - 256) host_build = true;  // the segmented sort's int counts
+                else st = build_css_device(p, A, o);
+                break;
             default:
                 set_error("unknown format");
                 st = SPMV_ERROR_INVALID_VALUE;
@@ -287,12 +291,11 @@ static int create_from_csr(const HostCsr &A, const spmv_options_t *opt_in, spmv_
     if (dev < 0) SPMV_HIP_TRY(hipGetDevice(&dev));
     SPMV_RETURN_IF(check_device(dev));
     SPMV_HIP_TRY(hipSetDevice(dev));
-    // the device builders make every format but CSS (and BIN only for rows
-    // in column order without the long-row run path): those, and a staging
-    // copy that does not fit, take the host builders below -- with the format
-    // AUTO resolved on the device
-    if (o.format != SPMV_FORMAT_CSS &&
-        (o.build == SPMV_BUILD_DEVICE || (o.build == SPMV_BUILD_AUTO && A.nnz >= kDeviceBuildMinNnz))) {
+    // the device builders make every format (BIN only for rows in column
+    // order without the long-row run path, CSS below 2^31 entries): the rest,
+    // and a staging copy that does not fit, take the host builders below --
+    // with the format AUTO resolved on the device
+    if (o.build == SPMV_BUILD_DEVICE || (o.build == SPMV_BUILD_AUTO && A.nnz >= kDeviceBuildMinNnz)) {
         spmv_options_t ho = o;
         const int st = create_via_device(A, o, dev, out, &ho);
         if (st != SPMV_ERROR_OUT_OF_MEMORY && st != kNeedHostBuild) return st;

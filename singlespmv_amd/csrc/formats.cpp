@@ -967,10 +967,6 @@ struct CssEntry {
     uint16_t slot;
     double val;
 };
-struct CssPiece {
-    int64_t begin, end;  // CSR entry range
-    int slot;            // LDS slot (row l -> slot l; extra pieces after the rows)
-};
 }  // namespace
 
 // Column-slab sweep (k_css.hip).  Rows are cut into nnz-balanced blocks, one
@@ -979,8 +975,18 @@ struct CssPiece {
 // (merged in piece order at pass end), pieces go to the 15 worker waves
 // longest-first onto the least loaded wave (LPT), and each wave's entries are
 // sorted by column.
-int build_css(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
+//
+// css_layout: every decision above from the row pointers alone (the host and
+// the device builder share it); the entry fill -- each wave list's entries
+// stably sorted by column into its chunks -- is css_fill_host below or
+// css_fill_device (k_css_build.hip).
+int css_layout(spmv_plan_s *p, const int64_t *row_ptr, int64_t m, int64_t n, int64_t nnz, const spmv_options_t &o,
+               CssLayout &CL) {
     CssDev &c = p->css;
+    struct {
+        int64_t m, n, nnz;
+        const int64_t *row_ptr;
+    } A{m, n, nnz, row_ptr};
     int ncu = 0;
     SPMV_HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, p->device));
     c.nwg = ncu > 0 ? ncu : 256;
@@ -1005,8 +1011,8 @@ int build_css(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
     std::stable_sort(longs.begin(), longs.end(), [&](int64_t a, int64_t b) { return row_len(a) > row_len(b); });
     int64_t short_nnz = 0;
     for (int64_t r : shorts) short_nnz += row_len(r);
-    std::vector<int64_t> roff;          // [nb + 1] into rmap
-    std::vector<int32_t> rmap;          // block rows in slot order
+    std::vector<int64_t> &roff = CL.roff;  // [nb + 1] into rmap
+    std::vector<int32_t> &rmap = CL.rmap;  // block rows in slot order
     int64_t piece_cap = 0;
     int piece_div = 2;
     if (const char *d = probe_env("SPMV_CSS_PIECE_DIV")) piece_div = std::max(1, std::atoi(d));
@@ -1106,10 +1112,13 @@ int build_css(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
     c.pace_all = o.css_pace == 2 ? 0 : 1;
     const int64_t nblocks = (int64_t)c.P * c.nwg;
     const int64_t nlists = nblocks * W;
-    std::vector<int64_t> woff((size_t)nlists + 1, 0);
-    std::vector<int64_t> moff((size_t)nblocks + 1, 0);
+    std::vector<int64_t> &woff = CL.woff;
+    std::vector<int64_t> &moff = CL.moff;
+    woff.assign((size_t)nlists + 1, 0);
+    moff.assign((size_t)nblocks + 1, 0);
     std::vector<std::vector<int32_t>> merges((size_t)nblocks);
-    std::vector<std::vector<CssPiece>> wave_pieces((size_t)nlists);
+    std::vector<std::vector<CssPiece>> &wave_pieces = CL.wave_pieces;
+    wave_pieces.assign((size_t)nlists, {});
 #pragma omp parallel
     {
         std::vector<CssPiece> pieces;
@@ -1154,7 +1163,8 @@ int build_css(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
     // the chip stream one contiguous band of the entry arrays (measured:
     // tools/gather_probe.hip e10 vs e13); lists are padded to the longest of
     // the pass with benign entries (col 0, dummy slot, val 0).
-    std::vector<int32_t> wlen((size_t)nlists);
+    std::vector<int32_t> &wlen = CL.wlen;
+    wlen.assign((size_t)nlists, 0);
     for (int64_t L = 0; L < nlists; ++L) wlen[(size_t)L] = (int32_t)woff[(size_t)L + 1];
     for (int64_t b = 0; b < nblocks; ++b) moff[b + 1] += moff[b];
     const int64_t lists_per_pass = (int64_t)c.nwg * W;
@@ -1178,56 +1188,85 @@ int build_css(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
         total = woff[(size_t)nlists];
         c.chunk_stride = 256;
     }
+    CL.merge.assign((size_t)std::max<int64_t>(3 * moff[nblocks], 1), 0);
+#pragma omp parallel for schedule(static)
+    for (int64_t b = 0; b < nblocks; ++b)
+        std::copy(merges[(size_t)b].begin(), merges[(size_t)b].end(), CL.merge.begin() + 3 * moff[b]);
+    CL.total = total;
+    CL.nlists = nlists;
+    CL.nblocks = nblocks;
+    CL.has_longs = !longs.empty();
+    c.split_rows = moff[nblocks];
+    return SPMV_SUCCESS;
+}
+
+// the host fill: each wave list's entries, stably sorted by column (a row's
+// entries of one column keep their CSR order), into the list's chunks
+int css_fill_host(spmv_plan_s *p, const HostCsr &A, CssLayout &CL) {
+    CssDev &c = p->css;
+    const int64_t total = CL.total;
     std::vector<int32_t> col((size_t)std::max<int64_t>(total, 1), 0);
     std::vector<uint16_t> slot((size_t)std::max<int64_t>(total, 1), (uint16_t)kCssMaxRows);
     std::vector<double> val((size_t)std::max<int64_t>(total, 1), 0.0);
-    std::vector<int32_t> merge((size_t)std::max<int64_t>(3 * moff[nblocks], 1));
 #pragma omp parallel
     {
         std::vector<CssEntry> in;
 #pragma omp for schedule(dynamic, 4)
-        for (int64_t L = 0; L < nlists; ++L) {
+        for (int64_t L = 0; L < CL.nlists; ++L) {
             in.clear();
-            for (const CssPiece &pc : wave_pieces[(size_t)L])
+            for (const CssPiece &pc : CL.wave_pieces[(size_t)L])
                 for (int64_t j = pc.begin; j < pc.end; ++j) in.push_back(CssEntry{A.col[j], (uint16_t)pc.slot, A.val[j]});
             // column order = slab order; stable keeps a row's CSR order
             std::stable_sort(in.begin(), in.end(), [](const CssEntry &a, const CssEntry &b) { return a.col < b.col; });
-            const int64_t base = woff[L];
+            const int64_t base = CL.woff[L];
             for (size_t i = 0; i < in.size(); ++i) {
                 const int64_t out = base + (int64_t)(i / 256) * c.chunk_stride + (int64_t)(i % 256);
                 col[out] = in[i].col;
                 slot[out] = in[i].slot;
                 val[out] = in[i].val;
             }
-            std::vector<CssPiece>().swap(wave_pieces[(size_t)L]);
         }
-#pragma omp for schedule(static)
-        for (int64_t b = 0; b < nblocks; ++b)
-            std::copy(merges[(size_t)b].begin(), merges[(size_t)b].end(), merge.begin() + 3 * moff[b]);
     }
-    c.split_rows = moff[nblocks];
-    SPMV_RETURN_IF(upload(p, &c.woff, woff.data(), nlists + 1));
-    SPMV_RETURN_IF(upload(p, &c.wlen, wlen.data(), nlists));
-    SPMV_RETURN_IF(upload(p, &c.bstart, roff.data(), nblocks + 1));
-    c.rmap = nullptr;  // identity (rows in matrix order) unless long rows were dealt out
-    if (!longs.empty()) SPMV_RETURN_IF(upload(p, &c.rmap, rmap.data(), (int64_t)rmap.size()));
-    SPMV_RETURN_IF(upload(p, &c.moff, moff.data(), nblocks + 1));
-    SPMV_RETURN_IF(upload(p, &c.merge, merge.data(), 3 * moff[nblocks]));
     // +256 entries: a contiguous list's last chunk may read past the array
     // (masked lanes); zero col, val -- and slot 0, which masking overrides
     SPMV_RETURN_IF(upload(p, &c.col, col.data(), total, 256));
     SPMV_RETURN_IF(upload(p, &c.row, slot.data(), total, 256));
     SPMV_RETURN_IF(upload(p, &c.val, val.data(), total, 256));
+    return SPMV_SUCCESS;
+}
+
+// the layout's host arrays, pacing counters and plan info (both builders)
+int css_finish(spmv_plan_s *p, const CssLayout &CL, int64_t m, int64_t n, int64_t nnz) {
+    CssDev &c = p->css;
+    SPMV_RETURN_IF(upload(p, &c.woff, CL.woff.data(), CL.nlists + 1));
+    SPMV_RETURN_IF(upload(p, &c.wlen, CL.wlen.data(), CL.nlists));
+    SPMV_RETURN_IF(upload(p, &c.bstart, CL.roff.data(), CL.nblocks + 1));
+    c.rmap = nullptr;  // identity (rows in matrix order) unless long rows were dealt out
+    c.n_rmap = 0;
+    if (CL.has_longs) {
+        SPMV_RETURN_IF(upload(p, &c.rmap, CL.rmap.data(), (int64_t)CL.rmap.size()));
+        c.n_rmap = (int64_t)CL.rmap.size();
+    }
+    SPMV_RETURN_IF(upload(p, &c.moff, CL.moff.data(), CL.nblocks + 1));
+    SPMV_RETURN_IF(upload(p, &c.merge, CL.merge.data(), 3 * CL.moff[(size_t)CL.nblocks]));
     std::vector<uint64_t> zeros(8 * 16, 0);
     SPMV_RETURN_IF(upload(p, &c.prog, zeros.data(), (int64_t)zeros.size()));
     c.launches = 0;
+    c.n_lists = CL.nlists;
     if (const char *d = probe_env("SPMV_CSS_DEBUG")) c.dbg = std::atoi(d);
     if (c.dbg & 32) SPMV_RETURN_IF(dev_alloc(p, &c.tstamp, (int64_t)c.P * c.nwg * (kCssWorkers + 2)));
-    p->stored_slots = total;
-    p->algo_bytes = 12 * A.nnz + 8 * A.n + 8 * A.m;
+    p->stored_slots = CL.total;
+    p->algo_bytes = 12 * nnz + 8 * n + 8 * m;
     p->n_kernels = 1;
     p->kernel_name = "css_sweep_kernel";
     return SPMV_SUCCESS;
+}
+
+int build_css(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
+    CssLayout CL;
+    SPMV_RETURN_IF(css_layout(p, A.row_ptr, A.m, A.n, A.nnz, o, CL));
+    SPMV_RETURN_IF(css_fill_host(p, A, CL));
+    return css_finish(p, CL, A.m, A.n, A.nnz);
 }
 
 // ---------------------------------------------------------------- AUTO

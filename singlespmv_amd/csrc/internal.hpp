@@ -273,6 +273,23 @@ struct CssDev {
     uint64_t launches = 0;
     int dbg = 0;  // ablation switches (SPMV_CSS_DEBUG, internal)
     uint64_t *tstamp = nullptr;  // dbg & 32: [P*nwg][kCssWorkers + 2] s_memrealtime stamps
+    int64_t n_lists = 0;         // worker-wave lists (P * nwg * kCssWorkers)
+    int64_t n_rmap = 0;          // entries of rmap (0: identity)
+};
+// CSS layout decided from the row pointers (formats.cpp css_layout), shared by
+// the host fill and the device fill (k_css_build.hip)
+struct CssPiece {
+    int64_t begin, end;  // CSR entry range
+    int slot;            // LDS slot (row l -> slot l; extra pieces after the rows)
+};
+struct CssLayout {
+    std::vector<int64_t> roff;                     // [nblocks + 1] into rmap
+    std::vector<int32_t> rmap;                     // block rows in slot order
+    std::vector<std::vector<CssPiece>> wave_pieces; // [nlists] pieces of each worker-wave list, list order
+    std::vector<int64_t> woff, moff;               // physical list starts [nlists + 1]; merge offsets [nblocks + 1]
+    std::vector<int32_t> wlen, merge;              // list lengths [nlists]; merge triples
+    int64_t total = 0, nlists = 0, nblocks = 0;
+    bool has_longs = false;
 };
 
 // Binned two-phase Mul/Sum (BIN, k_bin.hip) -- opt_ss's Mul -> val_buf ->
@@ -488,6 +505,10 @@ struct DevCsr {
 constexpr int kDiaRefused = -1001;  // dia_offsets_device: too many diagonals / too much fill
 int dia_offsets_device(spmv_plan_s *p, const DevCsr &A, int max_diags, double max_fill, std::vector<int32_t> &offs);
 int build_dia_device(spmv_plan_s *p, const DevCsr &A, const spmv_options_t &o);
+int css_layout(spmv_plan_s *p, const int64_t *row_ptr, int64_t m, int64_t n, int64_t nnz, const spmv_options_t &o,
+               CssLayout &CL);
+int css_finish(spmv_plan_s *p, const CssLayout &CL, int64_t m, int64_t n, int64_t nnz);
+int build_css_device(spmv_plan_s *p, const DevCsr &A, const spmv_options_t &o);
 // every row's columns strictly ascending (no duplicates, no disorder)?
 int rows_strict_device(spmv_plan_s *p, const DevCsr &A, bool *strict);
 int build_ell_device(spmv_plan_s *p, const DevCsr &A, const spmv_options_t &o);

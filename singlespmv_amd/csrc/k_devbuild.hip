@@ -510,8 +510,22 @@ int plan_arrays(const spmv_plan_s *p, std::vector<ArrayRef> &a) {
             add("val", p->coo.val, 8 * total);
             return SPMV_SUCCESS;
         }
+        case SPMV_FORMAT_CSS: {
+            const CssDev &c = p->css;
+            const int64_t nb = (int64_t)c.P * c.nwg, total = p->stored_slots;
+            add("woff", c.woff, 8 * (c.n_lists + 1));
+            add("wlen", c.wlen, 4 * c.n_lists);
+            add("bstart", c.bstart, 8 * (nb + 1));
+            add("rmap", c.rmap, 4 * c.n_rmap);
+            add("moff", c.moff, 8 * (nb + 1));
+            add("merge", c.merge, 12 * c.split_rows);
+            add("col", c.col, 4 * total);
+            add("slot", c.row, (2 * total) & ~(int64_t)3);  // whole words (total is a multiple of 256 when interleaved)
+            add("val", c.val, 8 * total);
+            return SPMV_SUCCESS;
+        }
     }
-    set_error("spmv_plan_digest: BIN and CSS plans have no digest");
+    set_error("spmv_plan_digest: BIN plans have no digest");
     return SPMV_ERROR_NOT_SUPPORTED;
 }
 

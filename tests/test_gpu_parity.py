@@ -668,7 +668,8 @@ def _device_csr(rp, col, val):
 
 DEVICE_FORMATS = [("csr", {}), ("csr", {"csr_lanes": 1}), ("ss", {"ss_sigma": 4}), ("ss", {"ss_sigma": 16}),
                   ("ss", {"ss_sigma": 32}), ("ss", {"ss_sigma": 64}), ("ss", {}), ("ell", {}), ("hyb", {}), ("hyb", {"ell_width": 4}),
-                  ("jds", {}), ("jds", {"ell_width": 8}), ("dia", {}), ("coo", {}), ("auto", {})]
+                  ("jds", {}), ("jds", {"ell_width": 8}), ("dia", {}), ("coo", {}), ("css", {}),
+                  ("css", {"css_slab_shift": 12}), ("auto", {})]
 
 
 def _device_build_cases():
@@ -704,10 +705,10 @@ def _device_build_cases():
 def test_host_csr_build_routing():
     """spmv_options_t::build: a host CSR of >= 2^24 entries (AUTO) or any
     size (DEVICE) is staged into HBM and built by the device builders -- the
-    host builder's layout byte for byte and the same y; CSS, and BIN on rows
-    out of column order or with the long-row run path, take the host
-    builders with the format resolved on the device; small CSRs under AUTO
-    stay on the host builders."""
+    host builder's layout byte for byte and the same y; BIN on rows out of
+    column order or with the long-row run path takes the host builders with
+    the format resolved on the device; small CSRs under AUTO stay on the host
+    builders."""
     import torch
     # large: 1 M rows x 17 entries = 17 M entries, AUTO -> BIN (x too wide
     # for a window) built on the device
@@ -717,13 +718,13 @@ def test_host_csr_build_routing():
     assert int(rp[-1]) >= 1 << 24
     x = sp.generate_vector(m, seed=6)
     yo = oracle_y(rp, col, val, x)
-    for fmt in ("auto", "ell", "csr"):
+    for fmt in ("auto", "ell", "csr", "css"):
         pa = sp.Plan.from_csr(m, m, rp, col, val, fmt)
         assert pa.built_on_device(), fmt
         ph = sp.Plan.from_csr(m, m, rp, col, val, fmt, build="host")
         assert not ph.built_on_device()
         assert pa.info()["format"] == ph.info()["format"] and pa.info()["kernel"] == ph.info()["kernel"], fmt
-        if pa.info()["format"] not in ("bin", "css"):
+        if pa.info()["format"] != "bin":
             assert pa.digest() == ph.digest(), fmt
         ya, yh = run_plan(pa, x, m), run_plan(ph, x, m)
         assert np.array_equal(ya, yh), fmt
@@ -754,9 +755,9 @@ def test_host_csr_build_routing():
             nnz2 = int(rp2[-1])
             long_rows = lnnz > 0 and lnnz * 20 >= nnz2 and nnz2 + nnz2 // 2 + (S << 6) < (1 << 31)
             got = ph.info()["format"]  # AUTO resolves alike on the host and the device
-            expect_dev = got != "css" and (got != "bin" or (sorted_rows and not long_rows))
+            expect_dev = got != "bin" or (sorted_rows and not long_rows)
             assert pd.built_on_device() == expect_dev, (name, fmt)
-            if ph.info()["format"] not in ("bin", "css"):
+            if ph.info()["format"] != "bin":
                 assert pd.digest() == ph.digest(), (name, fmt)
             yd2, yh2 = run_plan(pd, x2, mm), run_plan(ph, x2, mm)
             if ph.info()["format"] == "coo":  # f64 atomics: unordered adds
@@ -792,7 +793,7 @@ def test_device_conversion_matches_host_build():
             for k in ("format", "kernel", "empty_rows", "stored_slots", "algo_bytes", "n_kernels", "ell_width",
                       "n_diags", "overflow_nnz", "csr_lanes", "ss_sigma"):
                 assert idv[k] == ih[k], f"{name} {fmt} {kw}: info {k} {idv[k]} != {ih[k]}"
-            if ih["format"] not in ("bin", "css"):
+            if ih["format"] != "bin":
                 dh, dd = ph.digest(), pd.digest()
                 assert list(dd) == list(dh), (name, fmt, list(dd), list(dh))
                 bad = [a for a in dh if dh[a] != dd[a]]
