@@ -180,16 +180,15 @@ int auto_csr_lanes(double mean_row) {
 }
 
 int auto_ss_sigma(double mean_row) {
-    // ~one row boundary per lane keeps the in-lane branch count low while
-    // each lane keeps SIGMA*12 bytes of loads in flight; long rows stop at 20:
-    // with the x window SIGMA = 32 needs 172 VGPRs (2 waves per SIMD) and was
-    // the slowest of 16 / 20 / 24 / 32 on three banded shapes (32, 40, 128
-    // per row), 20 within 3 % of the best on each; at config 4 (64 per row)
-    // plan placement alone moves a launch by up to 8 %, more than SIGMA does
-    // (profiles/round4/probe/ss_sigma_window_*.jsonl)
+    // ~one row boundary per lane keeps the in-lane work low while each lane
+    // keeps SIGMA*12 bytes of loads in flight.  Long rows: 32 since the
+    // streamed kernel (round 5: a lane holds PF + 1 quads, not SIGMA
+    // entries -- round 4's tile kernel needed 172 VGPRs at 32 and lost with
+    // it); config 4, same plans: SIGMA 20 / 32 / 48 / 64 at PF 2 2.629 /
+    // 2.537 / 2.542 / 2.635 ms (profiles/round5/probe/c4_ss_sigma_pf_sweep.jsonl)
     if (mean_row <= 6) return 8;
     if (mean_row <= 24) return 16;
-    return 20;
+    return 32;
 }
 
 // ---------------------------------------------------------------- CSR

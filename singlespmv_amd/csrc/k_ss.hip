@@ -250,7 +250,7 @@ __global__ __launch_bounds__(256) void ss_stream_kernel(
     // segment parks at rel0 - 1 until the scan), [1, kSsStageRows] = rel 0..,
     // then one dump slot per lane.
     __shared__ double ys[STAGE ? 4 : 1][STAGE ? kSsStageRows + 1 + 64 : 1];
-    const int total = __shfl(incl, 63, 64);
+    const int total = __builtin_amdgcn_readlane(incl, 63);
     const bool stage = STAGE && total <= kSsStageRows;  // wave-uniform
     double *yl = &ys[STAGE ? wv : 0][STAGE ? 1 : 0];
     double *dump = &ys[STAGE ? wv : 0][STAGE ? kSsStageRows + 1 + lane : 0];
