@@ -399,6 +399,7 @@ def time_formats(ctx, args, M, fmts, trials_head: int, y_check=None, setup_mark=
             "achieved_gbs": algo / launch_s / 1e9,
             "algo_bytes": algo, "format_bytes": info["algo_bytes"], "stored_slots": info["stored_slots"],
             "device_bytes": info["device_bytes"], "plan_build_s": round(t_plan, 3),
+            "built_on_device": plan.built_on_device(),
             "n_kernels": info["n_kernels"], "placement": info["placement"],
             "plan_ordinal": PLAN_ORDINAL[0],
             "placement_info": {"mode": info["placement"], "candidates": info["placement_candidates"],
