@@ -3,9 +3,10 @@
 // (src/opt_ss.cpp:52-142 builds opt_ss's segments and val_buf, untimed, once).
 //
 //   build_bin        host CSR: OpenMP-parallel over bins, then one upload
-//   build_bin_device device CSR (k_bin_build.hip): only the row pointers and
-//                    the (bin, strip) counts visit the host; the entry arrays
-//                    are filled in HBM
+//   build_bin_device device CSR (k_bin_build.hip): only the row pointers,
+//                    the (bin, strip) counts and the long rows' runs (strip,
+//                    first entry) visit the host; the entry arrays are
+//                    filled in HBM
 //
 // Both share the phases: parameters -> row bins -> segment counts -> offsets
 // (row groups, Mul / Sum orders) -> fill -> Mul pieces -> uploads and the
@@ -891,6 +892,128 @@ int build_bin(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o) {
     return bin_finish(p, A.n, L, o);
 }
 
+// ---- long rows from a device CSR: the same layout from the rows' runs (a
+// row's entries in one strip, contiguous when its strips are non-decreasing,
+// which bin_count_device checks) instead of its entries -- the run-based twin
+// of bin_long_prep and bin_long_count
+struct BinDevLong {
+    std::vector<int32_t> lrows;         // long rows, ascending
+    std::vector<int64_t> roff, rbeg;    // [nl + 1] runs per long row; each run's first entry
+    std::vector<int32_t> rstrip, rlen;  // each run's strip and length
+    std::vector<int64_t> order;         // the runs sorted [strip][row]
+};
+
+static int bin_long_prep_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col,
+                                const std::vector<int64_t> &rp, BinLayout &L, BinDevLong &D) {
+    const int64_t m = p->m, S = L.S;
+    D = BinDevLong();
+    for (int64_t r = 0; r < m; ++r)
+        if (L.is_long(rp.data(), r)) D.lrows.push_back((int32_t)r);
+    SPMV_RETURN_IF(bin_long_runs_device(p, d_rp, d_col, D.lrows, D.roff, D.rstrip, D.rbeg));
+    const int64_t nl = (int64_t)D.lrows.size(), R = D.roff[(size_t)nl];
+    D.rlen.resize((size_t)R);
+    // Sum entries per row: a long row needs one per strip it touches and one
+    // per 64 entries (bin_long_prep)
+    std::vector<int64_t> w((size_t)m);
+    for (int64_t r = 0; r < m; ++r) w[(size_t)r] = rp[(size_t)r + 1] - rp[(size_t)r];
+    for (int64_t i = 0; i < nl; ++i) {
+        const int64_t r = D.lrows[(size_t)i], k0 = D.roff[(size_t)i], k1 = D.roff[(size_t)i + 1];
+        for (int64_t k = k0; k < k1; ++k)
+            D.rlen[(size_t)k] = (int32_t)((k + 1 < k1 ? D.rbeg[(size_t)k + 1] : rp[(size_t)r + 1]) - D.rbeg[(size_t)k]);
+        w[(size_t)r] = (k1 - k0) + w[(size_t)r] / 64;
+    }
+    L.eff_rp.assign((size_t)m + 1, 0);
+    for (int64_t r = 0; r < m; ++r) L.eff_rp[(size_t)r + 1] = L.eff_rp[(size_t)r] + w[(size_t)r];
+    // long entries per strip, and the runs in [strip][row] order (a stable
+    // counting sort: the runs of a row come in strip order, rows ascending)
+    L.lb_off.assign((size_t)S + 1, 0);
+    std::vector<int64_t> rc((size_t)S + 1, 0);
+    for (int64_t k = 0; k < R; ++k) {
+        L.lb_off[(size_t)D.rstrip[(size_t)k] + 1] += D.rlen[(size_t)k];
+        ++rc[(size_t)D.rstrip[(size_t)k] + 1];
+    }
+    for (int64_t t = 0; t < S; ++t) {
+        L.lb_off[(size_t)t + 1] += L.lb_off[(size_t)t];
+        rc[(size_t)t + 1] += rc[(size_t)t];
+    }
+    D.order.resize((size_t)R);
+    for (int64_t k = 0; k < R; ++k) D.order[(size_t)rc[(size_t)D.rstrip[(size_t)k]]++] = k;
+    return SPMV_SUCCESS;
+}
+
+// the long row of run k (runs are numbered in long-row order)
+static inline int64_t run_row_index(const BinDevLong &D, int64_t k) {
+    return std::upper_bound(D.roff.begin(), D.roff.end(), k) - D.roff.begin() - 1;
+}
+
+// Walk the runs of every strip in [strip][row] order: f(t, k, row, bin, q0,
+// pieces).  A piece starts at each run's first entry and at every 64-entry
+// boundary of the strip's long block (long_starts).
+template <typename F>
+static void bin_long_walk(const BinLayout &L, const BinDevLong &D, F &&f) {
+    int64_t t = 0, q0 = 0, b = 0;
+    for (size_t i = 0; i < D.order.size(); ++i) {
+        const int64_t k = D.order[i];
+        if (D.rstrip[(size_t)k] != t || i == 0) {
+            t = D.rstrip[(size_t)k];
+            q0 = 0;
+            b = 0;
+        }
+        const int32_t r = D.lrows[(size_t)run_row_index(D, k)];
+        while (L.row0[(size_t)b + 1] <= r) ++b;
+        const int64_t len = D.rlen[(size_t)k];
+        f(t, k, r, b, q0, 1 + ((q0 + len - 1) >> 6) - (q0 >> 6));
+        q0 += len;
+    }
+}
+
+static void bin_long_count_device(BinLayout &L, const BinDevLong &D) {
+    const int64_t S = L.S, NB = L.NB;
+    L.lpc.assign((size_t)(NB * S), 0);
+    L.lpad.assign((size_t)S, 0);
+    bin_long_walk(L, D, [&](int64_t t, int64_t, int32_t, int64_t b, int64_t, int64_t pieces) {
+        L.lpc[(size_t)(b * S + t)] += (int32_t)pieces;
+    });
+    for (int64_t t = 0; t < S; ++t) L.lpad[(size_t)t] = (L.lb_off[(size_t)t + 1] - L.lb_off[(size_t)t] + 63) & ~(int64_t)63;
+}
+
+// the fill's per-run table (bin_fill_arrays' long blocks): the product
+// position of each run's first piece -- the pieces of bin b in strip t number
+// on from lpoff[b][t] in strip order
+static void bin_long_runs_table(const BinLayout &L, const BinDevLong &D, BinLongRuns &LR) {
+    const int64_t S = L.S, R = (int64_t)D.order.size();
+    LR.j0.resize((size_t)R);
+    LR.q0.resize((size_t)R);
+    LR.fpos.resize((size_t)R);
+    LR.len.resize((size_t)R);
+    LR.strip.resize((size_t)R);
+    LR.slot.resize((size_t)R);
+    LR.bin.resize((size_t)R);
+    size_t i = 0;
+    int64_t pos = -1, lastb = -1, lastt = -1;
+    bin_long_walk(L, D, [&](int64_t t, int64_t k, int32_t r, int64_t b, int64_t q0, int64_t pieces) {
+        if (t != lastt) {
+            lastt = t;
+            lastb = -1;
+        }
+        if (b != lastb) {
+            pos = L.lpoff[(size_t)(b * S + t)];
+            lastb = b;
+        } else {
+            ++pos;
+        }
+        LR.j0[i] = D.rbeg[(size_t)k];
+        LR.q0[i] = q0;
+        LR.fpos[i] = pos;
+        LR.len[i] = D.rlen[(size_t)k];
+        LR.strip[i] = (int32_t)t;
+        LR.slot[i] = r - L.row0[(size_t)b];
+        LR.bin[i] = (int32_t)b;
+        pos += pieces - 1;
+        ++i;
+    });
+}
+
 int build_bin_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, const double *d_val,
                      const spmv_options_t &o) {
     BinDev &B = p->bin;
@@ -901,20 +1024,51 @@ int build_bin_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, 
     }
     std::vector<int64_t> rp((size_t)p->m + 1);
     SPMV_HIP_TRY(hipMemcpy(rp.data(), d_rp, 8 * (size_t)(p->m + 1), hipMemcpyDeviceToHost));
-    // long rows take the host builder (the run path is laid out on the host)
-    if (bin_long_threshold(o, rp.data(), p->m, p->nnz, std::max<int64_t>(1, (p->n + B.strip - 1) / B.strip)) > 0)
-        return kBinNeedHostBuild;
+    const int64_t S = std::max<int64_t>(1, (p->n + B.strip - 1) / B.strip);
+    int64_t LL = bin_long_threshold(o, rp.data(), p->m, p->nnz, S);
+    // bin_layout's loop: long rows take the run path when their product
+    // positions fit lcode, else the layout is redone without it
     BinLayout L;
-    bin_mo_resolve(B, o, 0, p->nnz);
-    SPMV_RETURN_IF(bin_rows(p, rp.data(), p->m, p->n, L));
-    std::vector<int64_t> bstart((size_t)L.NB + 1);
-    for (int64_t b = 0; b <= L.NB; ++b) bstart[(size_t)b] = rp[(size_t)L.row0[(size_t)b]];
+    BinDevLong D;
+    std::vector<int64_t> bstart;
+    for (;;) {
+        L = BinLayout();
+        L.S = S;
+        L.LL = LL;
+        B.long_rows = 0;
+        if (LL > 0) {
+            SPMV_RETURN_IF(bin_long_prep_device(p, d_rp, d_col, rp, L, D));
+            B.long_rows = (int64_t)D.lrows.size();
+        }
+        bin_mo_resolve(B, o, LL, p->nnz);
+        SPMV_RETURN_IF(bin_rows(p, rp.data(), p->m, p->n, L));
+        bstart.assign((size_t)L.NB + 1, 0);
+        for (int64_t b = 0; b <= L.NB; ++b) bstart[(size_t)b] = rp[(size_t)L.row0[(size_t)b]];
+        const int st = bin_count_device(p, d_rp, d_col, L.row0, bstart, L.S, LL, L.cnt);
+        if (st != SPMV_SUCCESS) return st;  // kBinNeedHostBuild: unsorted rows
+        if (LL > 0) bin_long_count_device(L, D);
+        bin_offsets(p, o, L);
+        if (LL > 0 && L.TRASH + L.PAD > kBinLongPosLimit) {
+            LL = 0;
+            continue;
+        }
+        break;
+    }
     std::vector<int64_t>().swap(rp);
-    const int st = bin_count_device(p, d_rp, d_col, L.row0, bstart, L.S, L.cnt);
-    if (st != SPMV_SUCCESS) return st;  // kBinNeedHostBuild: unsorted rows
-    bin_offsets(p, o, L);
     SPMV_RETURN_IF(bin_fill_device(p, d_rp, d_col, d_val, L.row0, bstart, L.cnt, L.off1, L.off2, L.run_off,
-                                   L.srun_off, L.S, L.E, L.ES));
+                                   L.srun_off, L.S, L.E, L.ES, LL, LL > 0 ? L.E1 : L.E,
+                                   (int32_t)(L.TRASH >> B.pad_log)));
+    if (LL > 0) {
+        BinLongRuns LR;
+        bin_long_runs_table(L, D, LR);
+        D = BinDevLong();
+        SPMV_RETURN_IF(bin_long_fill_device(p, d_col, d_val, LR, L.lb_off, L.lpad, L.lstart, L.lcode_off, L.run_off,
+                                            L.srun_off, (B.n_blocks - 1) * L.NB, L.TRASH));
+        std::vector<int64_t> lshift((size_t)S);
+        for (int64_t t = 0; t < S; ++t) lshift[(size_t)t] = L.lcode_off[(size_t)t] - L.lstart[(size_t)t];
+        SPMV_RETURN_IF(upload_vec(p, &B.lstart, L.lstart));
+        SPMV_RETURN_IF(upload_vec(p, &B.lshift, lshift));
+    }
     if (B.mo) {  // the chunk table needs only the layout
         std::vector<int32_t> tab;
         bin_mo_table(B, L, tab);

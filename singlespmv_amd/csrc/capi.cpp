@@ -79,8 +79,7 @@ constexpr int64_t kDeviceBuildMinNnz = (int64_t)1 << 24;
 static int create_from_csr(const HostCsr &A, const spmv_options_t *opt_in, spmv_plan_t *out);
 
 // spmv_plan_create_csr_device's body.  A plan whose format the device
-// builders do not make (BIN rows out of column order or with the long-row run
-// path; CSS from 2^31 entries) is built by the host builders: from a D2H copy of the CSR, or --
+// builders do not make (BIN rows out of column order; CSS from 2^31 entries) is built by the host builders: from a D2H copy of the CSR, or --
 // when need_host_fmt is given (create_via_device, whose caller still holds the
 // host CSR) -- by returning kNeedHostBuild with the resolved options there
 // (format chosen, crs_exact's rewrites applied, build = HOST).
@@ -292,7 +291,7 @@ static int create_from_csr(const HostCsr &A, const spmv_options_t *opt_in, spmv_
     SPMV_RETURN_IF(check_device(dev));
     SPMV_HIP_TRY(hipSetDevice(dev));
     // the device builders make every format (BIN only for rows in column
-    // order without the long-row run path, CSS below 2^31 entries): the rest,
+    // strip order, CSS below 2^31 entries): the rest,
     // and a staging copy that does not fit, take the host builders below --
     // with the format AUTO resolved on the device
     if (o.build == SPMV_BUILD_DEVICE || (o.build == SPMV_BUILD_AUTO && A.nnz >= kDeviceBuildMinNnz)) {

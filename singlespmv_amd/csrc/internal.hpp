@@ -450,20 +450,39 @@ int build_css(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o);
 int build_coo(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o);
 int build_jds(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o);
 int build_bin(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o);  // build_bin.cpp
-// BIN from a device CSR (build_bin.cpp + k_bin_build.hip).  Returns
-// kBinNeedHostBuild when a row's column strips are not non-decreasing (the
-// caller then stages the CSR through the host builder).
+// BIN from a device CSR (build_bin.cpp + k_bin_build.hip), long rows
+// included.  Returns kBinNeedHostBuild when a row's column strips are not
+// non-decreasing (the caller then stages the CSR through the host builder).
 constexpr int kBinNeedHostBuild = -1000;
 int build_bin_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, const double *d_val,
                      const spmv_options_t &o);
 // k_bin_build.hip: bstart[b] = row_ptr[row0[b]] (first entry of each bin)
+// LL > 0: rows of >= LL entries take the run path and stay out of the segments
 int bin_count_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, const std::vector<int32_t> &row0,
-                     const std::vector<int64_t> &bstart, int64_t S, std::vector<int32_t> &cnt);
+                     const std::vector<int64_t> &bstart, int64_t S, int64_t LL, std::vector<int32_t> &cnt);
 int bin_fill_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, const double *d_val,
                     const std::vector<int32_t> &row0, const std::vector<int64_t> &bstart,
                     const std::vector<int32_t> &cnt, const std::vector<int64_t> &off1,
                     const std::vector<int64_t> &off2, const std::vector<int64_t> &run_off,
-                    const std::vector<int64_t> &srun_off, int64_t S, int64_t E, int64_t ES);
+                    const std::vector<int64_t> &srun_off, int64_t S, int64_t E, int64_t ES, int64_t LL, int64_t E1,
+                    int32_t dst_fill);
+// Long rows from a device CSR: each run is one long row's entries in one
+// strip (contiguous, the row's strips being non-decreasing).  The runs'
+// (strip, first entry) come to the host to lay out the long blocks; the
+// entries never do.  BinLongRuns: the runs sorted [strip][row], with their
+// offset in the strip's long block (q0), length, the row's slot in its bin,
+// the bin and the product position of the run's first piece (fpos).
+struct BinLongRuns {
+    std::vector<int64_t> j0, q0, fpos;
+    std::vector<int32_t> len, strip, slot, bin;
+};
+int bin_long_runs_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, const std::vector<int32_t> &lrows,
+                         std::vector<int64_t> &roff, std::vector<int32_t> &rstrip, std::vector<int64_t> &rbeg);
+int bin_long_fill_device(spmv_plan_s *p, const int32_t *d_col, const double *d_val, const BinLongRuns &LR,
+                         const std::vector<int64_t> &lb_off, const std::vector<int64_t> &lpad,
+                         const std::vector<int64_t> &lstart, const std::vector<int64_t> &lcode_off,
+                         const std::vector<int64_t> &run_off, const std::vector<int64_t> &srun_off, int64_t lrun0,
+                         int64_t trash);
 // k_convert.hip -- device-input builders (the CSR already lives in HBM).
 int validate_csr_device(const int64_t *d_rp, int64_t m, const int32_t *d_col, int64_t nnz, int64_t n);
 int widen_row_ptr_device(const int32_t *d_rp32, int64_t m, int64_t **d_rp64);  // hipMalloc'd; caller frees

@@ -39,6 +39,11 @@ __device__ __forceinline__ int64_t upper_idx(const int64_t *__restrict__ a, int6
     return lo;
 }
 
+// a long row (>= LL entries, LL > 0) takes the run path, not the segments
+__device__ __forceinline__ bool is_long(const int64_t *__restrict__ rp, int64_t r, int64_t LL) {
+    return LL > 0 && rp[r + 1] - rp[r] >= LL;
+}
+
 struct EntryPos {
     int64_t b, r;
 };
@@ -54,11 +59,12 @@ __device__ __forceinline__ EntryPos locate(int64_t j, const int64_t *__restrict_
 __global__ __launch_bounds__(256) void bin_count_kernel(const int64_t *__restrict__ rp, const int32_t *__restrict__ col,
                                                         int64_t nnz, const int64_t *__restrict__ bstart, int64_t NB,
                                                         const int32_t *__restrict__ row0, int32_t C, int64_t S,
-                                                        int32_t *__restrict__ cnt, unsigned *__restrict__ bad) {
+                                                        int64_t LL, int32_t *__restrict__ cnt,
+                                                        unsigned *__restrict__ bad) {
     for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < nnz; j += (int64_t)gridDim.x * 256) {
         const EntryPos e = locate(j, rp, bstart, NB, row0);
         const int32_t t = col[j] / C;
-        atomicAdd(&cnt[e.b * S + t], 1);
+        if (!is_long(rp, e.r, LL)) atomicAdd(&cnt[e.b * S + t], 1);
         if (j > rp[e.r] && col[j - 1] / C > t) atomicOr(bad, 1u);
     }
 }
@@ -79,10 +85,11 @@ __device__ __forceinline__ int64_t entry_k(int64_t j, int64_t r, int32_t t, int3
 __global__ __launch_bounds__(256) void bin_khist_kernel(const int64_t *__restrict__ rp, const int32_t *__restrict__ col,
                                                         int64_t nnz, const int64_t *__restrict__ bstart, int64_t NB,
                                                         const int32_t *__restrict__ row0, int32_t C, int64_t S,
-                                                        const int64_t *__restrict__ off2,
+                                                        const int64_t *__restrict__ off2, int64_t LL,
                                                         unsigned long long *__restrict__ kh) {
     for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < nnz; j += (int64_t)gridDim.x * 256) {
         const EntryPos e = locate(j, rp, bstart, NB, row0);
+        if (is_long(rp, e.r, LL)) continue;
         const int32_t t = col[j] / C;
         const int64_t k = entry_k(j, e.r, t, C, rp, col);
         atomicAdd(&kh[off2[e.b * S + t] + k], 1ull);
@@ -94,10 +101,11 @@ __global__ __launch_bounds__(256) void bin_place_kernel(
     const int64_t *__restrict__ bstart, int64_t NB, const int32_t *__restrict__ row0, int32_t C, int64_t S,
     const int64_t *__restrict__ off1, const int64_t *__restrict__ off2, const int64_t *__restrict__ ks,
     unsigned long long *__restrict__ cur, const int64_t *__restrict__ pbb, int pad_log,
-    const int64_t *__restrict__ run_off, const int64_t *__restrict__ srun_off, int64_t SB, int sum_u,
+    const int64_t *__restrict__ run_off, const int64_t *__restrict__ srun_off, int64_t SB, int sum_u, int64_t LL,
     double *__restrict__ val1, uint16_t *__restrict__ cs1, uint16_t *__restrict__ slot2, int32_t *__restrict__ dst1) {
     for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < nnz; j += (int64_t)gridDim.x * 256) {
         const EntryPos e = locate(j, rp, bstart, NB, row0);
+        if (is_long(rp, e.r, LL)) continue;
         const int32_t c = col[j];
         const int32_t t = c / C;
         const int64_t k = entry_k(j, e.r, t, C, rp, col);
@@ -131,6 +139,86 @@ __global__ __launch_bounds__(256) void bin_pad_kernel(const int32_t *__restrict_
 
 __global__ __launch_bounds__(256) void fill_u16_kernel(uint16_t *__restrict__ a, int64_t n, uint16_t v) {
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) a[i] = v;
+}
+
+__global__ __launch_bounds__(256) void fill_i32_kernel(int32_t *__restrict__ a, int64_t n, int32_t v) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) a[i] = v;
+}
+
+// ---- long rows (the run path, internal.hpp BinDev) ----------------------
+// one wave per long row: its runs, the maximal ranges of entries in one
+// strip (a row's strips are non-decreasing, so a (row, strip) pair is one
+// contiguous range).  roff == nullptr: count them into nruns; else write
+// each run's strip and first entry at the row's offset roff[i].
+__global__ __launch_bounds__(256) void bin_long_runs_kernel(int64_t nl, const int32_t *__restrict__ lrows,
+                                                            const int64_t *__restrict__ rp,
+                                                            const int32_t *__restrict__ col, int32_t C,
+                                                            const int64_t *__restrict__ roff,
+                                                            int32_t *__restrict__ nruns,
+                                                            int32_t *__restrict__ rstrip,
+                                                            int64_t *__restrict__ rbeg) {
+    const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (i >= nl) return;
+    const int64_t r = lrows[i], a = rp[r], z = rp[r + 1];
+    int64_t k = roff ? roff[i] : 0;
+    for (int64_t j0 = a; j0 < z; j0 += 64) {
+        const int64_t j = j0 + lane;
+        int32_t t = 0;
+        bool st = false;
+        if (j < z) {
+            t = col[j] / C;
+            st = j == a || col[j - 1] / C != t;
+        }
+        const uint64_t m = __ballot(st);
+        if (roff && st) {
+            const int64_t q = k + __popcll(m & ((1ull << lane) - 1));
+            rstrip[q] = t;
+            rbeg[q] = j;
+        }
+        k += __popcll(m);
+    }
+    if (!roff && lane == 0) nruns[i] = (int32_t)k;
+}
+
+// one wave per run (sorted [strip][row], BinLongRuns): its entries into the
+// strip's long block, lcode = piece start bit | (last entry of its piece ?
+// the piece's product position : 0x7FFFFFFF); pieces start at the run's
+// first entry and at every 64-entry boundary of the block, and number on
+// from the run's first piece (fpos); each piece's slot in its bin's long run
+__global__ __launch_bounds__(256) void bin_long_fill_kernel(
+    int64_t R, const int64_t *__restrict__ j0, const int32_t *__restrict__ len, const int32_t *__restrict__ strip,
+    const int32_t *__restrict__ slot, const int32_t *__restrict__ bin, const int64_t *__restrict__ q0,
+    const int64_t *__restrict__ fpos, const int32_t *__restrict__ col, const double *__restrict__ val, int32_t C,
+    const int64_t *__restrict__ lstart, const int64_t *__restrict__ lcode_off, const int64_t *__restrict__ run_off,
+    const int64_t *__restrict__ srun_off, int64_t lrun0, int sum_u, double *__restrict__ val1,
+    uint16_t *__restrict__ cs1, int32_t *__restrict__ lcode, uint16_t *__restrict__ slot2) {
+    const int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (g >= R) return;
+    const int64_t a = j0[g], q = q0[g], n = len[g], fp = fpos[g];
+    const int32_t t = strip[g];
+    const int64_t ms = lstart[t], cs = lcode_off[t], run = lrun0 + bin[g];
+    for (int64_t i = lane; i < n; i += 64) {
+        const int64_t p2 = q + i;
+        const bool start = i == 0 || (p2 & 63) == 0;
+        const bool end = i + 1 == n || ((p2 + 1) & 63) == 0;
+        const int64_t pos = fp + (p2 >> 6) - (q >> 6);
+        val1[ms + p2] = val[a + i];
+        cs1[ms + p2] = (uint16_t)(col[a + i] - t * C);
+        lcode[cs + p2] = (int32_t)((start ? 0x80000000u : 0u) | (end ? (uint32_t)pos : 0x7FFFFFFFu));
+        if (start) slot2[bin_slot_index(pos, run_off[run], srun_off[run], sum_u)] = (uint16_t)slot[g];
+    }
+}
+
+// padding lanes of each strip's long block: their own piece, to the trash line
+__global__ __launch_bounds__(256) void bin_long_pad_kernel(int64_t S, const int64_t *__restrict__ lb_off,
+                                                           const int64_t *__restrict__ lpad,
+                                                           const int64_t *__restrict__ lcode_off, int32_t trash,
+                                                           int32_t *__restrict__ lcode) {
+    for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < S; t += (int64_t)gridDim.x * 256)
+        for (int64_t p2 = lb_off[t + 1] - lb_off[t]; p2 < lpad[t]; ++p2)
+            lcode[lcode_off[t] + p2] = (int32_t)(0x80000000u | (uint32_t)trash);
 }
 
 // hipMalloc'd scratch, freed (after the stream drains) on every exit path
@@ -174,7 +262,7 @@ int finish(hipStream_t st, const char *what) {
 }  // namespace
 
 int bin_count_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, const std::vector<int32_t> &row0,
-                     const std::vector<int64_t> &bstart, int64_t S, std::vector<int32_t> &cnt) {
+                     const std::vector<int64_t> &bstart, int64_t S, int64_t LL, std::vector<int32_t> &cnt) {
     const hipStream_t st = p->stream;
     const int64_t NB = (int64_t)row0.size() - 1;
     Scratch sc{st, {}};
@@ -188,7 +276,7 @@ int bin_count_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, 
     SPMV_HIP_TRY(hipMemsetAsync(d_cnt, 0, sizeof(int32_t) * (size_t)(NB * S), st));
     SPMV_HIP_TRY(hipMemsetAsync(d_bad, 0, sizeof(unsigned), st));
     hipLaunchKernelGGL(bin_count_kernel, dim3(grid_of(p->nnz)), dim3(256), 0, st, d_rp, d_col, p->nnz, d_bstart, NB,
-                       d_row0, (int32_t)p->bin.strip, S, d_cnt, d_bad);
+                       d_row0, (int32_t)p->bin.strip, S, LL, d_cnt, d_bad);
     SPMV_RETURN_IF(finish(st, "counts"));
     unsigned bad = 0;
     cnt.assign((size_t)(NB * S), 0);
@@ -201,7 +289,8 @@ int bin_fill_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, c
                     const std::vector<int32_t> &row0, const std::vector<int64_t> &bstart,
                     const std::vector<int32_t> &cnt, const std::vector<int64_t> &off1,
                     const std::vector<int64_t> &off2, const std::vector<int64_t> &run_off,
-                    const std::vector<int64_t> &srun_off, int64_t S, int64_t E, int64_t ES) {
+                    const std::vector<int64_t> &srun_off, int64_t S, int64_t E, int64_t ES, int64_t LL, int64_t E1,
+                    int32_t dst_fill) {
     BinDev &B = p->bin;
     const hipStream_t st = p->stream;
     const int64_t NB = (int64_t)row0.size() - 1, C = B.strip;
@@ -212,21 +301,29 @@ int bin_fill_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, c
         for (int g = 0; g < B.G; ++g)
             for (int64_t b = B.g_bin[(size_t)g]; b < B.g_bin[(size_t)g + 1]; ++b) pbb[(size_t)b] = B.g_prod[(size_t)g];
     void *q;
-    // val1 / cs1 / dst1 with the Mul's unclamped-batch slack (kBinMulSlack), zeroed
-    // (Mul order: the entries fill [0, nnz) unpadded, the rest is slack)
-    const int64_t Ez = B.mo ? p->nnz : E;
-    SPMV_RETURN_IF(p->arena.alloc(&q, sizeof(double) * (size_t)(E + kBinMulSlack)));
+    // val1 / cs1 / dst1 over the Mul positions [0, E1) with the Mul's
+    // unclamped-batch slack (kBinMulSlack), zeroed past the entries (Mul
+    // order: the entries fill [0, nnz) unpadded, the rest is slack).  With
+    // long rows the Mul positions hold voids and long blocks too: all zeroed
+    // first, and every destination group points at the trash line (dst_fill)
+    // until a segment claims it -- as the host fill leaves them.
+    const int64_t Ez = LL > 0 ? 0 : B.mo ? p->nnz : E;
+    SPMV_RETURN_IF(p->arena.alloc(&q, sizeof(double) * (size_t)(E1 + kBinMulSlack)));
     B.val1 = (double *)q;
-    SPMV_HIP_TRY(hipMemsetAsync(B.val1 + Ez, 0, sizeof(double) * (size_t)(E - Ez + kBinMulSlack), st));
-    SPMV_RETURN_IF(p->arena.alloc(&q, sizeof(uint16_t) * (size_t)(E + kBinMulSlack)));
+    SPMV_HIP_TRY(hipMemsetAsync(B.val1 + Ez, 0, sizeof(double) * (size_t)(E1 - Ez + kBinMulSlack), st));
+    SPMV_RETURN_IF(p->arena.alloc(&q, sizeof(uint16_t) * (size_t)(E1 + kBinMulSlack)));
     B.cs1 = (uint16_t *)q;
-    SPMV_HIP_TRY(hipMemsetAsync(B.cs1 + Ez, 0, sizeof(uint16_t) * (size_t)(E - Ez + kBinMulSlack), st));
+    SPMV_HIP_TRY(hipMemsetAsync(B.cs1 + Ez, 0, sizeof(uint16_t) * (size_t)(E1 - Ez + kBinMulSlack), st));
     SPMV_RETURN_IF(p->arena.alloc(&q, sizeof(uint16_t) * (size_t)std::max<int64_t>(ES, 1)));
     B.slot2 = (uint16_t *)q;
     if (!B.mo) {  // Mul-ordered products need no destinations
-        SPMV_RETURN_IF(p->arena.alloc(&q, sizeof(int32_t) * (size_t)std::max<int64_t>((E + kBinMulSlack) >> B.pad_log, 1)));
+        const int64_t nd = (E1 + kBinMulSlack) >> B.pad_log;
+        SPMV_RETURN_IF(p->arena.alloc(&q, sizeof(int32_t) * (size_t)std::max<int64_t>(nd, 1)));
         B.dst1 = (int32_t *)q;
-        SPMV_HIP_TRY(hipMemsetAsync(B.dst1 + (E >> B.pad_log), 0, sizeof(int32_t) * (size_t)(kBinMulSlack >> B.pad_log), st));
+        if (LL > 0)
+            hipLaunchKernelGGL(fill_i32_kernel, dim3(grid_of(nd)), dim3(256), 0, st, B.dst1, nd, dst_fill);
+        else
+            SPMV_HIP_TRY(hipMemsetAsync(B.dst1 + (E >> B.pad_log), 0, sizeof(int32_t) * (size_t)(kBinMulSlack >> B.pad_log), st));
     }
     Scratch sc{st, {}};
     int32_t *d_row0, *d_cnt;
@@ -248,17 +345,84 @@ int bin_fill_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, c
     SPMV_HIP_TRY(hipMemsetAsync(d_kh, 0, 8 * (size_t)E, st));
     const unsigned grid = grid_of(p->nnz);
     hipLaunchKernelGGL(bin_khist_kernel, dim3(grid), dim3(256), 0, st, d_rp, d_col, p->nnz, d_bstart, NB, d_row0,
-                       (int32_t)C, S, d_off2, d_kh);
+                       (int32_t)C, S, d_off2, LL, d_kh);
     SPMV_RETURN_IF(exclusive_scan_i64((const int64_t *)d_kh, d_ks, E, st, sc.v));
     SPMV_HIP_TRY(hipMemsetAsync(d_kh, 0, 8 * (size_t)E, st));  // now the k-run cursors
     hipLaunchKernelGGL(bin_place_kernel, dim3(grid), dim3(256), 0, st, d_rp, d_col, d_val, p->nnz, d_bstart, NB,
                        d_row0, (int32_t)C, S, d_off1, d_off2, d_ks, d_kh, d_pbb, B.pad_log, d_run, d_srun,
-                       B.strip_block, B.sum_u, B.val1, B.cs1, B.slot2,
-                       B.dst1);
+                       B.strip_block, B.sum_u, LL, B.val1, B.cs1, B.slot2, B.dst1);
     if (!B.mo)  // (Mul order: the Mul's segments are not padded)
         hipLaunchKernelGGL(bin_pad_kernel, dim3(grid_of(NB * S)), dim3(256), 0, st, d_cnt, NB * S, d_off1, B.pad_log,
                            B.val1, B.cs1);
     return finish(st, "fill");
+}
+
+int bin_long_runs_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, const std::vector<int32_t> &lrows,
+                         std::vector<int64_t> &roff, std::vector<int32_t> &rstrip, std::vector<int64_t> &rbeg) {
+    const hipStream_t st = p->stream;
+    const int64_t nl = (int64_t)lrows.size();
+    const unsigned grid = (unsigned)std::max<int64_t>(1, (nl + 3) / 4);
+    Scratch sc{st, {}};
+    int32_t *d_lrows, *d_n, *d_strip;
+    int64_t *d_roff, *d_beg;
+    SPMV_RETURN_IF(sc.upload(&d_lrows, lrows));
+    SPMV_RETURN_IF(sc.alloc(&d_n, (size_t)nl));
+    hipLaunchKernelGGL(bin_long_runs_kernel, dim3(grid), dim3(256), 0, st, nl, d_lrows, d_rp, d_col,
+                       (int32_t)p->bin.strip, (const int64_t *)nullptr, d_n, (int32_t *)nullptr, (int64_t *)nullptr);
+    SPMV_RETURN_IF(finish(st, "long-row runs"));
+    std::vector<int32_t> n((size_t)nl);
+    SPMV_HIP_TRY(hipMemcpy(n.data(), d_n, sizeof(int32_t) * (size_t)nl, hipMemcpyDeviceToHost));
+    roff.assign((size_t)nl + 1, 0);
+    for (int64_t i = 0; i < nl; ++i) roff[(size_t)i + 1] = roff[(size_t)i] + n[(size_t)i];
+    const int64_t R = roff[(size_t)nl];
+    SPMV_RETURN_IF(sc.upload(&d_roff, roff));
+    SPMV_RETURN_IF(sc.alloc(&d_strip, (size_t)R));
+    SPMV_RETURN_IF(sc.alloc(&d_beg, (size_t)R));
+    hipLaunchKernelGGL(bin_long_runs_kernel, dim3(grid), dim3(256), 0, st, nl, d_lrows, d_rp, d_col,
+                       (int32_t)p->bin.strip, (const int64_t *)d_roff, d_n, d_strip, d_beg);
+    SPMV_RETURN_IF(finish(st, "long-row runs"));
+    rstrip.resize((size_t)R);
+    rbeg.resize((size_t)R);
+    SPMV_HIP_TRY(hipMemcpy(rstrip.data(), d_strip, sizeof(int32_t) * (size_t)R, hipMemcpyDeviceToHost));
+    SPMV_HIP_TRY(hipMemcpy(rbeg.data(), d_beg, sizeof(int64_t) * (size_t)R, hipMemcpyDeviceToHost));
+    return SPMV_SUCCESS;
+}
+
+int bin_long_fill_device(spmv_plan_s *p, const int32_t *d_col, const double *d_val, const BinLongRuns &LR,
+                         const std::vector<int64_t> &lb_off, const std::vector<int64_t> &lpad,
+                         const std::vector<int64_t> &lstart, const std::vector<int64_t> &lcode_off,
+                         const std::vector<int64_t> &run_off, const std::vector<int64_t> &srun_off, int64_t lrun0,
+                         int64_t trash) {
+    BinDev &B = p->bin;
+    const hipStream_t st = p->stream;
+    const int64_t S = (int64_t)lpad.size(), R = (int64_t)LR.j0.size();
+    void *q;
+    const int64_t ncode = lcode_off.back() + lpad.back();
+    SPMV_RETURN_IF(p->arena.alloc(&q, sizeof(int32_t) * (size_t)std::max<int64_t>(ncode, 1)));
+    B.lcode = (int32_t *)q;
+    Scratch sc{st, {}};
+    int64_t *d_j0, *d_q0, *d_fpos, *d_lb, *d_lpad, *d_lstart, *d_lco, *d_run, *d_srun;
+    int32_t *d_len, *d_strip, *d_slot, *d_bin;
+    SPMV_RETURN_IF(sc.upload(&d_j0, LR.j0));
+    SPMV_RETURN_IF(sc.upload(&d_q0, LR.q0));
+    SPMV_RETURN_IF(sc.upload(&d_fpos, LR.fpos));
+    SPMV_RETURN_IF(sc.upload(&d_len, LR.len));
+    SPMV_RETURN_IF(sc.upload(&d_strip, LR.strip));
+    SPMV_RETURN_IF(sc.upload(&d_slot, LR.slot));
+    SPMV_RETURN_IF(sc.upload(&d_bin, LR.bin));
+    SPMV_RETURN_IF(sc.upload(&d_lb, lb_off));
+    SPMV_RETURN_IF(sc.upload(&d_lpad, lpad));
+    SPMV_RETURN_IF(sc.upload(&d_lstart, lstart));
+    SPMV_RETURN_IF(sc.upload(&d_lco, lcode_off));
+    SPMV_RETURN_IF(sc.upload(&d_run, run_off));
+    SPMV_RETURN_IF(sc.upload(&d_srun, srun_off));
+    if (R > 0)
+        hipLaunchKernelGGL(bin_long_fill_kernel, dim3((unsigned)std::max<int64_t>(1, (R + 3) / 4)), dim3(256), 0, st, R,
+                           d_j0, d_len, d_strip, d_slot, d_bin, d_q0, d_fpos, d_col, d_val, (int32_t)B.strip, d_lstart,
+                           d_lco, d_run, d_srun, lrun0, B.sum_u, B.val1, B.cs1, B.lcode, B.slot2);
+    hipLaunchKernelGGL(bin_long_pad_kernel, dim3(grid_of(S)), dim3(256), 0, st, S, d_lb, d_lpad, d_lco, (int32_t)trash,
+                       B.lcode);
+    return finish(st, "long rows");
 }
 
 }  // namespace spmv

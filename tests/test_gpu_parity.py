@@ -706,8 +706,8 @@ def test_host_csr_build_routing():
     """spmv_options_t::build: a host CSR of >= 2^24 entries (AUTO) or any
     size (DEVICE) is staged into HBM and built by the device builders -- the
     host builder's layout byte for byte and the same y; BIN on rows out of
-    column order or with the long-row run path takes the host builders with
-    the format resolved on the device; small CSRs under AUTO stay on the host
+    column order takes the host builders with the format resolved on the
+    device; small CSRs under AUTO stay on the host
     builders."""
     import torch
     # large: 1 M rows x 17 entries = 17 M entries, AUTO -> BIN (x too wide
@@ -747,15 +747,8 @@ def test_host_csr_build_routing():
             inner = rp2[1:-1]
             dec[inner[(inner > 0) & (inner < len(col2))] - 1] = False  # ... inside one row
             sorted_rows = not dec.any()  # BIN's device fill wants each row's strips in order
-            # BIN's long-row run path is laid out on the host (build_bin.cpp
-            # bin_long_threshold with the default options)
-            lens2 = np.diff(rp2)
-            S = max(1, -(-n // 20480))
-            lnnz = int(lens2[lens2 >= max(128, S)].sum())
-            nnz2 = int(rp2[-1])
-            long_rows = lnnz > 0 and lnnz * 20 >= nnz2 and nnz2 + nnz2 // 2 + (S << 6) < (1 << 31)
             got = ph.info()["format"]  # AUTO resolves alike on the host and the device
-            expect_dev = got != "bin" or (sorted_rows and not long_rows)
+            expect_dev = got != "bin" or sorted_rows
             assert pd.built_on_device() == expect_dev, (name, fmt)
             if ph.info()["format"] != "bin":
                 assert pd.digest() == ph.digest(), (name, fmt)
@@ -919,6 +912,12 @@ def test_auto_format_choice():
 
 
 # ---------------------------------------------------------------- BIN
+# plan info fields that fix a BIN layout (host and device builds must agree)
+BIN_LAYOUT_KEYS = ("format", "stored_slots", "bin_bins", "bin_strips", "bin_pad", "bin_groups", "bin_product_order",
+                   "bin_sum_entries", "bin_long_len", "bin_long_rows", "bin_long_pieces", "bin_long_entries",
+                   "bin_products")
+
+
 def _bin_matrix(kind, m, n, seed):
     if kind == "empty_rows":
         spec = sp.gen_spec("powerlaw", m, n, max_len=700, seed=seed)
@@ -977,6 +976,16 @@ def test_bin_long_rows_run_path(long_len, opts):
     assert info["bin_long_pieces"] >= runs
     y = run_plan(plan, x, m)
     assert_bin_rows(plan, y, rp, col, val, x, what=f"long_len {long_len} {opts}")
+    # the same plan from a device CSR: the long blocks laid out from the
+    # rows' runs (k_bin_build.hip), the same layout, y bit-identical
+    import torch
+    pd = sp.Plan.from_device_csr(m, n, torch.from_numpy(rp).cuda(), torch.from_numpy(col).cuda(),
+                                 torch.from_numpy(val).cuda(), "bin", bin_long_len=long_len, **opts)
+    assert pd.built_on_device()
+    idv = pd.info()
+    for k in BIN_LAYOUT_KEYS:
+        assert idv[k] == info[k], (long_len, opts, k, info[k], idv[k])
+    assert np.array_equal(run_plan(pd, x, m), y), f"device long_len {long_len} {opts}"
     again = sp.Plan.from_csr(m, n, rp, col, val, "bin", bin_long_len=long_len, **opts)
     assert np.array_equal(run_plan(again, x, m), y)
     # signed values: the partials still meet the 1e-12 bound of sum |a x|
@@ -1238,10 +1247,11 @@ def test_bin_empty_bins_between_full_ones(sum_waves):
 
 @pytest.mark.parametrize("opts", [{}, {"bin_strip_cols": 3001}, {"bin_groups": 3}, {"bin_product_order": 1}])
 def test_bin_device_build(opts, monkeypatch):
-    """spmv_plan_create_csr_device with BIN: the segments are counted, laid
-    out and filled on the GPU (k_bin_build.hip).  Same bins / strips / slots
-    as the host builder and y bit-identical to it and to the oracle; rows
-    whose column strips are not ascending stage through the host builder."""
+    """spmv_plan_create_csr_device with BIN: the segments (and the long rows'
+    run path) are counted, laid out and filled on the GPU (k_bin_build.hip).
+    Same bins / strips / slots / pieces as the host builder and y
+    bit-identical to it and to the oracle; rows whose column strips are not
+    ascending stage through the host builder."""
     import torch
     cases = [("uniform", 40_000, 40_000), ("powerlaw", 30_011, 100_003), ("empty_rows", 70_001, 9_000),
              ("uniform", 5, 3), ("powerlaw", 1, 70_000)]
@@ -1253,8 +1263,8 @@ def test_bin_device_build(opts, monkeypatch):
         pd = sp.Plan.from_device_csr(m, n, torch.from_numpy(rp).cuda(), torch.from_numpy(col).cuda(),
                                      torch.from_numpy(val).cuda(), "bin", **opts)
         ih, idv = ph.info(), pd.info()
-        for k in ("format", "stored_slots", "bin_bins", "bin_strips", "bin_pad", "bin_groups", "bin_product_order",
-                  "bin_sum_entries"):
+        assert pd.built_on_device() and not ph.built_on_device()
+        for k in BIN_LAYOUT_KEYS:
             assert ih[k] == idv[k], (kind, m, n, k, ih[k], idv[k])
         yd = run_plan(pd, x, m)
         assert np.array_equal(yd, run_plan(ph, x, m)), f"{kind} {m}x{n} {opts}"
@@ -1268,6 +1278,7 @@ def test_bin_device_build(opts, monkeypatch):
     pd = sp.Plan.from_device_csr(50_000, 50_000, torch.from_numpy(rp).cuda(), torch.from_numpy(col).cuda(),
                                  torch.from_numpy(val).cuda(), "bin", **opts)
     ph = sp.Plan.from_csr(50_000, 50_000, rp, col, val, "bin", **opts)
+    assert not pd.built_on_device()
     yd = run_plan(pd, x, 50_000)
     assert np.array_equal(yd, run_plan(ph, x, 50_000))
     # BIN adds a row's strips in strip order: with unsorted columns that is
