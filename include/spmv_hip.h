@@ -225,7 +225,7 @@ int spmv_plan_create_csr32(int32_t m, int32_t n, int32_t nnz, const int32_t *row
  * that depend on row lengths alone; AUTO is resolved there too, its diagonal
  * census run on the device; CSS's per-wave column sorts are one segmented
  * sort.  The layouts are byte-identical to the host builders'
- * (spmv_plan_digest; BIN: the same layout sizes and y bit for bit).  BIN when
+ * (spmv_plan_digest).  BIN when
  * some row's columns are not ascending by 20480-column strip, and CSS from
  * 2^31 entries, copy the CSR to the host and take the host builder.  The input is validated on the device like
  * spmv_plan_create_csr's host check. */
@@ -386,8 +386,8 @@ int spmv_plan_info(spmv_plan_t plan, spmv_plan_info_t *info);
  * of one matrix -- e.g. a host build and a device build -- can be compared
  * array by array without copying them out.  *n_arrays = the plan's array
  * count (digests beyond `cap` are not written); spmv_plan_digest_name(plan,
- * k) names array k.  CSR, ELL, HYB, JDS, SS, DIA, COO and CSS plans; BIN
- * returns SPMV_ERROR_NOT_SUPPORTED. */
+ * k) names array k.  Every format (BIN: its entry, slot, destination and
+ * run-path arrays and the small tables; not the product scratch). */
 int spmv_plan_digest(spmv_plan_t plan, uint64_t *digests, int32_t cap, int32_t *n_arrays);
 const char *spmv_plan_digest_name(spmv_plan_t plan, int32_t k);
 

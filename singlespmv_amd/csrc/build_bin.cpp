@@ -826,6 +826,7 @@ static int bin_finish(spmv_plan_s *p, int64_t n, const BinLayout &L, const spmv_
     if (B.mo) p->kernel_name = "bin_mul_kernel+bin_sum_bin_kernel";  // the Mul-ordered Sum
     p->stored_slots = L.E1;
     B.mul_entries = L.E1;
+    B.slot_entries = L.ES;
     B.long_pieces = L.NP;
     B.long_entries = 0;
     for (int64_t v : L.lpad) B.long_entries += v;
@@ -1056,7 +1057,7 @@ int build_bin_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, 
     }
     std::vector<int64_t>().swap(rp);
     SPMV_RETURN_IF(bin_fill_device(p, d_rp, d_col, d_val, L.row0, bstart, L.cnt, L.off1, L.off2, L.run_off,
-                                   L.srun_off, L.S, L.E, L.ES, LL, LL > 0 ? L.E1 : L.E,
+                                   L.srun_off, L.S, L.E, L.ES, LL, L.E1,
                                    (int32_t)(L.TRASH >> B.pad_log)));
     if (LL > 0) {
         BinLongRuns LR;

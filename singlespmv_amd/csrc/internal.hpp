@@ -391,6 +391,7 @@ struct BinDev {
     int64_t long_len = 0;         // rows with >= long_len entries take the run path (0: none)
     int64_t long_rows = 0, long_pieces = 0, long_entries = 0;
     int64_t mul_entries = 0;      // Mul-order length (segments + voids + long blocks)
+    int64_t slot_entries = 0;     // slot2 length (every slot run padded to whole Sum batches)
     int64_t *lstart = nullptr;    // [n_strips]: Mul position where the strip's long blocks start
     int64_t *lshift = nullptr;    // [n_strips]: lcode index - Mul position in those blocks
     int32_t *lcode = nullptr;     // per long-block entry: piece start bit | product position

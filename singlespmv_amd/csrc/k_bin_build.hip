@@ -2,21 +2,25 @@
 // build_bin.cpp drives it).  The OptimizeProblem counterpart is opt_ss's
 // host-side segment build (src/opt_ss.cpp:52-142); here a 1 G-entry matrix
 // never round-trips through the host: only the row pointers (to cut the row
-// bins) and the (bin, strip) entry counts (to lay out the segments) visit it.
+// bins), the (bin, strip) entry counts (to lay out the segments) and the long
+// rows' runs visit it.
 //
-// One thread per CSR entry j throughout:
+// One thread per CSR entry j:
 //   bin   b = last bin whose first entry <= j     (binary search, NB + 1 starts)
 //   row   r = last row of b whose first entry <= j (binary search in row_ptr)
 //   strip t = col[j] / C
 //   k       = ordinal of j among row r's entries in strip t
 //             (= j - first entry of r in strip t; rows must have
 //              non-decreasing strips, checked by bin_count_kernel)
-// Phases: counts per (b, t) -> [host offsets] -> k-run sizes per segment
-// (atomicAdd) -> exclusive scan -> placement (atomic cursor per k-run) ->
-// padding.  Inside one k-run rows are placed in atomic-cursor order rather
-// than ascending; every product of a row still reaches the Sum in column
-// order and no two entries of a k-run share a row, so y is bit-identical to
-// the host-built plan's (tests/test_gpu_parity.py::test_bin_device_build).
+// Phases: counts per (b, t) -> [host offsets] -> key off2(b, t) + k per
+// entry -> stable radix sort of (key, j) -> placement: the i-th sorted entry
+// sits at i - (entries of the earlier segments) in its segment -> padding.
+// Within a segment that is the host fill's order exactly -- k-runs ascending,
+// rows ascending inside a k-run (the sort is stable and j ascends with the
+// row) -- so the arrays are byte-identical to the host-built plan's
+// (spmv_plan_digest, tests/test_gpu_parity.py::test_bin_device_build).
+#include <hipcub/hipcub.hpp>
+
 #include <algorithm>
 #include <vector>
 
@@ -82,36 +86,44 @@ __device__ __forceinline__ int64_t entry_k(int64_t j, int64_t r, int32_t t, int3
     return j - lo;
 }
 
-__global__ __launch_bounds__(256) void bin_khist_kernel(const int64_t *__restrict__ rp, const int32_t *__restrict__ col,
-                                                        int64_t nnz, const int64_t *__restrict__ bstart, int64_t NB,
-                                                        const int32_t *__restrict__ row0, int32_t C, int64_t S,
-                                                        const int64_t *__restrict__ off2, int64_t LL,
-                                                        unsigned long long *__restrict__ kh) {
+// sort key of entry j: its (bin, strip) segment's Sum position + k (long
+// rows: `none`, past every segment); value: j
+template <typename K, typename V>
+__global__ __launch_bounds__(256) void bin_key_kernel(const int64_t *__restrict__ rp, const int32_t *__restrict__ col,
+                                                      int64_t nnz, const int64_t *__restrict__ bstart, int64_t NB,
+                                                      const int32_t *__restrict__ row0, int32_t C, int64_t S,
+                                                      const int64_t *__restrict__ off2, int64_t LL, K none,
+                                                      K *__restrict__ keys, V *__restrict__ vals) {
     for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < nnz; j += (int64_t)gridDim.x * 256) {
         const EntryPos e = locate(j, rp, bstart, NB, row0);
-        if (is_long(rp, e.r, LL)) continue;
-        const int32_t t = col[j] / C;
-        const int64_t k = entry_k(j, e.r, t, C, rp, col);
-        atomicAdd(&kh[off2[e.b * S + t] + k], 1ull);
+        K key = none;
+        if (!is_long(rp, e.r, LL)) {
+            const int32_t t = col[j] / C;
+            key = (K)(off2[e.b * S + t] + entry_k(j, e.r, t, C, rp, col));
+        }
+        keys[j] = key;
+        vals[j] = (V)j;
     }
 }
 
+// the i-th entry in key order (i < the segments' entries): position
+// i - cbase(segment) in its segment
+template <typename V>
 __global__ __launch_bounds__(256) void bin_place_kernel(
-    const int64_t *__restrict__ rp, const int32_t *__restrict__ col, const double *__restrict__ val, int64_t nnz,
-    const int64_t *__restrict__ bstart, int64_t NB, const int32_t *__restrict__ row0, int32_t C, int64_t S,
-    const int64_t *__restrict__ off1, const int64_t *__restrict__ off2, const int64_t *__restrict__ ks,
-    unsigned long long *__restrict__ cur, const int64_t *__restrict__ pbb, int pad_log,
-    const int64_t *__restrict__ run_off, const int64_t *__restrict__ srun_off, int64_t SB, int sum_u, int64_t LL,
+    const int64_t *__restrict__ rp, const int32_t *__restrict__ col, const double *__restrict__ val,
+    const V *__restrict__ order, int64_t n_seg_entries, const int64_t *__restrict__ bstart, int64_t NB,
+    const int32_t *__restrict__ row0, int32_t C, int64_t S, const int64_t *__restrict__ off1,
+    const int64_t *__restrict__ off2, const int64_t *__restrict__ cbase, const int64_t *__restrict__ pbb, int pad_log,
+    const int64_t *__restrict__ run_off, const int64_t *__restrict__ srun_off, int64_t SB, int sum_u,
     double *__restrict__ val1, uint16_t *__restrict__ cs1, uint16_t *__restrict__ slot2, int32_t *__restrict__ dst1) {
-    for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < nnz; j += (int64_t)gridDim.x * 256) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n_seg_entries; i += (int64_t)gridDim.x * 256) {
+        const int64_t j = (int64_t)order[i];
         const EntryPos e = locate(j, rp, bstart, NB, row0);
-        if (is_long(rp, e.r, LL)) continue;
         const int32_t c = col[j];
         const int32_t t = c / C;
-        const int64_t k = entry_k(j, e.r, t, C, rp, col);
         const int64_t seg = e.b * S + t;
         const int64_t o1 = off1[seg], o2 = off2[seg];
-        const int64_t pos = (ks[o2 + k] - ks[o2]) + (int64_t)atomicAdd(&cur[o2 + k], 1ull);
+        const int64_t pos = i - cbase[seg];
         val1[o1 + pos] = val[j];
         cs1[o1 + pos] = (uint16_t)(c - t * C);
         const int64_t run = (t / SB) * NB + e.b;
@@ -259,6 +271,48 @@ int finish(hipStream_t st, const char *what) {
     return SPMV_SUCCESS;
 }
 
+struct SortPlaceArgs {
+    const int64_t *rp;
+    const int32_t *col;
+    const double *val;
+    int64_t NB, S;
+    const int32_t *row0;
+    const int64_t *bstart, *off1, *off2, *cbase, *pbb, *run, *srun;
+    int64_t E, LL, n_seg;
+};
+
+// keys, stable radix sort (the keys' significant bits only), placement
+template <typename K, typename V>
+int bin_sort_place(spmv_plan_s *p, Scratch &sc, const SortPlaceArgs &A) {
+    BinDev &B = p->bin;
+    const hipStream_t st = p->stream;
+    const int64_t nnz = p->nnz;
+    int bits = 1;  // none = 2^bits - 1 >= E > every key
+    while (bits < (int)(8 * sizeof(K)) && (((uint64_t)1 << bits) - 1) < (uint64_t)A.E) ++bits;
+    const K none = bits >= 64 ? (K)~0ull : (K)(((uint64_t)1 << bits) - 1);
+    K *k0, *k1;
+    V *v0, *v1;
+    SPMV_RETURN_IF(sc.alloc(&k0, (size_t)nnz));
+    SPMV_RETURN_IF(sc.alloc(&k1, (size_t)nnz));
+    SPMV_RETURN_IF(sc.alloc(&v0, (size_t)nnz));
+    SPMV_RETURN_IF(sc.alloc(&v1, (size_t)nnz));
+    const unsigned grid = grid_of(nnz);
+    hipLaunchKernelGGL((bin_key_kernel<K, V>), dim3(grid), dim3(256), 0, st, A.rp, A.col, nnz, A.bstart, A.NB, A.row0,
+                       (int32_t)B.strip, A.S, A.off2, A.LL, none, k0, v0);
+    hipcub::DoubleBuffer<K> dk(k0, k1);
+    hipcub::DoubleBuffer<V> dv(v0, v1);
+    size_t tb = 0;
+    SPMV_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, dk, dv, nnz, 0, bits, st));
+    char *tmp = nullptr;
+    SPMV_RETURN_IF(sc.alloc(&tmp, tb));
+    SPMV_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, tb, dk, dv, nnz, 0, bits, st));
+    hipLaunchKernelGGL((bin_place_kernel<V>), dim3(grid_of(A.n_seg)), dim3(256), 0, st, A.rp, A.col, A.val,
+                       (const V *)dv.Current(), A.n_seg, A.bstart, A.NB, A.row0, (int32_t)B.strip, A.S, A.off1, A.off2,
+                       A.cbase, A.pbb, B.pad_log, A.run, A.srun, B.strip_block, B.sum_u, B.val1, B.cs1, B.slot2,
+                       B.dst1);
+    return SPMV_SUCCESS;
+}
+
 }  // namespace
 
 int bin_count_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, const std::vector<int32_t> &row0,
@@ -327,30 +381,39 @@ int bin_fill_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, c
     }
     Scratch sc{st, {}};
     int32_t *d_row0, *d_cnt;
-    int64_t *d_bstart, *d_off1, *d_off2, *d_pbb, *d_ks, *d_run, *d_srun;
-    unsigned long long *d_kh;
+    int64_t *d_bstart, *d_off1, *d_off2, *d_cbase, *d_pbb, *d_run, *d_srun;
+    // cbase: entries of the segments before each one in the Sum order
+    // ([strip block][bin][strip], bin_offsets), i.e. the sorted index of its
+    // first entry
+    std::vector<int64_t> cbase((size_t)(NB * S));
+    int64_t n_seg = 0;
+    {
+        const int64_t SB = B.strip_block > 0 ? B.strip_block : S;
+        for (int64_t k = 0; k * SB < S; ++k)
+            for (int64_t b = 0; b < NB; ++b)
+                for (int64_t t = k * SB; t < std::min(S, (k + 1) * SB); ++t) {
+                    cbase[(size_t)(b * S + t)] = n_seg;
+                    n_seg += cnt[(size_t)(b * S + t)];
+                }
+    }
     SPMV_RETURN_IF(sc.upload(&d_row0, row0));
     SPMV_RETURN_IF(sc.upload(&d_bstart, bstart));
     SPMV_RETURN_IF(sc.upload(&d_cnt, cnt));
     SPMV_RETURN_IF(sc.upload(&d_off1, off1));
     SPMV_RETURN_IF(sc.upload(&d_off2, off2));
+    SPMV_RETURN_IF(sc.upload(&d_cbase, cbase));
     SPMV_RETURN_IF(sc.upload(&d_run, run_off));
     SPMV_RETURN_IF(sc.upload(&d_srun, srun_off));
     // every slot starts as the dummy slot (segment padding and the padding of
     // each slot run to whole Sum batches)
     hipLaunchKernelGGL(fill_u16_kernel, dim3(grid_of(ES)), dim3(256), 0, st, B.slot2, ES, (uint16_t)B.max_rows);
     SPMV_RETURN_IF(sc.upload(&d_pbb, pbb));
-    SPMV_RETURN_IF(sc.alloc(&d_kh, (size_t)E));
-    SPMV_RETURN_IF(sc.alloc(&d_ks, (size_t)E));
-    SPMV_HIP_TRY(hipMemsetAsync(d_kh, 0, 8 * (size_t)E, st));
-    const unsigned grid = grid_of(p->nnz);
-    hipLaunchKernelGGL(bin_khist_kernel, dim3(grid), dim3(256), 0, st, d_rp, d_col, p->nnz, d_bstart, NB, d_row0,
-                       (int32_t)C, S, d_off2, LL, d_kh);
-    SPMV_RETURN_IF(exclusive_scan_i64((const int64_t *)d_kh, d_ks, E, st, sc.v));
-    SPMV_HIP_TRY(hipMemsetAsync(d_kh, 0, 8 * (size_t)E, st));  // now the k-run cursors
-    hipLaunchKernelGGL(bin_place_kernel, dim3(grid), dim3(256), 0, st, d_rp, d_col, d_val, p->nnz, d_bstart, NB,
-                       d_row0, (int32_t)C, S, d_off1, d_off2, d_ks, d_kh, d_pbb, B.pad_log, d_run, d_srun,
-                       B.strip_block, B.sum_u, LL, B.val1, B.cs1, B.slot2, B.dst1);
+    const SortPlaceArgs A{d_rp, d_col, d_val, NB, S, d_row0, d_bstart, d_off1, d_off2, d_cbase, d_pbb, d_run, d_srun,
+                          E, LL, n_seg};
+    if (E < ((int64_t)1 << 32) - 1 && p->nnz < ((int64_t)1 << 32))
+        SPMV_RETURN_IF((bin_sort_place<uint32_t, uint32_t>(p, sc, A)));
+    else
+        SPMV_RETURN_IF((bin_sort_place<uint64_t, uint64_t>(p, sc, A)));
     if (!B.mo)  // (Mul order: the Mul's segments are not padded)
         hipLaunchKernelGGL(bin_pad_kernel, dim3(grid_of(NB * S)), dim3(256), 0, st, d_cnt, NB * S, d_off1, B.pad_log,
                            B.val1, B.cs1);

@@ -525,7 +525,23 @@ int plan_arrays(const spmv_plan_s *p, std::vector<ArrayRef> &a) {
             return SPMV_SUCCESS;
         }
     }
-    set_error("spmv_plan_digest: BIN plans have no digest");
+    if (p->format == SPMV_FORMAT_BIN) {
+        const BinDev &B = p->bin;
+        const int64_t E1 = B.mul_entries + kBinMulSlack, S = B.n_strips, NR = B.n_blocks * B.n_bins;
+        add("bin_row0", B.bin_row0, 4 * (B.n_bins + 1));
+        add("run_off", B.run_off, 8 * (NR + 1));
+        add("srun_off", B.srun_off, 8 * (NR + 1));
+        add("val1", B.val1, 8 * E1);
+        add("cs1", B.cs1, (2 * E1) & ~(int64_t)3);
+        add("slot2", B.slot2, (2 * B.slot_entries) & ~(int64_t)3);
+        add("dst1", B.dst1, 4 * (E1 >> B.pad_log));
+        add("mtab", B.mtab, 4 * (B.slot_entries / 8));
+        add("lstart", B.lstart, 8 * S);
+        add("lshift", B.lshift, 8 * S);
+        add("lcode", B.lcode, 4 * B.long_entries);
+        return SPMV_SUCCESS;
+    }
+    set_error("spmv_plan_digest: unknown format");
     return SPMV_ERROR_NOT_SUPPORTED;
 }
 

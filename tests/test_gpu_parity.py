@@ -669,7 +669,8 @@ def _device_csr(rp, col, val):
 DEVICE_FORMATS = [("csr", {}), ("csr", {"csr_lanes": 1}), ("ss", {"ss_sigma": 4}), ("ss", {"ss_sigma": 16}),
                   ("ss", {"ss_sigma": 32}), ("ss", {"ss_sigma": 64}), ("ss", {}), ("ell", {}), ("hyb", {}), ("hyb", {"ell_width": 4}),
                   ("jds", {}), ("jds", {"ell_width": 8}), ("dia", {}), ("coo", {}), ("css", {}),
-                  ("css", {"css_slab_shift": 12}), ("auto", {})]
+                  ("css", {"css_slab_shift": 12}), ("bin", {}), ("bin", {"bin_long_len": 40}),
+                  ("bin", {"bin_strip_cols": 3001}), ("bin", {"bin_product_order": 2}), ("auto", {})]
 
 
 def _device_build_cases():
@@ -724,8 +725,7 @@ def test_host_csr_build_routing():
         ph = sp.Plan.from_csr(m, m, rp, col, val, fmt, build="host")
         assert not ph.built_on_device()
         assert pa.info()["format"] == ph.info()["format"] and pa.info()["kernel"] == ph.info()["kernel"], fmt
-        if pa.info()["format"] != "bin":
-            assert pa.digest() == ph.digest(), fmt
+        assert pa.digest() == ph.digest(), fmt
         ya, yh = run_plan(pa, x, m), run_plan(ph, x, m)
         assert np.array_equal(ya, yh), fmt
         check_close(ya, yo, what=f"routed {fmt}")
@@ -750,8 +750,7 @@ def test_host_csr_build_routing():
             got = ph.info()["format"]  # AUTO resolves alike on the host and the device
             expect_dev = got != "bin" or sorted_rows
             assert pd.built_on_device() == expect_dev, (name, fmt)
-            if ph.info()["format"] != "bin":
-                assert pd.digest() == ph.digest(), (name, fmt)
+            assert pd.digest() == ph.digest(), (name, fmt)
             yd2, yh2 = run_plan(pd, x2, mm), run_plan(ph, x2, mm)
             if ph.info()["format"] == "coo":  # f64 atomics: unordered adds
                 check_close(yd2, yh2, what=f"routed coo {name}")
@@ -786,11 +785,10 @@ def test_device_conversion_matches_host_build():
             for k in ("format", "kernel", "empty_rows", "stored_slots", "algo_bytes", "n_kernels", "ell_width",
                       "n_diags", "overflow_nnz", "csr_lanes", "ss_sigma"):
                 assert idv[k] == ih[k], f"{name} {fmt} {kw}: info {k} {idv[k]} != {ih[k]}"
-            if ih["format"] != "bin":
-                dh, dd = ph.digest(), pd.digest()
-                assert list(dd) == list(dh), (name, fmt, list(dd), list(dh))
-                bad = [a for a in dh if dh[a] != dd[a]]
-                assert not bad, f"{name} {fmt} {kw}: device layout differs in {bad}"
+            dh, dd = ph.digest(), pd.digest()
+            assert list(dd) == list(dh), (name, fmt, list(dd), list(dh))
+            bad = [a for a in dh if dh[a] != dd[a]]
+            assert not bad, f"{name} {fmt} {kw}: device layout differs in {bad}"
             yh = run_plan(ph, x, m)
             yd = run_plan(pd, x, m)
             if ih["format"] == "coo":
@@ -985,6 +983,7 @@ def test_bin_long_rows_run_path(long_len, opts):
     idv = pd.info()
     for k in BIN_LAYOUT_KEYS:
         assert idv[k] == info[k], (long_len, opts, k, info[k], idv[k])
+    assert pd.digest() == plan.digest(), (long_len, opts)
     assert np.array_equal(run_plan(pd, x, m), y), f"device long_len {long_len} {opts}"
     again = sp.Plan.from_csr(m, n, rp, col, val, "bin", bin_long_len=long_len, **opts)
     assert np.array_equal(run_plan(again, x, m), y)
@@ -1249,7 +1248,7 @@ def test_bin_empty_bins_between_full_ones(sum_waves):
 def test_bin_device_build(opts, monkeypatch):
     """spmv_plan_create_csr_device with BIN: the segments (and the long rows'
     run path) are counted, laid out and filled on the GPU (k_bin_build.hip).
-    Same bins / strips / slots / pieces as the host builder and y
+    The host builder's layout byte for byte (spmv_plan_digest) and y
     bit-identical to it and to the oracle; rows whose column strips are not
     ascending stage through the host builder."""
     import torch
@@ -1266,6 +1265,7 @@ def test_bin_device_build(opts, monkeypatch):
         assert pd.built_on_device() and not ph.built_on_device()
         for k in BIN_LAYOUT_KEYS:
             assert ih[k] == idv[k], (kind, m, n, k, ih[k], idv[k])
+        assert pd.digest() == ph.digest(), (kind, m, n, opts)
         yd = run_plan(pd, x, m)
         assert np.array_equal(yd, run_plan(ph, x, m)), f"{kind} {m}x{n} {opts}"
         assert_bin_rows(pd, yd, rp, col, val, x, what=f"device {kind} {m}x{n} {opts}")
