@@ -1296,7 +1296,8 @@ def test_bin_device_build(opts, monkeypatch):
 def test_full_size_headline_bit_exact(config):
     """BASELINE configs 2 and 3 at their full size (160 M / 29.6 M entries):
     the AUTO plan (BIN) against the oracle's opt_crs restatement -- bit for
-    bit -- plus linearity A(x1 + x2) = A x1 + A x2 to fp64 rounding."""
+    bit -- plus linearity A(x1 + x2) = A x1 + A x2 to fp64 rounding; at
+    config 3 also HYB, CSR, SS and CSS to 1e-12."""
     import torch
     if config == "c2":
         spec = sp.gen_spec("uniform", 10_000_000, per_row=16, seed=42)
@@ -1319,6 +1320,18 @@ def test_full_size_headline_bit_exact(config):
     lin = np.abs(outs[2] - (outs[0] + outs[1]))
     assert np.all(lin <= 1e-12 * np.abs(outs[2]) + 1e-300)
     plan.destroy()
+    if config == "c3":
+        # the named ELL + CSR hybrid and the other skew-tolerant formats at
+        # full size against the same oracle (each folds in its own fixed
+        # order: 1e-12 relative)
+        yo = oracle_y(rp, col, val, x1)
+        xd = torch.from_numpy(x1).cuda()
+        for fmt in ("hyb", "csr", "ss", "css"):
+            p2 = sp.Plan.from_csr(m, m, rp, col, val, fmt)
+            y.fill_(float("nan"))
+            p2.execute(xd, y)
+            check_close(y.cpu().numpy(), yo, what=f"c3 {fmt}")
+            p2.destroy()
 
 
 
@@ -1350,9 +1363,9 @@ def test_full_size_c5_rank_shape():
 
 def test_full_size_c4_banded():
     """BASELINE config 4 at full size: 20 M rows, diagonals -32..+31 (64),
-    1.28 G entries -- the largest index range in the product.  The DIA plan
-    bit for bit and the CSR plan (16 lanes per row) to 1e-12 against the
-    oracle's opt_crs restatement."""
+    1.28 G entries -- the largest index range in the product.  The DIA, ELL
+    and JDS plans bit for bit and the CSR (16 lanes per row) and SS plans to
+    1e-12 against the oracle's opt_crs restatement."""
     import torch
     m = 20_000_000
     spec = sp.gen_spec("banded", m, band_lo=-32, band_hi=31, seed=42)
@@ -1385,10 +1398,19 @@ def test_full_size_c4_banded():
         pd.destroy()
     del drp, dcol, dval, pd
     torch.cuda.empty_cache()
-    plan = sp.Plan.from_csr(m, m, rp, col, val, "csr")
-    plan.execute(xd, y)
-    check_close(y.cpu().numpy(), yo, what="c4 csr")
-    plan.destroy()
+    # the other config-4 formats, built through the host-CSR routing (>= 2^24
+    # entries: the device builders): ELL / JDS sum each row in column order
+    # (bit for bit), CSR / SS fold in their own fixed order (1e-12)
+    for fmt in ("csr", "ell", "jds", "ss"):
+        plan = sp.Plan.from_csr(m, m, rp, col, val, fmt)
+        assert plan.built_on_device(), fmt
+        y.fill_(float("nan"))
+        plan.execute(xd, y)
+        if fmt in ("ell", "jds"):
+            assert np.array_equal(y.cpu().numpy(), yo), f"c4 {fmt}"
+        else:
+            check_close(y.cpu().numpy(), yo, what=f"c4 {fmt}")
+        plan.destroy()
 
 
 def test_bin_refuses_huge_sparse_grid_and_auto_avoids_it():
