@@ -4,7 +4,9 @@
 // compute -> calibrate -> tail) with a fused, deterministic, idempotent
 // wave64 design.
 //
-// ss_tile_kernel<SIGMA>: one wave = one tile of 64 lanes x SIGMA nnz.  Lane l
+// The product launches ss_stream_kernel (below); ss_tile_kernel, its
+// all-loads-first twin, stays for the probe build's A/Bs (SPMV_SS_KERNEL=0).
+// The tile, common to both: one wave = 64 lanes x SIGMA nnz.  Lane l
 // owns SIGMA consecutive nnz (see SsDev layout: every wave load instruction is
 // 1 KiB contiguous -- col as 4 ints per lane, val as two 1-KiB halves of 2
 // doubles per lane, like ELL's values).  Products never touch memory (no val_buf: opt_ss's extra
