@@ -135,10 +135,9 @@ typedef struct spmv_options {
                                 the device builders (every format;
                                 byte-identical layouts, spmv_plan_digest), when
                                 the staging copy fits in device memory
-                                (BIN rows out of column-strip order, and CSS
-                                from 2^31 entries,
-                                take the host builders with the format resolved
-                                there); smaller ones take the host builders */
+                                (CSS from 2^31 entries takes the host builder
+                                with the format resolved there); smaller ones
+                                take the host builders */
 } spmv_options_t;
 
 /* Where spmv_plan_create_csr / _csr32 / _coo build the layout. */
@@ -225,9 +224,9 @@ int spmv_plan_create_csr32(int32_t m, int32_t n, int32_t nnz, const int32_t *row
  * that depend on row lengths alone; AUTO is resolved there too, its diagonal
  * census run on the device; CSS's per-wave column sorts are one segmented
  * sort.  The layouts are byte-identical to the host builders'
- * (spmv_plan_digest).  BIN when
- * some row's columns are not ascending by 20480-column strip, and CSS from
- * 2^31 entries, copy the CSR to the host and take the host builder.  The input is validated on the device like
+ * (spmv_plan_digest); BIN sorts rows whose columns are not ascending by
+ * 20480-column strip on the device first.  CSS from 2^31 entries copies the
+ * CSR to the host and takes the host builder.  The input is validated on the device like
  * spmv_plan_create_csr's host check. */
 int spmv_plan_create_csr_device(int64_t m, int64_t n, int64_t nnz, const int64_t *d_row_ptr,
                                 const int32_t *d_col_idx, const double *d_val,

@@ -1015,8 +1015,8 @@ static void bin_long_runs_table(const BinLayout &L, const BinDevLong &D, BinLong
     });
 }
 
-int build_bin_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, const double *d_val,
-                     const spmv_options_t &o) {
+static int build_bin_device_impl(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, const double *d_val,
+                                 const spmv_options_t &o) {
     BinDev &B = p->bin;
     SPMV_RETURN_IF(bin_params(p, o, p->m, p->n, p->nnz));
     if (p->m == 0 || p->nnz == 0) {
@@ -1076,6 +1076,30 @@ int build_bin_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, 
         SPMV_RETURN_IF(upload_vec(p, &B.mtab, tab));
     }
     return bin_finish(p, p->n, L, o);
+}
+
+int build_bin_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, const double *d_val,
+                     const spmv_options_t &o) {
+    const int st = build_bin_device_impl(p, d_rp, d_col, d_val, o);
+    if (st != kBinNeedHostBuild) return st;
+    // some row's column strips are out of order: sort every row's entries by
+    // strip on the device (stable, so a strip's entries keep their CSR order
+    // -- the order the host fill reads them in) and build from that copy: the
+    // host builder's layout byte for byte.  No room for the copy: the caller
+    // stages the CSR through the host builder.
+    void *c2 = nullptr, *v2 = nullptr;
+    const size_t nz = (size_t)std::max<int64_t>(p->nnz, 1);
+    if (hipMalloc(&c2, 4 * nz) != hipSuccess || hipMalloc(&v2, 8 * nz) != hipSuccess) {
+        (void)hipGetLastError();
+        if (c2) (void)hipFree(c2);
+        return kBinNeedHostBuild;
+    }
+    int st2 = bin_sort_rows_device(p, d_rp, d_col, d_val, (int32_t *)c2, (double *)v2);
+    if (st2 == SPMV_SUCCESS) st2 = build_bin_device_impl(p, d_rp, (const int32_t *)c2, (const double *)v2, o);
+    (void)hipStreamSynchronize(p->stream);
+    (void)hipFree(c2);
+    (void)hipFree(v2);
+    return st2;
 }
 
 }  // namespace spmv

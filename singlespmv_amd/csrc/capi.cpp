@@ -78,8 +78,9 @@ constexpr int64_t kDeviceBuildMinNnz = (int64_t)1 << 24;
 
 static int create_from_csr(const HostCsr &A, const spmv_options_t *opt_in, spmv_plan_t *out);
 
-// spmv_plan_create_csr_device's body.  A plan whose format the device
-// builders do not make (BIN rows out of column order; CSS from 2^31 entries) is built by the host builders: from a D2H copy of the CSR, or --
+// spmv_plan_create_csr_device's body.  A plan the device builders do not
+// make (CSS from 2^31 entries; BIN rows out of strip order when the device
+// has no room for their sorted copy) is built by the host builders: from a D2H copy of the CSR, or --
 // when need_host_fmt is given (create_via_device, whose caller still holds the
 // host CSR) -- by returning kNeedHostBuild with the resolved options there
 // (format chosen, crs_exact's rewrites applied, build = HOST).
@@ -186,8 +187,8 @@ static int create_device_impl(int64_t m, int64_t n, int64_t nnz, const int64_t *
             case SPMV_FORMAT_BIN:
                 if (probe_env("SPMV_BIN_HOST_BUILD")) host_build = true;
                 else st = build_bin_device(p, d_row_ptr, d_col_idx, d_val, o);
-                // BIN's device fill needs every row's column strips
-                // non-decreasing; other CSRs take the host builder below
+                // (kBinNeedHostBuild: rows out of strip order and no room
+                // for their sorted copy -- the host builder below)
                 if (st == kBinNeedHostBuild) host_build = true;
                 break;
             case SPMV_FORMAT_CSS:
@@ -290,8 +291,8 @@ static int create_from_csr(const HostCsr &A, const spmv_options_t *opt_in, spmv_
     if (dev < 0) SPMV_HIP_TRY(hipGetDevice(&dev));
     SPMV_RETURN_IF(check_device(dev));
     SPMV_HIP_TRY(hipSetDevice(dev));
-    // the device builders make every format (BIN only for rows in column
-    // strip order, CSS below 2^31 entries): the rest,
+    // the device builders make every format (CSS below 2^31 entries): the
+    // rest,
     // and a staging copy that does not fit, take the host builders below --
     // with the format AUTO resolved on the device
     if (o.build == SPMV_BUILD_DEVICE || (o.build == SPMV_BUILD_AUTO && A.nnz >= kDeviceBuildMinNnz)) {

@@ -452,12 +452,17 @@ int build_coo(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o);
 int build_jds(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o);
 int build_bin(spmv_plan_s *p, const HostCsr &A, const spmv_options_t &o);  // build_bin.cpp
 // BIN from a device CSR (build_bin.cpp + k_bin_build.hip), long rows
-// included.  Returns kBinNeedHostBuild when a row's column strips are not
-// non-decreasing (the caller then stages the CSR through the host builder).
+// included; rows whose column strips are out of order are first sorted by
+// strip on the device (bin_sort_rows_device).  kBinNeedHostBuild is then
+// internal to the builder.
 constexpr int kBinNeedHostBuild = -1000;
 int build_bin_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, const double *d_val,
                      const spmv_options_t &o);
 // k_bin_build.hip: bstart[b] = row_ptr[row0[b]] (first entry of each bin)
+// rows whose column strips are out of order: col2 / val2 (nnz each, the
+// caller's) = the CSR's entries stably sorted by strip inside every row
+int bin_sort_rows_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, const double *d_val,
+                         int32_t *col2, double *val2);
 // LL > 0: rows of >= LL entries take the run path and stay out of the segments
 int bin_count_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, const std::vector<int32_t> &row0,
                      const std::vector<int64_t> &bstart, int64_t S, int64_t LL, std::vector<int32_t> &cnt);

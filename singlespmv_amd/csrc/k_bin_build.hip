@@ -11,7 +11,9 @@
 //   strip t = col[j] / C
 //   k       = ordinal of j among row r's entries in strip t
 //             (= j - first entry of r in strip t; rows must have
-//              non-decreasing strips, checked by bin_count_kernel)
+//              non-decreasing strips, checked by bin_count_kernel -- a CSR
+//              with rows out of strip order is first sorted by strip per
+//              row, stably, bin_sort_rows_device)
 // Phases: counts per (b, t) -> [host offsets] -> key off2(b, t) + k per
 // entry -> stable radix sort of (key, j) -> placement: the i-th sorted entry
 // sits at i - (entries of the earlier segments) in its segment -> padding.
@@ -155,6 +157,33 @@ __global__ __launch_bounds__(256) void fill_u16_kernel(uint16_t *__restrict__ a,
 
 __global__ __launch_bounds__(256) void fill_i32_kernel(int32_t *__restrict__ a, int64_t n, int32_t v) {
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) a[i] = v;
+}
+
+// ---- rows whose strips are out of order: each row's entries stably sorted
+// by strip (CSR order kept inside a strip, the order the host fill reads
+// them in) -- key = row * S + strip, value = entry
+template <typename V>
+__global__ __launch_bounds__(256) void bin_row_strip_key_kernel(const int64_t *__restrict__ rp, int64_t m,
+                                                                const int32_t *__restrict__ col, int64_t nnz,
+                                                                int32_t C, int64_t S, uint64_t *__restrict__ keys,
+                                                                V *__restrict__ vals) {
+    for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < nnz; j += (int64_t)gridDim.x * 256) {
+        const int64_t r = upper_idx(rp, 0, m + 1, j) - 1;
+        keys[j] = (uint64_t)r * (uint64_t)S + (uint64_t)(col[j] / C);
+        vals[j] = (V)j;
+    }
+}
+
+template <typename V>
+__global__ __launch_bounds__(256) void bin_gather_entries_kernel(const V *__restrict__ order, int64_t nnz,
+                                                                 const int32_t *__restrict__ col,
+                                                                 const double *__restrict__ val,
+                                                                 int32_t *__restrict__ col2, double *__restrict__ val2) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nnz; i += (int64_t)gridDim.x * 256) {
+        const int64_t j = (int64_t)order[i];
+        col2[i] = col[j];
+        val2[i] = val[j];
+    }
 }
 
 // ---- long rows (the run path, internal.hpp BinDev) ----------------------
@@ -311,6 +340,33 @@ int bin_sort_place(spmv_plan_s *p, Scratch &sc, const SortPlaceArgs &A) {
                        A.cbase, A.pbb, B.pad_log, A.run, A.srun, B.strip_block, B.sum_u, B.val1, B.cs1, B.slot2,
                        B.dst1);
     return SPMV_SUCCESS;
+}
+
+template <typename V>
+int bin_sort_rows_t(spmv_plan_s *p, Scratch &sc, const int64_t *d_rp, const int32_t *d_col, const double *d_val,
+                    int32_t *col2, double *val2) {
+    const hipStream_t st = p->stream;
+    const int64_t m = p->m, nnz = p->nnz, C = p->bin.strip, S = std::max<int64_t>(1, (p->n + C - 1) / C);
+    int bits = 1;
+    while (bits < 64 && (((uint64_t)1 << bits) - 1) < (uint64_t)m * (uint64_t)S) ++bits;
+    uint64_t *k0, *k1;
+    V *v0, *v1;
+    SPMV_RETURN_IF(sc.alloc(&k0, (size_t)nnz));
+    SPMV_RETURN_IF(sc.alloc(&k1, (size_t)nnz));
+    SPMV_RETURN_IF(sc.alloc(&v0, (size_t)nnz));
+    SPMV_RETURN_IF(sc.alloc(&v1, (size_t)nnz));
+    hipLaunchKernelGGL((bin_row_strip_key_kernel<V>), dim3(grid_of(nnz)), dim3(256), 0, st, d_rp, m, d_col, nnz,
+                       (int32_t)C, S, k0, v0);
+    hipcub::DoubleBuffer<uint64_t> dk(k0, k1);
+    hipcub::DoubleBuffer<V> dv(v0, v1);
+    size_t tb = 0;
+    SPMV_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, dk, dv, nnz, 0, bits, st));
+    char *tmp = nullptr;
+    SPMV_RETURN_IF(sc.alloc(&tmp, tb));
+    SPMV_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, tb, dk, dv, nnz, 0, bits, st));
+    hipLaunchKernelGGL((bin_gather_entries_kernel<V>), dim3(grid_of(nnz)), dim3(256), 0, st, (const V *)dv.Current(),
+                       nnz, d_col, d_val, col2, val2);
+    return finish(st, "row strip sort");
 }
 
 }  // namespace
@@ -486,6 +542,13 @@ int bin_long_fill_device(spmv_plan_s *p, const int32_t *d_col, const double *d_v
     hipLaunchKernelGGL(bin_long_pad_kernel, dim3(grid_of(S)), dim3(256), 0, st, S, d_lb, d_lpad, d_lco, (int32_t)trash,
                        B.lcode);
     return finish(st, "long rows");
+}
+
+int bin_sort_rows_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, const double *d_val,
+                         int32_t *col2, double *val2) {
+    Scratch sc{p->stream, {}};
+    if (p->nnz < ((int64_t)1 << 32)) return bin_sort_rows_t<uint32_t>(p, sc, d_rp, d_col, d_val, col2, val2);
+    return bin_sort_rows_t<uint64_t>(p, sc, d_rp, d_col, d_val, col2, val2);
 }
 
 }  // namespace spmv

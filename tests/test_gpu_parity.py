@@ -706,10 +706,9 @@ def _device_build_cases():
 def test_host_csr_build_routing():
     """spmv_options_t::build: a host CSR of >= 2^24 entries (AUTO) or any
     size (DEVICE) is staged into HBM and built by the device builders -- the
-    host builder's layout byte for byte and the same y; BIN on rows out of
-    column order takes the host builders with the format resolved on the
-    device; small CSRs under AUTO stay on the host
-    builders."""
+    host builder's layout byte for byte and the same y (BIN rows out of
+    column order sorted by strip on the device first); small CSRs under AUTO
+    stay on the host builders."""
     import torch
     # large: 1 M rows x 17 entries = 17 M entries, AUTO -> BIN (x too wide
     # for a window) built on the device
@@ -743,13 +742,7 @@ def test_host_csr_build_routing():
                 continue
             assert not sp.Plan.from_csr(mm, n, rp2, col2, val2, fmt).built_on_device()
             pd = sp.Plan.from_csr(mm, n, rp2, col2, val2, fmt, build="device")
-            dec = np.diff(col2.astype(np.int64) // 20480) < 0  # entry j+1 in an earlier x strip ...
-            inner = rp2[1:-1]
-            dec[inner[(inner > 0) & (inner < len(col2))] - 1] = False  # ... inside one row
-            sorted_rows = not dec.any()  # BIN's device fill wants each row's strips in order
-            got = ph.info()["format"]  # AUTO resolves alike on the host and the device
-            expect_dev = got != "bin" or sorted_rows
-            assert pd.built_on_device() == expect_dev, (name, fmt)
+            assert pd.built_on_device(), (name, fmt)  # every format, AUTO resolved alike
             assert pd.digest() == ph.digest(), (name, fmt)
             yd2, yh2 = run_plan(pd, x2, mm), run_plan(ph, x2, mm)
             if ph.info()["format"] == "coo":  # f64 atomics: unordered adds
@@ -1250,7 +1243,7 @@ def test_bin_device_build(opts, monkeypatch):
     run path) are counted, laid out and filled on the GPU (k_bin_build.hip).
     The host builder's layout byte for byte (spmv_plan_digest) and y
     bit-identical to it and to the oracle; rows whose column strips are not
-    ascending stage through the host builder."""
+    ascending are sorted by strip on the device first, same layout."""
     import torch
     cases = [("uniform", 40_000, 40_000), ("powerlaw", 30_011, 100_003), ("empty_rows", 70_001, 9_000),
              ("uniform", 5, 3), ("powerlaw", 1, 70_000)]
@@ -1277,8 +1270,8 @@ def test_bin_device_build(opts, monkeypatch):
     x = sp.generate_vector(50_000, seed=5)
     pd = sp.Plan.from_device_csr(50_000, 50_000, torch.from_numpy(rp).cuda(), torch.from_numpy(col).cuda(),
                                  torch.from_numpy(val).cuda(), "bin", **opts)
-    ph = sp.Plan.from_csr(50_000, 50_000, rp, col, val, "bin", **opts)
-    assert not pd.built_on_device()
+    ph = sp.Plan.from_csr(50_000, 50_000, rp, col, val, "bin", build="host", **opts)
+    assert pd.built_on_device() and pd.digest() == ph.digest()
     yd = run_plan(pd, x, 50_000)
     assert np.array_equal(yd, run_plan(ph, x, 50_000))
     # BIN adds a row's strips in strip order: with unsorted columns that is
