@@ -806,6 +806,76 @@ def test_device_conversion_matches_host_build():
         sp.Plan.from_device_csr(2, 6, rp, bad_col, v, "csr")  # host row_ptr
 
 
+def _fuzz_csr(seed):
+    """A random CSR: mixed row lengths (empty rows, short rows, a few long
+    ones), columns uniform, banded or clustered, duplicates possible, rows
+    sorted or (some) shuffled."""
+    rng = np.random.default_rng(seed)
+    m = int(rng.integers(1, 4000))
+    n = int(rng.choice([1, 7, 300, 5000, 70_000]))
+    lens = rng.integers(0, int(rng.choice([2, 9, 40])), m)
+    lens[rng.random(m) < 0.15] = 0
+    if rng.random() < 0.5:  # a few long rows
+        k = max(1, m // 200)
+        lens[rng.choice(m, k, replace=False)] = rng.integers(100, 3000, k)
+    rp = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    nnz = int(rp[-1])
+    rows = np.repeat(np.arange(m), lens)
+    mode = seed % 3
+    if mode == 0:
+        col = rng.integers(0, n, nnz)
+    elif mode == 1:  # banded around the diagonal
+        col = np.clip(rows * n // max(m, 1) + rng.integers(-5, 6, nnz), 0, n - 1)
+    else:  # clustered in a few column ranges
+        c0 = rng.integers(0, n, 4)
+        col = np.clip(c0[rng.integers(0, 4, nnz)] + rng.integers(0, 50, nnz), 0, n - 1)
+    col = col.astype(np.int32)
+    for r in range(m):  # sorted rows, except some shuffled ones
+        a, z = rp[r], rp[r + 1]
+        if z - a > 1:
+            col[a:z] = np.sort(col[a:z]) if rng.random() > 0.1 else rng.permutation(col[a:z])
+    val = rng.random(nnz) + 0.01
+    return m, n, rp, col, val
+
+
+FUZZ_FORMATS = [("csr", {}), ("ss", {}), ("ss", {"ss_sigma": 8}), ("ell", {}), ("hyb", {}), ("jds", {}), ("dia", {}),
+                ("coo", {}), ("css", {}), ("bin", {}), ("bin", {"bin_long_len": 16}),
+                ("bin", {"bin_strip_cols": 1000}), ("auto", {})]
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_device_build_fuzz(seed):
+    """Random CSRs (mixed row lengths, duplicates, unsorted rows, several
+    column patterns): every format built on the GPU from the device CSR is the
+    host builder's layout byte for byte (spmv_plan_digest) with the same y;
+    a format the host refuses is refused on the device too."""
+    m, n, rp, col, val = _fuzz_csr(seed)
+    x = sp.generate_vector(n, seed=seed + 100)
+    yo = oracle_y(rp, col, val, x)
+    drp, dcol, dval = _device_csr(rp, col, val)
+    for fmt, kw in FUZZ_FORMATS:
+        try:
+            ph = sp.Plan.from_csr(m, n, rp, col, val, fmt, build="host", **kw)
+        except sp.SpmvError as e:
+            assert "not supported" in str(e), (seed, fmt, e)
+            with pytest.raises(sp.SpmvError, match="not supported"):
+                sp.Plan.from_device_csr(m, n, drp, dcol, dval, fmt, **kw)
+            continue
+        pd = sp.Plan.from_device_csr(m, n, drp, dcol, dval, fmt, **kw)
+        assert pd.built_on_device() and pd.info()["format"] == ph.info()["format"], (seed, fmt, kw)
+        dh, dd = ph.digest(), pd.digest()
+        bad = [a for a in dh if dh[a] != dd.get(a)]
+        assert list(dd) == list(dh) and not bad, f"seed {seed} {fmt} {kw}: layout differs in {bad}"
+        yh, yd = run_plan(ph, x, m), run_plan(pd, x, m)
+        if ph.info()["format"] == "coo":
+            check_close(yd, yh, what=f"fuzz {seed} coo")
+        else:
+            assert np.array_equal(yd, yh), (seed, fmt, kw)
+        check_close(yd, yo, what=f"fuzz {seed} {fmt} {kw}")
+        ph.destroy()
+        pd.destroy()
+
+
 def test_profile_phases():
     """spmv_profile: the per-phase split (reference g_profile Mul/Sum)."""
     import torch
