@@ -135,9 +135,9 @@ typedef struct spmv_options {
                                 the device builders (every format;
                                 byte-identical layouts, spmv_plan_digest), when
                                 the staging copy fits in device memory
-                                (CSS from 2^31 entries takes the host builder
-                                with the format resolved there); smaller ones
-                                take the host builders */
+                                (else the host builders, with the format
+                                resolved there); smaller ones take the host
+                                builders */
 } spmv_options_t;
 
 /* Where spmv_plan_create_csr / _csr32 / _coo build the layout. */
@@ -225,8 +225,8 @@ int spmv_plan_create_csr32(int32_t m, int32_t n, int32_t nnz, const int32_t *row
  * census run on the device; CSS's per-wave column sorts are one segmented
  * sort.  The layouts are byte-identical to the host builders'
  * (spmv_plan_digest); BIN sorts rows whose columns are not ascending by
- * 20480-column strip on the device first.  CSS from 2^31 entries copies the
- * CSR to the host and takes the host builder.  The input is validated on the device like
+ * 20480-column strip on the device first (when the device has no room for
+ * that copy, the CSR is copied to the host and the host builder runs).  The input is validated on the device like
  * spmv_plan_create_csr's host check. */
 int spmv_plan_create_csr_device(int64_t m, int64_t n, int64_t nnz, const int64_t *d_row_ptr,
                                 const int32_t *d_col_idx, const double *d_val,

@@ -79,8 +79,8 @@ constexpr int64_t kDeviceBuildMinNnz = (int64_t)1 << 24;
 static int create_from_csr(const HostCsr &A, const spmv_options_t *opt_in, spmv_plan_t *out);
 
 // spmv_plan_create_csr_device's body.  A plan the device builders do not
-// make (CSS from 2^31 entries; BIN rows out of strip order when the device
-// has no room for their sorted copy) is built by the host builders: from a D2H copy of the CSR, or --
+// make (BIN rows out of strip order when the device has no room for their
+// sorted copy) is built by the host builders: from a D2H copy of the CSR, or --
 // when need_host_fmt is given (create_via_device, whose caller still holds the
 // host CSR) -- by returning kNeedHostBuild with the resolved options there
 // (format chosen, crs_exact's rewrites applied, build = HOST).
@@ -191,10 +191,7 @@ static int create_device_impl(int64_t m, int64_t n, int64_t nnz, const int64_t *
                 // for their sorted copy -- the host builder below)
                 if (st == kBinNeedHostBuild) host_build = true;
                 break;
-            case SPMV_FORMAT_CSS:
-                if (nnz >= ((int64_t)1 << 31) - 256) host_build = true;  // the segmented sort's int counts
-                else st = build_css_device(p, A, o);
-                break;
+            case SPMV_FORMAT_CSS: st = build_css_device(p, A, o); break;
             default:
                 set_error("unknown format");
                 st = SPMV_ERROR_INVALID_VALUE;
@@ -291,10 +288,10 @@ static int create_from_csr(const HostCsr &A, const spmv_options_t *opt_in, spmv_
     if (dev < 0) SPMV_HIP_TRY(hipGetDevice(&dev));
     SPMV_RETURN_IF(check_device(dev));
     SPMV_HIP_TRY(hipSetDevice(dev));
-    // the device builders make every format (CSS below 2^31 entries): the
-    // rest,
-    // and a staging copy that does not fit, take the host builders below --
-    // with the format AUTO resolved on the device
+    // the device builders make every format; what they cannot (BIN rows out
+    // of strip order without room for their sorted copy) and a staging copy
+    // that does not fit take the host builders below -- with the format AUTO
+    // resolved on the device
     if (o.build == SPMV_BUILD_DEVICE || (o.build == SPMV_BUILD_AUTO && A.nnz >= kDeviceBuildMinNnz)) {
         spmv_options_t ho = o;
         const int st = create_via_device(A, o, dev, out, &ho);

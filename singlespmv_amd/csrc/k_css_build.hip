@@ -3,11 +3,12 @@
 // pointers -- row blocks, long-row pieces, the LPT dealing of pieces to the
 // 15 worker waves, list offsets -- and the entries never visit the host:
 // each worker-wave list's entries are expanded in list order (pieces in
-// dealing order, a piece in CSR order), stably sorted by column with a
-// segmented sort (one segment per list: a row's entries of one column keep
-// their CSR order, as std::stable_sort does on the host), and scattered into
-// the list's 256-entry chunks.  Byte-identical to the host fill
-// (spmv_plan_digest).
+// dealing order, a piece in CSR order) with the key (list, column), stably
+// radix-sorted (hipCUB, the key's significant bits only: within a list by
+// column, a row's entries of one column keeping their CSR order, as
+// std::stable_sort does on the host), and scattered into the list's
+// 256-entry chunks.  Byte-identical to the host fill (spmv_plan_digest); no
+// 32-bit entry limit.
 #include <hipcub/hipcub.hpp>
 
 #include "device.hpp"
@@ -17,14 +18,14 @@ namespace spmv {
 
 namespace {
 
-// one wave per list: its pieces' entries in list order; key = column, value
-// = entry index << 16 | LDS slot
+// one wave per list: its pieces' entries in list order; key = list <<
+// cbits | column, value = entry index << 16 | LDS slot
 __global__ __launch_bounds__(256) void css_expand_kernel(int64_t nlists, const int64_t *__restrict__ poff,
                                                          const int64_t *__restrict__ pb,
                                                          const int64_t *__restrict__ pe,
                                                          const int32_t *__restrict__ ps,
-                                                         const int32_t *__restrict__ eoff,
-                                                         const int32_t *__restrict__ col, int32_t *__restrict__ keys,
+                                                         const int64_t *__restrict__ eoff, int cbits,
+                                                         const int32_t *__restrict__ col, uint64_t *__restrict__ keys,
                                                          uint64_t *__restrict__ vals) {
     const int64_t L = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
@@ -34,7 +35,7 @@ __global__ __launch_bounds__(256) void css_expand_kernel(int64_t nlists, const i
         const int64_t b = pb[q], len = pe[q] - b;
         const uint64_t slot = (uint32_t)ps[q];
         for (int64_t i = lane; i < len; i += 64) {
-            keys[k + i] = col[b + i];
+            keys[k + i] = ((uint64_t)L << cbits) | (uint32_t)col[b + i];
             vals[k + i] = ((uint64_t)(b + i) << 16) | slot;
         }
         k += len;
@@ -42,9 +43,9 @@ __global__ __launch_bounds__(256) void css_expand_kernel(int64_t nlists, const i
 }
 
 // one wave per list: sorted entry i to chunk i / 256, lane i % 256
-__global__ __launch_bounds__(256) void css_scatter_kernel(int64_t nlists, const int32_t *__restrict__ eoff,
+__global__ __launch_bounds__(256) void css_scatter_kernel(int64_t nlists, const int64_t *__restrict__ eoff,
                                                           const int64_t *__restrict__ woff, int64_t chunk_stride,
-                                                          const int32_t *__restrict__ keys,
+                                                          const uint64_t *__restrict__ keys, int cbits,
                                                           const uint64_t *__restrict__ vals,
                                                           const double *__restrict__ val, int32_t *__restrict__ ocol,
                                                           uint16_t *__restrict__ orow, double *__restrict__ oval) {
@@ -55,7 +56,7 @@ __global__ __launch_bounds__(256) void css_scatter_kernel(int64_t nlists, const 
     for (int64_t i = lane; i < len; i += 64) {
         const int64_t out = base + (i >> 8) * chunk_stride + (i & 255);
         const uint64_t v = vals[e0 + i];
-        ocol[out] = keys[e0 + i];
+        ocol[out] = (int32_t)(keys[e0 + i] & (((uint64_t)1 << cbits) - 1));
         orow[out] = (uint16_t)(v & 0xFFFFu);
         oval[out] = val[v >> 16];
     }
@@ -106,7 +107,6 @@ int plan_alloc(spmv_plan_s *p, T **dst, int64_t count) {
 }  // namespace
 
 int build_css_device(spmv_plan_s *p, const DevCsr &A, const spmv_options_t &o) {
-    SPMV_CHECK_ARG(A.nnz < ((int64_t)1 << 31) - 256, "device CSS build: fewer than 2^31 entries");
     CssLayout CL;
     SPMV_RETURN_IF(css_layout(p, A.h_rp, A.m, A.n, A.nnz, o, CL));
     CssDev &c = p->css;
@@ -114,7 +114,8 @@ int build_css_device(spmv_plan_s *p, const DevCsr &A, const spmv_options_t &o) {
     const int64_t nl = CL.nlists, total = CL.total;
     // the pieces, flattened in list order, and each list's entry offset
     std::vector<int64_t> poff((size_t)nl + 1, 0), pb, pe;
-    std::vector<int32_t> ps, eoff((size_t)nl + 1, 0);
+    std::vector<int32_t> ps;
+    std::vector<int64_t> eoff((size_t)nl + 1, 0);
     for (int64_t L = 0; L < nl; ++L) {
         int64_t len = 0;
         for (const CssPiece &pc : CL.wave_pieces[(size_t)L]) {
@@ -125,7 +126,7 @@ int build_css_device(spmv_plan_s *p, const DevCsr &A, const spmv_options_t &o) {
         }
         std::vector<CssPiece>().swap(CL.wave_pieces[(size_t)L]);
         poff[(size_t)L + 1] = (int64_t)pb.size();
-        eoff[(size_t)L + 1] = eoff[(size_t)L] + (int32_t)len;
+        eoff[(size_t)L + 1] = eoff[(size_t)L] + len;
     }
     if (eoff[(size_t)nl] != A.nnz) {
         set_error("device CSS build: the lists do not cover the entries");
@@ -144,9 +145,9 @@ int build_css_device(spmv_plan_s *p, const DevCsr &A, const spmv_options_t &o) {
                            st, c.row, total, (uint16_t)kCssMaxRows);
     if (A.nnz > 0) {
         Scratch sc{st, {}};
-        int64_t *d_poff, *d_pb, *d_pe, *d_woff;
-        int32_t *d_ps, *d_eoff, *k_in, *k_out;
-        uint64_t *v_in, *v_out;
+        int64_t *d_poff, *d_pb, *d_pe, *d_woff, *d_eoff;
+        int32_t *d_ps;
+        uint64_t *k_in, *k_out, *v_in, *v_out;
         SPMV_RETURN_IF(sc.upload(&d_poff, poff));
         SPMV_RETURN_IF(sc.upload(&d_pb, pb));
         SPMV_RETURN_IF(sc.upload(&d_pe, pe));
@@ -157,17 +158,21 @@ int build_css_device(spmv_plan_s *p, const DevCsr &A, const spmv_options_t &o) {
         SPMV_RETURN_IF(sc.alloc(&k_out, (size_t)A.nnz));
         SPMV_RETURN_IF(sc.alloc(&v_in, (size_t)A.nnz));
         SPMV_RETURN_IF(sc.alloc(&v_out, (size_t)A.nnz));
+        // key bits: the column's, then the list's above them
+        int cbits = 1, lbits = 1;
+        while (cbits < 31 && ((int64_t)1 << cbits) < A.n) ++cbits;
+        while (lbits < 32 && ((int64_t)1 << lbits) < nl) ++lbits;
         hipLaunchKernelGGL(css_expand_kernel, dim3(waves_grid(nl)), dim3(256), 0, st, nl, d_poff, d_pb, d_pe, d_ps,
-                           d_eoff, A.d_col, k_in, v_in);
+                           d_eoff, cbits, A.d_col, k_in, v_in);
+        hipcub::DoubleBuffer<uint64_t> dk(k_in, k_out), dv(v_in, v_out);
         size_t tb = 0;
-        SPMV_HIP_TRY(hipcub::DeviceSegmentedSort::StableSortPairs(nullptr, tb, k_in, k_out, v_in, v_out, (int)A.nnz,
-                                                                  (int)nl, d_eoff, d_eoff + 1, st));
+        SPMV_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, dk, dv, A.nnz, 0, cbits + lbits, st));
         void *tmp = nullptr;
         SPMV_RETURN_IF(sc.alloc((char **)&tmp, tb));
-        SPMV_HIP_TRY(hipcub::DeviceSegmentedSort::StableSortPairs(tmp, tb, k_in, k_out, v_in, v_out, (int)A.nnz,
-                                                                  (int)nl, d_eoff, d_eoff + 1, st));
+        SPMV_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, tb, dk, dv, A.nnz, 0, cbits + lbits, st));
         hipLaunchKernelGGL(css_scatter_kernel, dim3(waves_grid(nl)), dim3(256), 0, st, nl, d_eoff, d_woff,
-                           c.chunk_stride, k_out, v_out, A.d_val, c.col, c.row, c.val);
+                           c.chunk_stride, (const uint64_t *)dk.Current(), cbits, (const uint64_t *)dv.Current(), A.d_val,
+                           c.col, c.row, c.val);
         hipError_t e = hipGetLastError();
         if (e == hipSuccess) e = hipStreamSynchronize(st);
         if (e != hipSuccess) {
