@@ -220,13 +220,14 @@ int spmv_plan_create_csr32(int32_t m, int32_t n, int32_t nnz, const int32_t *row
  * all three arrays on the plan's device, only read).  Every format is built
  * on the device (the CSR5 conversion pipeline's role,
  * CSR5_cuda/detail/cuda/format_cuda.h:21-718): only the row pointers (and,
- * for BIN, the (bin, strip) counts) visit the host, for the layout decisions
- * that depend on row lengths alone; AUTO is resolved there too, its diagonal
- * census run on the device; CSS's per-wave column sorts are one segmented
- * sort.  The layouts are byte-identical to the host builders'
- * (spmv_plan_digest); BIN sorts rows whose columns are not ascending by
- * 20480-column strip on the device first (when the device has no room for
- * that copy, the CSR is copied to the host and the host builder runs).  The input is validated on the device like
+ * for BIN, the (bin, strip) counts and the long rows' run descriptors) visit
+ * the host, for the layout decisions that depend on row lengths alone; AUTO
+ * is resolved there too, its diagonal census run on the device; CSS's
+ * per-wave column sorts are one stable radix sort.  The layouts are
+ * byte-identical to the host builders' (spmv_plan_digest); BIN sorts rows
+ * whose columns are not ascending by 20480-column strip on the device first
+ * (when the device has no room for that copy, the CSR is copied to the host
+ * and the host builder runs).  The input is validated on the device like
  * spmv_plan_create_csr's host check. */
 int spmv_plan_create_csr_device(int64_t m, int64_t n, int64_t nnz, const int64_t *d_row_ptr,
                                 const int32_t *d_col_idx, const double *d_val,
