@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
-"""Beyond 2^31 entries: the CSS and BIN plans built on the device from a
-2.16 G-entry CSR already in HBM (135 M x 135 M, 16 per row), y against the
-oracle's opt_crs restatement (BIN bit for bit, CSS to 1e-12).  One JSON line
-per format.  A one-off check (too heavy for the suite)."""
+"""Beyond 2^31 entries: plans built on the device from a 2.16 G-entry CSR
+already in HBM (135 M x 135 M, 16 per row), y against the oracle's opt_crs
+restatement (to 1e-12; bit_exact reported).  One JSON line per format.
+  python tools/huge_device_build_check.py [m] [fmt,fmt,...]   (default css,bin)
+A one-off check (too heavy for the suite)."""
 import json
 import os
 import sys
@@ -17,6 +18,7 @@ import oracle  # noqa: E402
 import singlespmv_amd as sp  # noqa: E402
 
 m = int(sys.argv[1]) if len(sys.argv) > 1 else 135_000_000
+fmts = sys.argv[2].split(",") if len(sys.argv) > 2 else ["css", "bin"]
 t0 = time.time()
 rp, col, val = sp.generate_csr(sp.gen_spec("uniform", m, per_row=16, seed=42))
 nnz = int(rp[-1])
@@ -28,7 +30,7 @@ drp, dcol, dval = (torch.from_numpy(a).cuda() for a in (rp, col, val))
 del col, val
 xd = torch.from_numpy(x).cuda()
 y = torch.empty(m, dtype=torch.float64, device="cuda")
-for fmt in ("css", "bin"):
+for fmt in fmts:
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     p = sp.Plan.from_device_csr(m, m, drp, dcol, dval, fmt)
