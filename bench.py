@@ -168,6 +168,8 @@ def parse():
     ap.add_argument("--verify", action="store_true",
                     help="gather y to rank 0 and compare with the oracle over the full matrix "
                          "(tests; small sizes only)")
+    ap.add_argument("--build", default="auto", choices=["auto", "host", "device"],
+                    help="plan builders (spmv_options_t.build; AUTO: host CSRs of >= 2^24 entries on the device)")
     ap.add_argument("--sim-world", type=int, default=0,
                     help="development: run rank 0's share of a K-GPU job on one GPU "
                          "(n = K * rows); the JSON marks it as emulated")
@@ -347,7 +349,8 @@ def time_formats(ctx, args, M, fmts, trials_head: int, y_check=None, setup_mark=
         tp = time.time()
         plan, err = None, None
         try:
-            plan = sp.Plan.from_csr(M["rows"], M["n"], M["rp"], M["col"], M["val"], fmt=fmt, device=ctx.local)
+            plan = sp.Plan.from_csr(M["rows"], M["n"], M["rp"], M["col"], M["val"], fmt=fmt, device=ctx.local,
+                                    build=args.build)
         except sp.SpmvError as e:
             err = str(e)
         # every rank skips a format that failed on any rank (the timed trials
