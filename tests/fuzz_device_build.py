@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """One-off wide run of tests/test_gpu_parity.py::test_device_build_fuzz over
-many more seeds (host build vs device build: digests and y).  Prints one
-JSON line per failing (seed, format) and a summary line.
-  python tools/device_build_fuzz.py 40 440
+many more seeds (host build vs device build: digests and y; y against the
+oracle).  Prints one JSON line per failing (seed, format) and a summary line.
+  python tests/fuzz_device_build.py 40 640
 """
 import json
 import os
