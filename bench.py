@@ -27,6 +27,13 @@ max_rel_err_vs_cpu against the CPU port on the same matrix (`--only-config`
 skips them).  At N > 1 `per_rank` lists every rank's rows, nnz, Mul / Sum
 phases and event time, so the max-over-ranks step can be read per rank.
 
+Every timed format carries `max_rel_err_vs_cpu`, at every N: each rank
+compares its y slice with the oracle's opt_crs restatement of its own shard
+(computed once on the host, untimed), and the figure is the max over ranks
+(`per_rank[*].max_rel_err_vs_cpu` holds each rank's).  The process group has
+a bounded timeout (BENCH_PG_TIMEOUT_S, default 900 s), so a hung collective
+ends the job with an error.
+
 `--gpus N` with no torchrun environment starts `torch.distributed.run` with N
 ranks (one per GPU) as a child process before anything in this process loads
 HIP (the GPUs are counted from the KFD topology in sysfs), and exits with the
@@ -38,6 +45,7 @@ child's return code.
 Prints ONE JSON line on rank 0.
 """
 import argparse
+import datetime
 import json
 import os
 import socket
@@ -279,10 +287,15 @@ class Ctx:
         self.dev = torch.device("cuda", self.local)
         self.distributed = self.world > 1
         if self.distributed:
+            # bounded: a rank that never reaches a collective (a hung peer, a
+            # lost GPU) ends the job with an error instead of holding it until
+            # the driver's kill.  Generous enough for the slowest untimed setup
+            # step between two collectives (the 8-rank shard generation).
+            timeout = datetime.timedelta(seconds=float(os.environ.get("BENCH_PG_TIMEOUT_S", "900")))
             if self.backend == "nccl":
-                dist.init_process_group("nccl", device_id=self.dev)
+                dist.init_process_group("nccl", device_id=self.dev, timeout=timeout)
             else:
-                dist.init_process_group(self.backend)
+                dist.init_process_group(self.backend, timeout=timeout)
         sdist.set_cpu_collectives(self.backend == "gloo")
         self.shape_world = args.sim_world if (args.sim_world and self.world == 1) else self.world
 
@@ -419,7 +432,10 @@ def time_formats(ctx, args, M, fmts, trials_head: int, y_check=None, setup_mark=
             r["traffic_over_algo"] = tb / algo
         if y_check is not None:
             torch.cuda.synchronize()
-            r.update(y_check(y))
+            own = y_check(y)["max_rel_err_vs_cpu"]
+            # every rank checks its own slice; the format's figure is the max
+            r["max_rel_err_vs_cpu"] = ctx.sdist.max_over_ranks([own], ctx.dev)[0]
+            r["own_max_rel_err_vs_cpu"] = own
         results[fmt if fmt not in results else f"{fmt}_{fi}"] = r
         if fi == 0:
             headline = (plan, info, r)
@@ -481,22 +497,35 @@ def roofline_of(config: str, M, r) -> dict:
     return out
 
 
-def extra_config(ctx, args, config: str, fmts, stream_gbs: float) -> dict:
-    """One of configs 3 / 4 beside the N = 1 headline: headline format, the
-    others beside it, roofline + PMC traffic, y against the CPU port."""
+def shard_check(M):
+    """The correctness check every timed format carries (src/main.cpp:40-56
+    verifies before timing): the oracle's opt_crs restatement (oracle/oracle.c,
+    src/opt_crs.cpp:44-70) of THIS rank's shard -- its rows, global columns,
+    the replicated x -- computed once on the host, untimed, outside every timed
+    trial.  Returns (y_check, cpu ms of the one call); y_check(y) gives
+    max_rel_err_vs_cpu of a format's y slice (relative to |y_cpu|, the
+    north star's 1e-6 measure)."""
     import oracle
-    M = build_matrix(ctx, args, config)
-    # the CPU port's y first (untimed for the GPU): every format's y is
-    # checked against it right after that format's timed trials
     x_host = M["x"].cpu().numpy()
     tc = time.perf_counter()
     y_cpu = oracle.csr_spmv(M["rp"], M["col"], M["val"], x_host)
     t_cpu = time.perf_counter() - tc
     den = np.maximum(np.abs(y_cpu), 1e-300)
+    del x_host
 
     def y_check(y):
-        return {"max_rel_err_vs_cpu": float(np.max(np.abs(y.cpu().numpy() - y_cpu) / den))}
+        return {"max_rel_err_vs_cpu": float(np.max(np.abs(y.cpu().numpy() - y_cpu) / den, initial=0.0))}
 
+    return y_check, t_cpu * 1e3
+
+
+def extra_config(ctx, args, config: str, fmts, stream_gbs: float) -> dict:
+    """One of configs 3 / 4 beside the N = 1 headline: headline format, the
+    others beside it, roofline + PMC traffic, y against the CPU port."""
+    M = build_matrix(ctx, args, config)
+    # the CPU port's y first (untimed for the GPU): every format's y is
+    # checked against it right after that format's timed trials
+    y_check, t_cpu_ms = shard_check(M)
     results, head, y_head = time_formats(ctx, args, M, fmts, trials_head=args.trials, y_check=y_check)
     if head is None:
         return {"error": "no plan could be built", "details": results}
@@ -516,7 +545,7 @@ def extra_config(ctx, args, config: str, fmts, stream_gbs: float) -> dict:
            "format": r["format"], "kernel": r["kernel"], "value": r["gflops"], "unit": "GFLOP/s",
            "ms_per_step": r["ms_per_step"], "event_ms_per_launch": r["event_ms_per_launch"],
            "roofline": roof, "max_rel_err_vs_cpu": max_rel,
-           "cpu_check": {"kind": "port", "ms_one_call": t_cpu * 1e3,
+           "cpu_check": {"kind": "port", "ms_one_call": t_cpu_ms,
                          "note": "oracle opt_crs restatement (src/opt_crs.cpp:44-70), all host threads, one call"},
            "gen_s": round(M["gen_s"], 2), "formats": results}
     if device_build is not None:
@@ -561,7 +590,11 @@ def main():
 
     fmts_arg = args.formats or ("auto,csr,ell,ss,css" if world == 1 else "auto,csr")
     fmts = [f for f in fmts_arg.split(",") if f]
-    results, headline, y_head = time_formats(ctx, args, M, fmts, args.trials, setup_mark=True)
+    # every rank's oracle y of its own shard: each format's y is checked
+    # against it after that format's timed trials, at every N
+    y_check, t_check_ms = shard_check(M)
+    progress(f"{args.config}: oracle y of this rank's shard in {t_check_ms:.0f} ms")
+    results, headline, y_head = time_formats(ctx, args, M, fmts, args.trials, y_check=y_check, setup_mark=True)
     if headline is None:
         if rank == 0:
             print(json.dumps({"error": "no plan could be built", "details": results}))
@@ -578,14 +611,16 @@ def main():
                                         float(ph.get("mul", -1.0)), float(ph.get("sum", -1.0)),
                                         su.get("setup_s", -1.0), su.get("peak_rss_gb", -1.0),
                                         su.get("device_used_gb", -1.0), su.get("plan_device_gb", -1.0),
-                                        host_rss_peak_gb(), time.time() - T_START], dev)
+                                        host_rss_peak_gb(), time.time() - T_START,
+                                        r["own_max_rel_err_vs_cpu"]], dev)
         per_rank = [{"rank": int(v[0]), "rows": [int(v[1]), int(v[2])], "nnz": int(v[3]),
                      "wall_ms_per_step": v[4], "event_ms_per_launch": v[5],
                      "phases_ms": {"mul": v[6], "sum": v[7]} if v[6] >= 0 else None,
                      "placement": info["placement"],
                      "setup_s_to_first_trial": v[8], "peak_rss_gb_at_first_trial": v[9],
                      "device_used_gb_after_build": v[10], "headline_plan_device_gb": v[11],
-                     "peak_rss_gb": v[12], "elapsed_s": v[13]} for v in rows_all]
+                     "peak_rss_gb": v[12], "elapsed_s": v[13],
+                     "max_rel_err_vs_cpu": v[14]} for v in rows_all]
 
     # y gather (RCCL all_gather over xGMI), timed separately from the kernel
     # (slices padded to the longest rank's rows)
@@ -674,18 +709,17 @@ def main():
     # (SURVEY §8(c)); it was timed beside the port in the build container
     # (profiles/round2/cpu_ref_vs_port.json).
     cpu = None
-    max_rel = None
+    # the headline's y against the oracle, max over every rank's slice
+    max_rel = r["max_rel_err_vs_cpu"]
     if rank == 0 and world == 1 and not args.no_cpu:
         import oracle
         nthreads = min(host_cores, int(os.environ.get("OMP_NUM_THREADS", host_cores)))
         x_host = x.cpu().numpy()
-        t_cpu, loop, y_cpu = cpu_time(oracle, M["rp"], M["col"], M["val"], x_host, nthreads, args.cpu_seconds)
+        t_cpu, loop, _ = cpu_time(oracle, M["rp"], M["col"], M["val"], x_host, nthreads, args.cpu_seconds)
         r1 = max(1, rows // 10)
         e1 = int(M["rp"][r1])
         t_cpu1, loop1, _ = cpu_time(oracle, M["rp"][:r1 + 1], M["col"][:e1], M["val"][:e1], x_host, 1,
                                     args.cpu_seconds)
-        ygpu = y_head.cpu().numpy()
-        max_rel = float(np.max(np.abs(ygpu - y_cpu) / np.maximum(np.abs(y_cpu), 1e-300)))
         cpu = {"value": 2.0 * nnz_local / t_cpu / 1e9, "unit": "GFLOP/s", "cores": nthreads,
                "kind": "port", "nproc": os.cpu_count(),
                "omp_proc_bind": os.environ.get("OMP_PROC_BIND"),
@@ -769,6 +803,8 @@ def main():
         "iterative": iterative,
         "host_buffers": host_mode,
         "max_rel_err_vs_cpu": max_rel,
+        "check": "every format's y, on every rank, against the oracle's opt_crs restatement of that rank's "
+                 "shard (oracle/oracle.c, src/opt_crs.cpp:44-70), after its timed trials; max over ranks",
         "verify_max_rel": verify_rel,
         "gather_ceilings_per_s": {"l2_table": gather_gps, "x_table": gather_x_gps},
     }

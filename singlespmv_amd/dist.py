@@ -62,6 +62,7 @@ def shard_csr(row_ptr, col, val, rank: int, world: int):
 
 
 _CPU_COLLECTIVES = False
+_FORCE_COLLECTIVES = False
 
 
 def set_cpu_collectives(flag: bool) -> None:
@@ -71,9 +72,18 @@ def set_cpu_collectives(flag: bool) -> None:
     _CPU_COLLECTIVES = bool(flag)
 
 
+def force_collectives(flag: bool) -> None:
+    """Test hook: issue the collectives even in a world of one rank, so a
+    one-GPU box runs the device-tensor RCCL branches (broadcast,
+    all_gather_into_tensor) that an N > 1 job takes (RCCL refuses two ranks
+    on one GPU)."""
+    global _FORCE_COLLECTIVES
+    _FORCE_COLLECTIVES = bool(flag)
+
+
 def _dist_on():
     import torch.distributed as dist
-    return dist.is_initialized() and dist.get_world_size() > 1
+    return dist.is_initialized() and (dist.get_world_size() > 1 or _FORCE_COLLECTIVES)
 
 
 def replicate_x(x, src: int = 0):
@@ -129,7 +139,7 @@ def gather_y(y_local, rows_per_rank: int):
     world * rows_per_rank; the caller trims the padding)."""
     import torch
     import torch.distributed as dist
-    if not (dist.is_initialized() and dist.get_world_size() > 1):
+    if not _dist_on():
         return y_local
     world = dist.get_world_size()
     if y_local.numel() < rows_per_rank:

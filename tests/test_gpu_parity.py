@@ -1360,7 +1360,9 @@ def test_full_size_headline_bit_exact(config):
     """BASELINE configs 2 and 3 at their full size (160 M / 29.6 M entries):
     the AUTO plan (BIN) against the oracle's opt_crs restatement -- bit for
     bit -- plus linearity A(x1 + x2) = A x1 + A x2 to fp64 rounding; at
-    config 3 also HYB, CSR, SS and CSS to 1e-12."""
+    config 2 also CSR, ELL, SS and CSS (the formats the bench line times beside
+    AUTO), at config 3 HYB, CSR, SS and CSS: 1e-12, ELL (column order) bit for
+    bit."""
     import torch
     if config == "c2":
         spec = sp.gen_spec("uniform", 10_000_000, per_row=16, seed=42)
@@ -1383,18 +1385,20 @@ def test_full_size_headline_bit_exact(config):
     lin = np.abs(outs[2] - (outs[0] + outs[1]))
     assert np.all(lin <= 1e-12 * np.abs(outs[2]) + 1e-300)
     plan.destroy()
-    if config == "c3":
-        # the named ELL + CSR hybrid and the other skew-tolerant formats at
-        # full size against the same oracle (each folds in its own fixed
-        # order: 1e-12 relative)
-        yo = oracle_y(rp, col, val, x1)
-        xd = torch.from_numpy(x1).cuda()
-        for fmt in ("hyb", "csr", "ss", "css"):
-            p2 = sp.Plan.from_csr(m, m, rp, col, val, fmt)
-            y.fill_(float("nan"))
-            p2.execute(xd, y)
-            check_close(y.cpu().numpy(), yo, what=f"c3 {fmt}")
-            p2.destroy()
+    # c3: the named ELL + CSR hybrid and the other skew-tolerant formats; c2:
+    # every format the bench line times beside AUTO -- at full size against the
+    # same oracle (each folds in its own fixed order: 1e-12 relative)
+    yo = oracle_y(rp, col, val, x1)
+    xd = torch.from_numpy(x1).cuda()
+    for fmt in (("csr", "ell", "ss", "css") if config == "c2" else ("hyb", "csr", "ss", "css")):
+        p2 = sp.Plan.from_csr(m, m, rp, col, val, fmt)
+        y.fill_(float("nan"))
+        p2.execute(xd, y)
+        if fmt == "ell":
+            assert np.array_equal(y.cpu().numpy(), yo), f"{config} {fmt}"
+        else:
+            check_close(y.cpu().numpy(), yo, what=f"{config} {fmt}")
+        p2.destroy()
 
 
 
