@@ -125,10 +125,14 @@ typedef struct spmv_options {
                                 (src/opt_crs.cpp:57-69) on the fastest layout
                                 that sums so for this matrix: DIA (AUTO's banded
                                 rule, rows strictly ascending: no duplicates),
-                                BIN with no run path (AUTO's wide-x rule),
+                                BIN with no run path (AUTO's wide-x rule, rows
+                                strictly ascending: strip order = CSR order),
                                 ELL (near-uniform rows, none > 64), else CSR with
                                 one lane per row; spmv_plan_info reports the
-                                layout.  0 = the CSR kernels as configured
+                                layout.  Bit for bit for finite x: DIA and ELL
+                                padding adds 0 * x[c], which is NaN where x[c]
+                                is Inf or NaN (opt_crs skips no entry but has
+                                no padding).  0 = the CSR kernels as configured
                                 (row groups of L lanes: butterfly sums)       */
     int32_t build;           /* plan builders (SPMV_BUILD_*): AUTO = a host CSR of
                                 >= 2^24 entries is staged into HBM and built by
@@ -300,7 +304,9 @@ int spmv_lds_order_probe(int32_t device, int32_t rounds, const int32_t *slot, co
 /* y = A * x.  x holds n doubles, y holds m doubles. */
 int spmv_execute(spmv_plan_t plan, const double *x, double *y, uint32_t flags);
 
-/* Copy the y of the last SPMV_Y_STAGED execute to host memory (m doubles). */
+/* Copy the y of the latest execute to host memory (m doubles); that execute
+ * must have been SPMV_Y_STAGED (any other execute since then makes this
+ * SPMV_ERROR_INVALID_VALUE instead of returning an older y). */
 int spmv_fetch_y(spmv_plan_t plan, double *y_host);
 
 /* y = alpha * A * x (the CSR5 handle's spmv(alpha, y),

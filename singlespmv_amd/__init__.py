@@ -484,8 +484,10 @@ class Plan:
     @classmethod
     def from_device_csr(cls, m: int, n: int, row_ptr, col, val, fmt="auto", **opts) -> "Plan":
         """Plan from torch CUDA tensors (int64 row_ptr, int32 col, float64
-        val): every format but CSS is built on the device, AUTO resolved
-        there (spmv_plan_create_csr_device); CSS stages through the host."""
+        val): every format is built on the device, AUTO resolved there
+        (spmv_plan_create_csr_device).  The one exception: BIN rows out of
+        strip order when the device has no room for their sorted copy are
+        copied to the host and built by the host builders (same layout)."""
         for name, t, dt in (("row_ptr", row_ptr, torch.int64), ("col", col, torch.int32),
                             ("val", val, torch.float64)):
             if not _is_device(t) or t.dtype != dt or not t.is_contiguous():

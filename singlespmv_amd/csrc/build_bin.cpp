@@ -647,7 +647,7 @@ static int bin_place_search(spmv_plan_s *p, int64_t n, size_t prod_bytes) {
     if (const char *e = probe_env("SPMV_BIN_PLACEMENT")) K = std::max(1, std::min(12, std::atoi(e)));
     if (K == 1) return alloc_prod_plain(p, prod_bytes);
     double *xz = nullptr;
-    SPMV_HIP_TRY(hipMalloc(&xz, sizeof(double) * (size_t)std::max<int64_t>(n, 1)));
+    SPMV_RETURN_IF(scratch_malloc(&xz, sizeof(double) * (size_t)std::max<int64_t>(n, 1), "xz"));
     if (hipMemset(xz, 0, sizeof(double) * (size_t)std::max<int64_t>(n, 1)) != hipSuccess) {
         (void)hipFree(xz);
         SPMV_HIP_TRY(hipGetLastError());

@@ -165,10 +165,10 @@ static int create_device_impl(int64_t m, int64_t n, int64_t nnz, const int64_t *
                 return census == SPMV_SUCCESS;
             },
             [&]() {
-                bool strict = false;
-                const int s2 = rows_strict_device(p, A, &strict);
+                int order = kRowsUnsorted;
+                const int s2 = rows_order_device(p, A, &order);
                 if (s2 != SPMV_SUCCESS) census = s2;
-                return strict;
+                return order;
             });
         if (census != SPMV_SUCCESS && census != kDiaRefused) st = census;
     }
@@ -492,6 +492,9 @@ static int execute_impl(spmv_plan_t p, double alpha, const double *x, double *y,
     SPMV_CHECK_ARG(!(y_staged && (flags & SPMV_Y_DEVICE)), "SPMV_Y_STAGED with SPMV_Y_DEVICE");
     SPMV_CHECK_ARG(!staged || p->x_stage != nullptr, "SPMV_X_STAGED without a previously staged x");
     SPMV_RETURN_IF(bind_device(p));
+    // spmv_fetch_y serves the y of the latest execute only when that execute
+    // was SPMV_Y_STAGED: any other execute (device y, host y) clears the mark
+    p->y_staged = false;
     const double *dx = x;
     double *dy = y;
     if (staged) {

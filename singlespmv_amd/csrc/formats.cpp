@@ -830,8 +830,8 @@ int dia_placement(spmv_plan_s *p, int64_t m, int64_t n, size_t bytes, const spmv
     if (free_b < need) return SPMV_SUCCESS;  // no room for a search
     const size_t gap = std::max<size_t>((size_t)16 << 30, (free_b - need) / (size_t)(K - 1));
     double *xz = nullptr, *yz = nullptr;
-    SPMV_HIP_TRY(hipMalloc(&xz, 8 * (size_t)std::max<int64_t>(n, 1)));
-    SPMV_HIP_TRY(hipMalloc(&yz, 8 * (size_t)std::max<int64_t>(m, 1)));
+    SPMV_RETURN_IF(scratch_malloc(&xz, 8 * (size_t)std::max<int64_t>(n, 1), "xz"));
+    SPMV_RETURN_IF(scratch_malloc(&yz, 8 * (size_t)std::max<int64_t>(m, 1), "yz"));
     SPMV_HIP_TRY(hipMemset(xz, 0, 8 * (size_t)std::max<int64_t>(n, 1)));
     hipEvent_t a, b;
     SPMV_HIP_TRY(hipEventCreate(&a));
@@ -1284,11 +1284,14 @@ int choose_crs_exact(const HostCsr &A, spmv_options_t &o) {
             return dia_offsets(A, 256, 1.25, offs);
         },
         [&]() {
-            int64_t bad = 0;
-#pragma omp parallel for schedule(static) reduction(+ : bad)
+            int64_t desc = 0, dup = 0;
+#pragma omp parallel for schedule(static) reduction(+ : desc, dup)
             for (int64_t r = 0; r < A.m; ++r)
-                for (int64_t j = A.row_ptr[r] + 1; j < A.row_ptr[r + 1]; ++j) bad += A.col[j] <= A.col[j - 1];
-            return bad == 0;
+                for (int64_t j = A.row_ptr[r] + 1; j < A.row_ptr[r + 1]; ++j) {
+                    desc += A.col[j] < A.col[j - 1];
+                    dup += A.col[j] == A.col[j - 1];
+                }
+            return desc ? kRowsUnsorted : dup ? kRowsSorted : kRowsStrict;
         });
 }
 
@@ -1298,12 +1301,15 @@ int choose_crs_exact(const HostCsr &A, spmv_options_t &o) {
 // rule holds, sliced ELL for near-uniform rows of <= 64 entries, else CSR
 // with one lane per row.  `o` is rewritten for the chosen layout.
 int choose_crs_exact(int64_t m, int64_t n, int64_t nnz, const int64_t *row_ptr, spmv_options_t &o,
-                     const std::function<bool()> &dia_ok, const std::function<bool()> &rows_strict) {
+                     const std::function<bool()> &dia_ok, const std::function<int()> &rows_order) {
     const int f = choose_format_rp(m, n, nnz, row_ptr, o, dia_ok);
     // DIA adds duplicate entries into one slot before the product: bit-exact
-    // only when every row's columns are strictly ascending
-    if (f == SPMV_FORMAT_DIA && rows_strict()) return f;
-    if (f == SPMV_FORMAT_BIN) {
+    // only when every row's columns are strictly ascending.  BIN sums a row
+    // strip by strip, each strip's entries in CSR order: the CSR order
+    // whenever the columns ascend (duplicates allowed).  Otherwise ELL /
+    // one-lane CSR below.
+    if (f == SPMV_FORMAT_DIA && rows_order() == kRowsStrict) return f;
+    if (f == SPMV_FORMAT_BIN && rows_order() != kRowsUnsorted) {
         o.bin_long_len = -1;  // every row on the segment path: sequential sums
         return f;
     }

@@ -44,6 +44,28 @@ const char *last_error();
         if (s_ != SPMV_SUCCESS) return s_;                                      \
     } while (0)
 
+// Transient device scratch of the plan builders (freed before create
+// returns): a failed allocation clears HIP's sticky error (a later launch
+// check must not see it) and reports SPMV_ERROR_OUT_OF_MEMORY, so the
+// host-CSR routing falls back to the host builders (capi.cpp) instead of
+// failing a plan the host path builds fine.
+inline int scratch_malloc_bytes(void **q, size_t n, const char *what) {
+    *q = nullptr;
+    const hipError_t e = hipMalloc(q, n ? n : 16);
+    if (e == hipSuccess) return SPMV_SUCCESS;
+    (void)hipGetLastError();
+    *q = nullptr;
+    set_error(std::string("builder scratch ") + what + " (" + std::to_string(n) + " B): " + hipGetErrorString(e));
+    return e == hipErrorOutOfMemory ? SPMV_ERROR_OUT_OF_MEMORY : SPMV_ERROR_HIP;
+}
+template <typename T>
+inline int scratch_malloc(T **q, size_t n, const char *what = "") {
+    void *v = nullptr;
+    const int s = scratch_malloc_bytes(&v, n, what);
+    *q = static_cast<T *>(v);
+    return s;
+}
+
 // ---- experiment switches ------------------------------------------------
 // The probe build (`make probes`, -DSPMV_PROBES, probes_build/) reads the
 // SPMV_<FORMAT>_* tuning and ablation variables the tools/ scripts set; the
@@ -504,7 +526,7 @@ int choose_format_rp(int64_t m, int64_t n, int64_t nnz, const int64_t *row_ptr, 
 // spmv_options_t.crs_exact: the layout for a CSR request with opt_crs semantics
 int choose_crs_exact(const HostCsr &A, spmv_options_t &o);
 int choose_crs_exact(int64_t m, int64_t n, int64_t nnz, const int64_t *row_ptr, spmv_options_t &o,
-                     const std::function<bool()> &dia_ok, const std::function<bool()> &rows_strict);
+                     const std::function<bool()> &dia_ok, const std::function<int()> &rows_order);
 // layout decisions that need the row pointers only (host and device builders)
 int ell_slice_offsets(const int64_t *row_ptr, int64_t m, int cap, const int32_t *order, std::vector<int64_t> &off);
 void ell_finish_info(spmv_plan_s *p, int maxw, int64_t total);
@@ -535,7 +557,10 @@ int css_layout(spmv_plan_s *p, const int64_t *row_ptr, int64_t m, int64_t n, int
 int css_finish(spmv_plan_s *p, const CssLayout &CL, int64_t m, int64_t n, int64_t nnz);
 int build_css_device(spmv_plan_s *p, const DevCsr &A, const spmv_options_t &o);
 // every row's columns strictly ascending (no duplicates, no disorder)?
-int rows_strict_device(spmv_plan_s *p, const DevCsr &A, bool *strict);
+// column order of a CSR's rows (choose_crs_exact): kRowsStrict = every row
+// strictly ascending, kRowsSorted = ascending with duplicates, kRowsUnsorted
+constexpr int kRowsUnsorted = 0, kRowsSorted = 1, kRowsStrict = 2;
+int rows_order_device(spmv_plan_s *p, const DevCsr &A, int *order);
 int build_ell_device(spmv_plan_s *p, const DevCsr &A, const spmv_options_t &o);
 int build_hyb_device(spmv_plan_s *p, const DevCsr &A, const spmv_options_t &o);
 int build_jds_device(spmv_plan_s *p, const DevCsr &A, const spmv_options_t &o);

@@ -61,9 +61,9 @@ int exclusive_scan(spmv_plan_s *p, const int64_t *in, int64_t *out, int64_t n, h
     if (n == 0) return SPMV_SUCCESS;
     const int64_t nb = (n + kScanBlock - 1) / kScanBlock;
     int64_t *sums, *offs;
-    SPMV_HIP_TRY(hipMalloc(&sums, sizeof(int64_t) * nb));
+    SPMV_RETURN_IF(scratch_malloc(&sums, sizeof(int64_t) * nb, "sums"));
     tmp.push_back(sums);
-    SPMV_HIP_TRY(hipMalloc(&offs, sizeof(int64_t) * nb));
+    SPMV_RETURN_IF(scratch_malloc(&offs, sizeof(int64_t) * nb, "offs"));
     tmp.push_back(offs);
     hipLaunchKernelGGL(scan_block_sums, dim3((unsigned)nb), dim3(kScanBlock), 0, st, in, n, sums);
     if (nb > 1) SPMV_RETURN_IF(exclusive_scan(p, sums, offs, nb, st, tmp));
@@ -215,7 +215,7 @@ int exclusive_scan_i64(const int64_t *in, int64_t *out, int64_t n, hipStream_t s
 
 int widen_row_ptr_device(const int32_t *d_rp32, int64_t m, int64_t **d_rp64) {
     *d_rp64 = nullptr;
-    SPMV_HIP_TRY(hipMalloc(d_rp64, 8 * (size_t)(m + 1)));
+    SPMV_RETURN_IF(scratch_malloc(d_rp64, 8 * (size_t)(m + 1), "d_rp64"));
     hipLaunchKernelGGL(rp32_to_64, dim3(grid_for(m + 1)), dim3(256), 0, 0, d_rp32, m + 1, *d_rp64);
     const hipError_t e = hipDeviceSynchronize();
     if (e != hipSuccess) {
@@ -241,7 +241,7 @@ int validate_csr_device(const int64_t *d_rp, int64_t m, const int32_t *d_col, in
     SPMV_CHECK_ARG(ends[0] == 0, "row_ptr[0] != 0");
     SPMV_CHECK_ARG(ends[1] == nnz, "row_ptr[m] != nnz");
     unsigned long long *bad, hbad[2] = {0, 0};
-    SPMV_HIP_TRY(hipMalloc(&bad, sizeof(hbad)));
+    SPMV_RETURN_IF(scratch_malloc(&bad, sizeof(hbad), "bad"));
     (void)hipMemset(bad, 0, sizeof(hbad));
     hipLaunchKernelGGL(check_csr, dim3(grid_for(std::max(m, nnz))), dim3(256), 0, 0, d_rp, m, d_col, nnz, n, bad);
     hipError_t e = hipMemcpy(hbad, bad, sizeof(hbad), hipMemcpyDeviceToHost);
@@ -331,7 +331,7 @@ int csr_x_windows_device(spmv_plan_s *p, const int64_t *d_rp) {
     const int64_t ng = (p->m + kCsrWinGroup - 1) / kCsrWinGroup;
     if (ng == 0) return SPMV_SUCCESS;
     int32_t *d = nullptr;
-    SPMV_HIP_TRY(hipMalloc(&d, 2 * sizeof(int32_t) * (size_t)ng));
+    SPMV_RETURN_IF(scratch_malloc(&d, 2 * sizeof(int32_t) * (size_t)ng, "d"));
     hipLaunchKernelGGL(csr_window_kernel, dim3((unsigned)ng), dim3(256), 0, p->stream, d_rp, p->m, p->csr.col, d,
                        d + ng);
     std::vector<int32_t> lo((size_t)ng), hi((size_t)ng);
@@ -368,9 +368,9 @@ int build_ss_device(spmv_plan_s *p, const int64_t *d_rp, const int32_t *d_col, c
     std::vector<void *> &tmp = scratch.v;
     // non-empty ordinals
     int64_t *flg = nullptr, *nzord = nullptr;
-    SPMV_HIP_TRY(hipMalloc(&flg, 8 * (size_t)std::max<int64_t>(m + 1, 1)));
+    SPMV_RETURN_IF(scratch_malloc(&flg, 8 * (size_t)std::max<int64_t>(m + 1, 1), "flg"));
     tmp.push_back(flg);
-    SPMV_HIP_TRY(hipMalloc(&nzord, 8 * (size_t)std::max<int64_t>(m + 1, 1)));
+    SPMV_RETURN_IF(scratch_malloc(&nzord, 8 * (size_t)std::max<int64_t>(m + 1, 1), "nzord"));
     tmp.push_back(nzord);
     hipLaunchKernelGGL(nonempty_flags, dim3(grid_for(m)), dim3(256), 0, st, d_rp, m, flg);
     SPMV_HIP_TRY(hipMemsetAsync(flg + m, 0, 8, st));

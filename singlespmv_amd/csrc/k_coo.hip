@@ -83,9 +83,10 @@ int launch_coo(const spmv_plan_s *p, const double *x, double *y) {
     if (p->m) SPMV_HIP_TRY(hipMemsetAsync(y, 0, sizeof(double) * (size_t)p->m, p->stream));
     phase_mark(p);  // zero_y | segment
     if (p->coo.n_units == 0) return SPMV_SUCCESS;
-    // Probe build: units per step, grid cap (workgroups of 4 waves).
-    int u = 4;
     int64_t max_blocks = INT32_MAX;  // one step per wave: short waves interleave best
+#ifdef SPMV_PROBES
+    // probe build: units per step, grid cap (workgroups of 4 waves)
+    int u = 4;
     if (const char *v = probe_env("SPMV_LAUNCH_COO_U")) u = std::atoi(v);
     if (const char *v = probe_env("SPMV_LAUNCH_COO_BLOCKS")) max_blocks = std::atoll(v);
     switch (u) {
@@ -94,6 +95,9 @@ int launch_coo(const spmv_plan_s *p, const double *x, double *y) {
         case 8: launch_coo_u<8>(p, y, x, max_blocks); break;
         default: launch_coo_u<4>(p, y, x, max_blocks);
     }
+#else
+    launch_coo_u<4>(p, y, x, max_blocks);
+#endif
     SPMV_HIP_TRY(hipGetLastError());
     return SPMV_SUCCESS;
 }

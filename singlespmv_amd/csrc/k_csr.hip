@@ -528,6 +528,7 @@ struct CsrLaunch {
     int u = 4;       // slab: steps whose loads are issued together
     size_t lds = 0;  // dynamic LDS per workgroup (caps workgroups per CU; probe)
 };
+#ifdef SPMV_PROBES
 static CsrLaunch csr_launch_shape() {
     CsrLaunch s;
     if (const char *e = probe_env("SPMV_LAUNCH_CSR")) s.slab = std::atoi(e);
@@ -535,6 +536,7 @@ static CsrLaunch csr_launch_shape() {
     if (const char *e = probe_env("SPMV_LAUNCH_CSR_LDS_KB")) s.lds = (size_t)std::atoi(e) * 1024;
     return s;
 }
+#endif
 
 template <int L, typename RP, int U>
 static void launch_slab_u(const spmv_plan_s *p, int kind, size_t lds, const double *x, double *y) {
@@ -545,9 +547,10 @@ static void launch_slab_u(const spmv_plan_s *p, int kind, size_t lds, const doub
         // S granules (64-row slabs per wave) per workgroup: kCsrSlabsPerWave;
         // probe build: SPMV_LAUNCH_CSR_S = 1, 2 or 4 where that window fits
         int S = kCsrSlabsPerWave;
+#ifdef SPMV_PROBES
         if (const char *e = probe_env("SPMV_LAUNCH_CSR_S")) S = std::atoi(e);
-        const int si = S == 4 ? 2 : S == 1 ? 0 : 1;
-        if (!c.win_s[si]) S = kCsrSlabsPerWave;
+        if (!c.win_s[S == 4 ? 2 : S == 1 ? 0 : 1]) S = kCsrSlabsPerWave;
+#endif
         const int32_t win = c.win_s[S == 4 ? 2 : S == 1 ? 0 : 1];
         const size_t wl = std::max(lds, sizeof(double) * (size_t)win);
         const unsigned grid = (unsigned)((p->m + 256 * S - 1) / (256 * S));
@@ -556,15 +559,20 @@ static void launch_slab_u(const spmv_plan_s *p, int kind, size_t lds, const doub
                                x, y, c.win0, win, p->n, c.val_halves);
         };
         // 32-bit offsets span the wave's S slabs (off32 is per single slab)
-        if (c.off32 && (S == 1 || (int64_t)S * c.slab_max + 512 < ((int64_t)1 << 28))) {
-            if (S == 1) go(csr_slabx_kernel<L, RP, UU, 1, true>);
-            else if (S == 4) go(csr_slabx_kernel<L, RP, UU, 4, true>);
-            else go(csr_slabx_kernel<L, RP, UU, 2, true>);
-        } else {
-            if (S == 1) go(csr_slabx_kernel<L, RP, UU, 1, false>);
-            else if (S == 4) go(csr_slabx_kernel<L, RP, UU, 4, false>);
-            else go(csr_slabx_kernel<L, RP, UU, 2, false>);
-        }
+        auto go_s = [&](auto sc) {
+            constexpr int SS = decltype(sc)::value;
+            if (c.off32 && (SS == 1 || (int64_t)SS * c.slab_max + 512 < ((int64_t)1 << 28)))
+                go(csr_slabx_kernel<L, RP, UU, SS, true>);
+            else
+                go(csr_slabx_kernel<L, RP, UU, SS, false>);
+        };
+#ifdef SPMV_PROBES
+        if (S == 1) go_s(std::integral_constant<int, 1>{});
+        else if (S == 4) go_s(std::integral_constant<int, 4>{});
+        else go_s(std::integral_constant<int, 2>{});
+#else
+        go_s(std::integral_constant<int, kCsrSlabsPerWave>{});
+#endif
         return;
     }
     if (p->csr.off32)
@@ -575,11 +583,15 @@ static void launch_slab_u(const spmv_plan_s *p, int kind, size_t lds, const doub
                            p->stream, p->m, (const RP *)p->csr.row_ptr, p->csr.col, p->csr.val, x, y, c.val_halves);
 }
 
+// The product instantiates only the default shape (CsrLaunch{}: slab 3, U =
+// 4, S = kCsrSlabsPerWave); the probe build adds csr_vec4 and U / S / LDS
+// variants, read at every launch.
 template <int L, typename RP>
 static int launch_csr_t(const spmv_plan_s *p, int64_t nrows, const double *x, double *y) {
     const int64_t threads = nrows * L;
     const int64_t blocks = (threads + 255) / 256;
     if (blocks == 0) return SPMV_SUCCESS;
+#ifdef SPMV_PROBES
     const CsrLaunch sh = csr_launch_shape();
     if (sh.slab) {
         switch (sh.u) {
@@ -592,6 +604,10 @@ static int launch_csr_t(const spmv_plan_s *p, int64_t nrows, const double *x, do
         hipLaunchKernelGGL((csr_vec4_kernel<L, RP>), dim3((unsigned)blocks), dim3(256), sh.lds, p->stream, nrows,
                            (const RP *)p->csr.row_ptr, p->csr.col, p->csr.val, x, y, p->csr.val_halves);
     }
+#else
+    constexpr CsrLaunch sh{};
+    launch_slab_u<L, RP, sh.u>(p, sh.slab, sh.lds, x, y);
+#endif
     SPMV_HIP_TRY(hipGetLastError());
     return SPMV_SUCCESS;
 }

@@ -193,16 +193,21 @@ __global__ __launch_bounds__(256) void overflow_copy_kernel(const int64_t *__res
     }
 }
 
-// rows whose columns are not strictly ascending (duplicates or disorder)
-__global__ __launch_bounds__(256) void rows_strict_kernel(const int64_t *__restrict__ rp,
-                                                          const int32_t *__restrict__ col, int64_t m,
-                                                          unsigned long long *__restrict__ bad) {
-    unsigned long long b = 0;
+// column order of the rows: bad[0] counts entries below their predecessor
+// (disorder), bad[1] entries equal to it (duplicates)
+__global__ __launch_bounds__(256) void rows_order_kernel(const int64_t *__restrict__ rp,
+                                                         const int32_t *__restrict__ col, int64_t m,
+                                                         unsigned long long *__restrict__ bad) {
+    unsigned long long d = 0, q = 0;
     for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < m; r += (int64_t)gridDim.x * blockDim.x) {
         const int64_t e = rp[r + 1];
-        for (int64_t j = rp[r] + 1; j < e; ++j) b += col[j] <= col[j - 1];
+        for (int64_t j = rp[r] + 1; j < e; ++j) {
+            d += col[j] < col[j - 1];
+            q += col[j] == col[j - 1];
+        }
     }
-    if (b) atomicAdd(bad, b);
+    if (d) atomicAdd(bad, d);
+    if (q) atomicAdd(bad + 1, q);
 }
 
 // ---- COO row ids -------------------------------------------------------------------
@@ -300,13 +305,13 @@ int dia_offsets_device(spmv_plan_s *p, const DevCsr &A, int max_diags, double ma
     const hipStream_t st = p->stream;
     Scratch scratch{st, {}};
     uint8_t *occ = nullptr;
-    SPMV_HIP_TRY(hipMalloc(&occ, (size_t)N));
+    SPMV_RETURN_IF(scratch_malloc(&occ, (size_t)N, "occ"));
     scratch.v.push_back(occ);
     unsigned long long *cnt = nullptr;
-    SPMV_HIP_TRY(hipMalloc(&cnt, sizeof(unsigned long long)));
+    SPMV_RETURN_IF(scratch_malloc(&cnt, sizeof(unsigned long long), "cnt"));
     scratch.v.push_back(cnt);
     int32_t *out = nullptr;
-    SPMV_HIP_TRY(hipMalloc(&out, sizeof(int32_t) * (size_t)(max_diags + 1)));
+    SPMV_RETURN_IF(scratch_malloc(&out, sizeof(int32_t) * (size_t)(max_diags + 1), "out"));
     scratch.v.push_back(out);
     SPMV_HIP_TRY(hipMemsetAsync(occ, 0, (size_t)N, st));
     SPMV_HIP_TRY(hipMemsetAsync(cnt, 0, sizeof(unsigned long long), st));
@@ -326,19 +331,19 @@ int dia_offsets_device(spmv_plan_s *p, const DevCsr &A, int max_diags, double ma
     return SPMV_SUCCESS;
 }
 
-int rows_strict_device(spmv_plan_s *p, const DevCsr &A, bool *strict) {
-    *strict = true;
+int rows_order_device(spmv_plan_s *p, const DevCsr &A, int *order) {
+    *order = kRowsStrict;
     if (A.m == 0 || A.nnz == 0) return SPMV_SUCCESS;
     Scratch scratch{p->stream, {}};
-    unsigned long long *bad = nullptr, hb = 0;
-    SPMV_HIP_TRY(hipMalloc(&bad, sizeof(unsigned long long)));
+    unsigned long long *bad = nullptr, hb[2] = {0, 0};
+    SPMV_RETURN_IF(scratch_malloc(&bad, sizeof(hb), "bad"));
     scratch.v.push_back(bad);
     SPMV_HIP_TRY(hipMemsetAsync(bad, 0, sizeof(hb), p->stream));
-    hipLaunchKernelGGL(rows_strict_kernel, dim3(grid_for(A.m)), dim3(256), 0, p->stream, A.d_rp, A.d_col, A.m, bad);
+    hipLaunchKernelGGL(rows_order_kernel, dim3(grid_for(A.m)), dim3(256), 0, p->stream, A.d_rp, A.d_col, A.m, bad);
     SPMV_HIP_TRY(hipGetLastError());
-    SPMV_HIP_TRY(hipMemcpyAsync(&hb, bad, sizeof(hb), hipMemcpyDeviceToHost, p->stream));
+    SPMV_HIP_TRY(hipMemcpyAsync(hb, bad, sizeof(hb), hipMemcpyDeviceToHost, p->stream));
     SPMV_HIP_TRY(hipStreamSynchronize(p->stream));
-    *strict = hb == 0;
+    *order = hb[0] ? kRowsUnsorted : hb[1] ? kRowsSorted : kRowsStrict;
     return SPMV_SUCCESS;
 }
 
@@ -577,7 +582,7 @@ extern "C" int spmv_plan_digest(spmv_plan_t p, uint64_t *digests, int32_t cap, i
     SPMV_HIP_TRY(hipGetDevice(&cur));
     if (cur != p->device) SPMV_HIP_TRY(hipSetDevice(p->device));
     unsigned long long *d = nullptr;
-    SPMV_HIP_TRY(hipMalloc(&d, sizeof(unsigned long long) * std::max<size_t>(a.size(), 1)));
+    SPMV_RETURN_IF(scratch_malloc(&d, sizeof(unsigned long long) * std::max<size_t>(a.size(), 1), "d"));
     hipError_t e = hipMemset(d, 0, sizeof(unsigned long long) * std::max<size_t>(a.size(), 1));
     for (size_t k = 0; k < a.size() && e == hipSuccess; ++k) {
         // logical sizes are multiples of 4 bytes (int32 / int64 / f64 arrays)

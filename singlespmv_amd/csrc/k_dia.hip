@@ -153,11 +153,14 @@ int launch_dia(const spmv_plan_s *p, const double *x, double *y) {
         SPMV_HIP_TRY(hipGetLastError());
         return SPMV_SUCCESS;
     }
-#endif
-    if (win <= kDiaMaxWin && (dbg & 2))  // probe A/B: ordinary y stores
+    if (win <= kDiaMaxWin && (dbg & 2)) {  // probe A/B: ordinary y stores
         hipLaunchKernelGGL((dia_kernel<8, true, 1>), dim3((unsigned)blocks), dim3(256), lds,
                            p->stream, p->m, d.mp, p->n, d.n_diags, d.off, off_min, (int32_t)win, d.val, x, y, d.group);
-    else if (win <= kDiaMaxWin && !(dbg & 1))
+        SPMV_HIP_TRY(hipGetLastError());
+        return SPMV_SUCCESS;
+    }
+#endif
+    if (win <= kDiaMaxWin && !(dbg & 1))
         hipLaunchKernelGGL((dia_kernel<8, true>), dim3((unsigned)blocks), dim3(256), lds,
                            p->stream, p->m, d.mp, p->n, d.n_diags, d.off, off_min, (int32_t)win, d.val, x, y, d.group);
     else

@@ -129,16 +129,21 @@ int launch_ell(const spmv_plan_s *p, const double *x, double *y) {
     // registers allow -- fewer concurrent streams, as DIA's cap (config 4,
     // same plans: 2.421-2.425 -> 2.382-2.387 ms over three plans,
     // profiles/round4/probe/c4_ell_window_variants.jsonl).
-    // Probe build: launch-time unroll / LDS request.
-    int unroll = e.unroll;
+    // The product runs 2 quads (4 slots each) per lane per iteration; the
+    // probe build adds launch-time unroll 1 / 4 and LDS-request variants.
     size_t lds = (size_t)e.slots * sizeof(double) >= kStreamVmmMinBytes ? kEllLdsKb * 1024 : 0;
+#ifdef SPMV_PROBES
+    int unroll = e.unroll;
     if (const char *v = probe_env("SPMV_LAUNCH_ELL_UNROLL")) unroll = std::atoi(v);
     if (const char *v = probe_env("SPMV_LAUNCH_ELL_LDS_KB")) lds = (size_t)std::atoi(v) * 1024;
-    switch (unroll) {  // quads (4 slots each) per lane per iteration
+    switch (unroll) {
         case 1: launch_ell_u<1>(p, x, y, lds); break;
         case 4: launch_ell_u<4>(p, x, y, lds); break;
         default: launch_ell_u<2>(p, x, y, lds);
     }
+#else
+    launch_ell_u<2>(p, x, y, lds);
+#endif
     SPMV_HIP_TRY(hipGetLastError());
     return SPMV_SUCCESS;
 }

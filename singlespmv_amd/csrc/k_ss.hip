@@ -5,7 +5,9 @@
 // wave64 design.
 //
 // The product launches ss_stream_kernel (below); ss_tile_kernel, its
-// all-loads-first twin, stays for the probe build's A/Bs (SPMV_SS_KERNEL=0).
+// all-loads-first twin, is compiled into the probe build only (`make probes`,
+// SPMV_SS_KERNEL=0), like the stream kernel's non-default PF / stage / window
+// instances.
 // The tile, common to both: one wave = 64 lanes x SIGMA nnz.  Lane l
 // owns SIGMA consecutive nnz (see SsDev layout: every wave load instruction is
 // 1 KiB contiguous -- col as 4 ints per lane, val as two 1-KiB halves of 2
@@ -91,6 +93,7 @@ __device__ __forceinline__ void ss_tile_end(int lane, int64_t tile, uint64_t bal
     if (a) *a = v;
 }
 
+#ifdef SPMV_PROBES  // round 4's kernel: probe build only (launch_ss_probe)
 template <int SIGMA, bool WIN>
 __global__ __launch_bounds__(256) void ss_tile_kernel(
     int64_t n_tiles, const int32_t *__restrict__ col, const double *__restrict__ val,
@@ -190,6 +193,7 @@ __global__ __launch_bounds__(256) void ss_tile_kernel(
     if (has && started_before) ss_store(y, nzrow, n_nonempty, ord0 - 1, tot);
     ss_tile_end(lane, tile, ball, tot, S, 0, nullptr, 0, nzrow, n_nonempty, y, ht);
 }
+#endif
 
 // ss_stream_kernel<SIGMA, WIN, PF>: the same tile, sums and hand-off as
 // ss_tile_kernel (bit-identical y), streamed: the quads of a lane are loaded
@@ -378,26 +382,27 @@ int ss_plan_tail_ord(spmv_plan_s *p) {
     return SPMV_SUCCESS;
 }
 
+#ifdef SPMV_PROBES
+// Probe build only (`make probes`): the round-4 all-loads-first kernel
+// (SPMV_LAUNCH_SS = 0 / SPMV_SS_KERNEL = 0), the other prefetch depths
+// (SPMV_LAUNCH_SS_PF 1 / 4), unstaged rows (SPMV_LAUNCH_SS_STAGE = 0), no x
+// window (SPMV_LAUNCH_SS_WIN = 0) and a dynamic-LDS cap on workgroups per CU
+// (SPMV_LAUNCH_SS_LDS_KB).  None of these instances is in the product library.
 template <int SIGMA>
-static void launch_ss_t(const spmv_plan_s *p, const double *x, double *y) {
+static void launch_ss_probe(const spmv_plan_s *p, const double *x, double *y) {
     const SsDev &s = p->ss;
     const int64_t blocks = (s.n_tiles + 3) / 4;
-    // probe build: SPMV_LAUNCH_SS = 0 -> ss_tile_kernel (all SIGMA entries
-    // loaded up front, window from the loaded columns, round 4), else the
-    // streamed kernel with SPMV_LAUNCH_SS_PF quads ahead; SPMV_LAUNCH_SS_WIN=0
-    // gathers x from memory always
     int kind = SIGMA > 32 && s.kernel == 0 ? 1 : s.kernel, pf = s.pf;
-    size_t lds = 0;  // dynamic LDS per workgroup: caps workgroups per CU (probe: SPMV_LAUNCH_SS_LDS_KB)
+    size_t lds = 0;
     bool win = true, stage = s.stage;
     if (const char *v = probe_env("SPMV_LAUNCH_SS_STAGE")) stage = std::atoi(v) != 0;
     if (const char *v = probe_env("SPMV_LAUNCH_SS_LDS_KB")) lds = (size_t)std::atoi(v) * 1024;
     if (const char *v = probe_env("SPMV_LAUNCH_SS")) kind = SIGMA > 32 && std::atoi(v) == 0 ? 1 : std::atoi(v);
     if (const char *v = probe_env("SPMV_LAUNCH_SS_PF")) pf = std::atoi(v);
     if (const char *v = probe_env("SPMV_LAUNCH_SS_WIN")) win = std::atoi(v) != 0;
-    auto go = [&](auto kern, bool stream) {
-        if (stream)
-            hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), lds, p->stream, s.n_tiles, s.col, s.val, s.flags,
-                               s.tile_ord, s.win, s.nzrow, s.n_nonempty, x, y, s.ht);
+    auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), lds, p->stream, s.n_tiles, s.col, s.val, s.flags,
+                           s.tile_ord, s.win, s.nzrow, s.n_nonempty, x, y, s.ht);
     };
     if (kind == 0 && SIGMA <= 32) {
         constexpr int S0 = SIGMA <= 32 ? SIGMA : 32;
@@ -412,14 +417,34 @@ static void launch_ss_t(const spmv_plan_s *p, const double *x, double *y) {
     win = win && s.win;
     auto pick = [&](auto pfc) {
         constexpr int P = decltype(pfc)::value;
-        if (stage) win ? go(ss_stream_kernel<SIGMA, true, P, true>, true) : go(ss_stream_kernel<SIGMA, false, P, true>, true);
-        else win ? go(ss_stream_kernel<SIGMA, true, P, false>, true) : go(ss_stream_kernel<SIGMA, false, P, false>, true);
+        if (stage) win ? go(ss_stream_kernel<SIGMA, true, P, true>) : go(ss_stream_kernel<SIGMA, false, P, true>);
+        else win ? go(ss_stream_kernel<SIGMA, true, P, false>) : go(ss_stream_kernel<SIGMA, false, P, false>);
     };
     switch (pf) {
         case 1: pick(std::integral_constant<int, 1>{}); break;
         case 4: pick(std::integral_constant<int, 4>{}); break;
         default: pick(std::integral_constant<int, 2>{});
     }
+}
+#endif
+
+// The product launch: the streamed kernel, 2 quads ahead, finished rows
+// staged in LDS, x through the plan's per-tile windows (when the plan has any)
+// -- two instances per SIGMA.
+template <int SIGMA>
+static void launch_ss_t(const spmv_plan_s *p, const double *x, double *y) {
+#ifdef SPMV_PROBES
+    launch_ss_probe<SIGMA>(p, x, y);
+#else
+    const SsDev &s = p->ss;
+    const dim3 grid((unsigned)((s.n_tiles + 3) / 4));
+    if (s.win)
+        hipLaunchKernelGGL((ss_stream_kernel<SIGMA, true, 2, true>), grid, dim3(256), 0, p->stream, s.n_tiles, s.col,
+                           s.val, s.flags, s.tile_ord, s.win, s.nzrow, s.n_nonempty, x, y, s.ht);
+    else
+        hipLaunchKernelGGL((ss_stream_kernel<SIGMA, false, 2, true>), grid, dim3(256), 0, p->stream, s.n_tiles, s.col,
+                           s.val, s.flags, s.tile_ord, s.win, s.nzrow, s.n_nonempty, x, y, s.ht);
+#endif
 }
 
 int launch_ss(const spmv_plan_s *p, const double *x, double *y) {

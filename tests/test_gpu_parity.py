@@ -1553,3 +1553,94 @@ def test_graph_replays_the_execute(fmt):
     css = sp.Plan.from_csr(m, m, rp, col, val, "css")
     with pytest.raises(sp.SpmvError, match="not supported"):
         css.graph(xd, yg)
+
+
+def test_device_build_oom_falls_back_to_host_builders():
+    """A host CSR of >= 2^24 entries is staged into HBM and built there (build
+    AUTO); when the device builders' own scratch does not fit, the plan must
+    still come from the host builders (status OUT_OF_MEMORY -> host route,
+    HIP's sticky error cleared), never fail with a HIP error.  HBM is filled
+    with a blocker so that only the staging copy plus a small margin stays
+    free; the margins sweep across the SS builder's scratch (16 B per row)."""
+    import torch
+    spec = sp.gen_spec("uniform", 1_100_000, per_row=16, seed=21)
+    rp, col, val = sp.generate_csr(spec)
+    m, nnz = len(rp) - 1, int(rp[-1])
+    assert nnz >= 1 << 24  # the AUTO build routes this host CSR through the device builders
+    x = sp.generate_vector(m, seed=22)
+    yo = oracle_y(rp, col, val, x)
+    staging = 8 * (m + 1) + 12 * nnz
+    outcomes, host_built = [], False
+    for margin_mb in (4, 12, 20, 28, 40, 64, 128):
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        free, _ = torch.cuda.mem_get_info()
+        blocker = torch.empty(free - staging - (margin_mb << 20), dtype=torch.uint8, device="cuda")
+        try:
+            p = sp.Plan.from_csr(m, m, rp, col, val, "ss")
+        except sp.SpmvError as e:  # the host plan may not fit either: then the error must say so
+            assert "out of memory" in str(e), f"margin {margin_mb} MB: {e}"
+            outcomes.append((margin_mb, "oom"))
+            continue
+        finally:
+            del blocker
+            torch.cuda.empty_cache()
+        on_dev = p.built_on_device()
+        outcomes.append((margin_mb, "device" if on_dev else "host"))
+        y = np.full(m, np.nan)
+        p.execute(x, y)
+        check_close(y, yo, what=f"ss, margin {margin_mb} MB, built on {'device' if on_dev else 'host'}")
+        p.destroy()
+        host_built |= not on_dev
+        if on_dev:  # the scratch fits from here on
+            break
+    print("device-build OOM sweep:", outcomes)
+    assert host_built, f"no margin exercised the host fallback: {outcomes}"
+
+
+def test_fetch_y_serves_only_the_latest_staged_execute():
+    """spmv_fetch_y returns the y of the latest execute when that execute was
+    SPMV_Y_STAGED; after any other execute it refuses instead of handing back
+    an older y."""
+    import torch
+    m = 20_000
+    rp, col, val = sp.generate_csr(sp.gen_spec("uniform", m, per_row=8, seed=3))
+    x = sp.generate_vector(m, seed=4)
+    p = sp.Plan.from_csr(m, m, rp, col, val, "csr")
+    L = sp.lib()
+    y = np.full(m, np.nan)
+    assert L.spmv_execute(p._h, x.ctypes.data, None, sp.Y_STAGED) == 0
+    assert L.spmv_fetch_y(p._h, y.ctypes.data) == 0
+    check_close(y, oracle_y(rp, col, val, x))
+    yd = torch.empty(m, dtype=torch.float64, device="cuda")
+    p.execute(torch.from_numpy(x).cuda(), yd)  # device y: the staged y is no longer the latest
+    assert L.spmv_fetch_y(p._h, y.ctypes.data) == 1  # SPMV_ERROR_INVALID_VALUE
+    yh = np.empty(m)
+    p.execute(x, yh)  # host y (staging buffer + D2H): not a staged execute either
+    assert L.spmv_fetch_y(p._h, y.ctypes.data) == 1
+    assert L.spmv_execute(p._h, x.ctypes.data, None, sp.Y_STAGED) == 0
+    assert L.spmv_fetch_y(p._h, y.ctypes.data) == 0 and np.array_equal(y, yh)
+    p.destroy()
+
+
+def test_crs_exact_skips_bin_for_rows_out_of_column_order():
+    """crs_exact promises the sequential column-order sum bit for bit: BIN
+    sums a row strip by strip, so a matrix whose rows are not strictly
+    ascending (here every 7th row reversed, which AUTO would still route to
+    BIN) must get a layout that sums in CSR order (ELL at 16 per row), and y
+    must equal the oracle's opt_crs restatement bit for bit."""
+    m = 1_000_000
+    rp, col, val = sp.generate_csr(sp.gen_spec("uniform", m, per_row=16, seed=31))
+    col = col.copy()
+    for r in range(0, m, 7):
+        col[rp[r]:rp[r + 1]] = col[rp[r]:rp[r + 1]][::-1]
+    x = sp.generate_vector(m, seed=32)
+    pa = sp.Plan.from_csr(m, m, rp, col, val, "auto")
+    assert pa.info()["format"] == "bin"
+    pa.destroy()
+    p = sp.Plan.from_csr(m, m, rp, col, val, "csr", crs_exact=True)
+    assert p.info()["format"] in ("ell", "csr"), p.info()["format"]
+    y = np.full(m, np.nan)
+    p.execute(x, y)
+    assert np.array_equal(y, oracle_y(rp, col, val, x))
+    p.destroy()
