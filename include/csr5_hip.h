@@ -19,7 +19,8 @@
  *    asCSR/destroy (anonymouslib_cuda.h:203-204, 286-291);
  *  - spmv overwrites y (beta = 0) and repeated calls are identical
  *    (CSR5 is not);
- *  - sigma is rounded to the SS kernel's supported set {4,8,...,24,32}.
+ *  - sigma is rounded to the SS kernel's supported set {4,8,...,24,32,48,64}
+ *    (the benchmark's auto rule picks at most 32; 48 / 64 by setSigma).
  * Only <int, unsigned int, double> is instantiable (fp64 engine). */
 #ifndef CSR5_HIP_H
 #define CSR5_HIP_H
@@ -122,12 +123,14 @@ public:
     spmv_plan_t plan() const { return _plan; }
 
 private:
+    /* the SS kernel's sigma set {4,8,...,24,32,48,64}: the nearest member
+     * (ties upward); an explicit setSigma beyond 64 takes 64 */
     static int supported_sigma(int s) {
-        if (s <= 4) return 4;
-        if (s >= 30) return 32;
-        int r = (s + 2) / 4 * 4;  // nearest multiple of 4
-        if (r == 28) r = s < 28 ? 24 : 32;
-        return r;
+        static const int kSet[] = {4, 8, 12, 16, 20, 24, 32, 48, 64};
+        int best = kSet[0];
+        for (int c : kSet)
+            if ((c > s ? c - s : s - c) <= (best > s ? best - s : s - best)) best = c;
+        return best;
     }
     void drop() {
         if (_plan) spmv_plan_destroy(_plan);

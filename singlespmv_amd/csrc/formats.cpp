@@ -516,15 +516,14 @@ static int build_overflow(spmv_plan_s *p, const HostCsr &A, int K) {
 }
 
 // ---------------------------------------------------------------- JDS
-// opt_jds (src/opt_jds.cpp:29-71, 75-104): rows sorted by length (stable,
-// longest first), jagged diagonals = sliced ELL over the sorted rows, y
-// written back through the permutation.  Jagged diagonals are capped at K
-// (default max(64, 4 x mean row length)); the entries of longer rows beyond K
-// are finished by the overflow kernel, so the longest-row slices do not run
-// as single waves.  Rows of length <= K are the sequential sum, bit for bit.
-// JDS row order (rows by decreasing length, stable -- std::stable_sort's
-// order, by a counting sort over the lengths) and the jagged-diagonal cap K
-// (default max(64, 4 x mean row length)).  Returns true when the order is the
+// opt_jds (src/opt_jds.cpp:29-71, 75-104): rows sorted by decreasing length
+// (stable -- std::stable_sort's order, by a counting sort over the lengths),
+// jagged diagonals = sliced ELL over the sorted rows, y written back through
+// the permutation.  Jagged diagonals are capped at K (default max(64, 4 x mean
+// row length)); the entries of longer rows beyond K are finished by the
+// overflow kernel, so the longest-row slices do not run as single waves.
+// Rows of length <= K are the sequential sum, bit for bit.
+// jds_layout: that row order and K.  Returns true when the order is the
 // identity (rows already in non-increasing length order, config 4): the
 // slices then store rows in matrix order and the kernel writes y directly (no
 // perm[] load, coalesced y).

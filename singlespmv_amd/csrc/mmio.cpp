@@ -7,8 +7,10 @@
 // whitespace-separated triplets are read token by token, whatever the line
 // structure (:44-50) -- extra trailing entries are ignored (matrix/test/10x10
 // declares 27 of its 28 triplets); indices become 0-based; entries are sorted
-// row-major by (row, col) with duplicates kept, equal keys in file order
-// (:51 uses std::sort; the stable order makes the result deterministic).
+// row-major by (row, col) with duplicates kept.  Equal keys come out in the
+// order the reference's own std::sort (:51, not stable) leaves them: runs of
+// duplicates are re-sorted with std::sort on the reference's comparator
+// (below), pinned by the golden mtx_dups fixture.
 // Values are parsed with strtod (correctly rounded, as the stream extraction
 // of the reference).  Unlike the reference, a truncated file or an index
 // outside the declared shape is an error, not undefined behaviour.

@@ -894,19 +894,22 @@ def test_profile_phases():
         check_close(y.cpu().numpy(), yo, what=f"profile {fmt}")
 
 
-@pytest.mark.parametrize("args", [[], ["-", "1.0", "16"], ["-", "-0.5", "7"],
+@pytest.mark.parametrize("args", [[], ["-", "1.0", "16"], ["-", "-0.5", "7"], ["-", "1.0", "40"], ["-", "2.0", "64"],
                                   [os.path.join(os.path.dirname(__file__), "golden", "mtx", "random.mtx")]])
 def test_csr5_handle_api(args):
     """include/csr5_hip.h: the CSR5 benchmark's anonymouslibHandle flow
     (CSR5_cuda/main.cu call_anonymouslib) -- refuses spmv in CSR mode,
     y = alpha*A*x within 1e-10 of the benchmark's own check, identical on
-    repeated calls, caller's arrays untouched."""
+    repeated calls, caller's arrays untouched; an explicit setSigma takes the
+    nearest sigma of the SS kernel's set (7 -> 8, 40 -> 48, 64 -> 64)."""
     import subprocess
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     out = subprocess.run([os.path.join(root, "bin", "csr5_api")] + args, capture_output=True, text=True,
                          timeout=300)
     assert out.returncode == 0, out.stdout + out.stderr
     assert "-> OK" in out.stdout
+    if len(args) == 3:
+        assert f"sigma={ {'16': 16, '7': 8, '40': 48, '64': 64}[args[2]] } " in out.stdout, out.stdout
 
 
 def test_execute_alpha():
