@@ -238,3 +238,27 @@ def test_host_code_under_asan_ubsan():
                          env=env, capture_output=True, text=True, timeout=900, cwd=ROOT)
     assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
     assert "passed" in out.stdout
+
+
+def test_bench_shard_check_flags_a_wrong_slice():
+    """bench.shard_check: the oracle's opt_crs y of a rank's shard (its rows,
+    global columns, the replicated x) -- exact y scores 0, a y off in one
+    entry by 1e-9 relative scores ~1e-9, so every bench line's
+    max_rel_err_vs_cpu would expose a wrong slice (no GPU needed: CPU
+    tensors stand in for the device ones)."""
+    import bench
+    import oracle
+    spec = sp.gen_spec("powerlaw", 4000, 6000, max_len=300, seed=5)
+    rp, col, val = sp.generate_csr(spec, 1000, 2500)  # rows [1000, 2500) of a 4000 x 6000 matrix
+    x = torch.from_numpy(sp.generate_vector(6000, seed=6))
+    M = {"rp": rp, "col": col, "val": val, "x": x}
+    y_check, ms = bench.shard_check(M)
+    assert ms >= 0
+    yo = oracle.csr_spmv(rp, col, val, x.numpy())
+    assert len(yo) == 1500
+    assert y_check(torch.from_numpy(yo.copy()))["max_rel_err_vs_cpu"] == 0.0
+    bad = yo.copy()
+    k = int(np.argmax(np.abs(bad)))
+    bad[k] *= 1 + 1e-9
+    err = y_check(torch.from_numpy(bad))["max_rel_err_vs_cpu"]
+    assert 5e-10 < err < 2e-9
