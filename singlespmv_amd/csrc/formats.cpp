@@ -828,13 +828,25 @@ int dia_placement(spmv_plan_s *p, int64_t m, int64_t n, size_t bytes, const spmv
     const size_t need = need_for(K);
     if (free_b < need) return SPMV_SUCCESS;  // no room for a search
     const size_t gap = std::max<size_t>((size_t)16 << 30, (free_b - need) / (size_t)(K - 1));
-    double *xz = nullptr, *yz = nullptr;
-    SPMV_RETURN_IF(scratch_malloc(&xz, 8 * (size_t)std::max<int64_t>(n, 1), "xz"));
-    SPMV_RETURN_IF(scratch_malloc(&yz, 8 * (size_t)std::max<int64_t>(m, 1), "yz"));
+    // the search's scratch (zero x, a y, two events), released on every exit
+    struct SearchScratch {
+        double *xz = nullptr, *yz = nullptr;
+        hipEvent_t a = nullptr, b = nullptr;
+        ~SearchScratch() {
+            (void)hipDeviceSynchronize();
+            if (xz) (void)hipFree(xz);
+            if (yz) (void)hipFree(yz);
+            if (a) (void)hipEventDestroy(a);
+            if (b) (void)hipEventDestroy(b);
+        }
+    } sc;
+    SPMV_RETURN_IF(scratch_malloc(&sc.xz, 8 * (size_t)std::max<int64_t>(n, 1), "xz"));
+    SPMV_RETURN_IF(scratch_malloc(&sc.yz, 8 * (size_t)std::max<int64_t>(m, 1), "yz"));
+    double *xz = sc.xz, *yz = sc.yz;
     SPMV_HIP_TRY(hipMemset(xz, 0, 8 * (size_t)std::max<int64_t>(n, 1)));
-    hipEvent_t a, b;
-    SPMV_HIP_TRY(hipEventCreate(&a));
-    SPMV_HIP_TRY(hipEventCreate(&b));
+    SPMV_HIP_TRY(hipEventCreate(&sc.a));
+    SPMV_HIP_TRY(hipEventCreate(&sc.b));
+    hipEvent_t a = sc.a, b = sc.b;
     auto time_one = [&](float *ms) -> int {
         SPMV_RETURN_IF(launch_dia(p, xz, yz));  // warm
         SPMV_HIP_TRY(hipEventRecord(a, p->stream));
@@ -872,10 +884,6 @@ int dia_placement(spmv_plan_s *p, int64_t m, int64_t n, size_t bytes, const spmv
         if (k >= 3 && *std::min_element(t.begin(), t.end()) < 0.93f * *std::max_element(t.begin(), t.end())) break;
     }
     for (void *g : spacers) (void)hipFree(g);
-    (void)hipFree(xz);
-    (void)hipFree(yz);
-    (void)hipEventDestroy(a);
-    (void)hipEventDestroy(b);
     (void)hipGetLastError();
     const size_t best = st == SPMV_SUCCESS ? (size_t)(std::min_element(t.begin(), t.end()) - t.begin()) : 0;
     for (size_t k = 0; k < cand.size(); ++k)
