@@ -648,9 +648,11 @@ static int bin_place_search(spmv_plan_s *p, int64_t n, size_t prod_bytes) {
     if (K == 1) return alloc_prod_plain(p, prod_bytes);
     double *xz = nullptr;
     SPMV_RETURN_IF(scratch_malloc(&xz, sizeof(double) * (size_t)std::max<int64_t>(n, 1), "xz"));
-    if (hipMemset(xz, 0, sizeof(double) * (size_t)std::max<int64_t>(n, 1)) != hipSuccess) {
+    if (const hipError_t e = hipMemset(xz, 0, sizeof(double) * (size_t)std::max<int64_t>(n, 1)); e != hipSuccess) {
+        (void)hipGetLastError();
         (void)hipFree(xz);
-        SPMV_HIP_TRY(hipGetLastError());
+        set_error(std::string("BIN placement search: ") + hipGetErrorString(e));
+        return SPMV_ERROR_HIP;
     }
     std::vector<double *> cand;
     std::vector<float> t;
